@@ -1,0 +1,216 @@
+"""bench.py -- STFT frames/s of the MI355X engine on BASELINE.json's multi-GPU workload.
+
+Workload ("C4 per-GPU shard", BASELINE.json configs[3]): every rank owns 1000 synthetic
+48 kHz 30 s stereo tracks (int16-quantised chirp + noise, stored as interleaved f32 -- the
+reference's in-memory format after open_audio_file, audio.rs:9-37), resident in HBM before
+timing. One step = one pass of the hot path over the rank's whole shard: channel-sum
+downmix (lib.rs:42) -> reflect framing + Hann/n_fft (lib.rs:367-440) -> real FFT
+(realfft.rs) -> |X| (lib.rs:124) -> 128-band mel MFMA projection (lib.rs:131) -> amp dB
+(decibel.rs:79-88), n_fft 2048 / hop 512 / win 2048, one kernel launch. Files shard across
+ranks with no data-path collective ("weak" scaling: per-GPU work is fixed).
+
+Launch: python bench.py [--gpus N --steps K --warmup W]; for N > 1 under
+torch.distributed.run (one rank per GPU; gloo is used only for the timing barrier / max).
+Prints ONE JSON line on rank 0.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "multi-spectrogram-viewer_amd"))
+
+import numpy as np  # noqa: E402
+
+import thesia  # noqa: E402  (loads libthesia before torch: one HIP runtime in the process)
+from thesia import engine  # noqa: E402
+
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s HBM3E (spec)
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=20)
+    p.add_argument("--warmup", type=int, default=3)
+    p.add_argument("--tracks", type=int, default=1000, help="tracks per GPU")
+    p.add_argument("--seconds", type=float, default=30.0)
+    p.add_argument("--sr", type=int, default=48000)
+    p.add_argument("--channels", type=int, default=2)
+    p.add_argument("--input", choices=["f32", "s16"], default="f32")
+    p.add_argument("--n-fft", type=int, default=2048)
+    p.add_argument("--hop", type=int, default=512)
+    p.add_argument("--n-mels", type=int, default=128)
+    p.add_argument("--output", choices=["mel_db", "amp_db", "power_db", "complex"], default="mel_db")
+    p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--cpu-workers", type=int, default=16)
+    return p.parse_args()
+
+
+def dist_setup(args):
+    ws = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    pg = None
+    if ws > 1:
+        import torch.distributed as dist
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        dist.init_process_group("gloo", rank=rank, world_size=ws)
+        pg = dist
+    return ws, rank, local, pg
+
+
+def barrier(pg):
+    if pg is not None:
+        pg.barrier()
+
+
+def max_over_ranks(pg, v: float) -> float:
+    if pg is None:
+        return v
+    import torch
+    t = torch.tensor([v], dtype=torch.float64)
+    pg.all_reduce(t, op=pg.ReduceOp.MAX)
+    return float(t.item())
+
+
+def algorithmic_bytes(args, n_samples, total_frames, row_bins):
+    in_el = 4 if args.input == "f32" else 2
+    out_el = 8 if args.output == "complex" else 4
+    return args.tracks * n_samples * args.channels * in_el + total_frames * row_bins * out_el
+
+
+def cpu_baseline(args, n_samples):
+    """The oracle (oracle/thesia_oracle.c, a C restatement of the reference path) on a
+    bounded sample of the same workload: per-track parallel with one plan per track, like
+    the reference's rayon path (lib.rs:161-166)."""
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import oracle_ffi as O
+    from concurrent.futures import ThreadPoolExecutor
+
+    workers = max(1, min(args.cpu_workers, os.cpu_count() or 1))
+    n_tracks = 2 * workers
+    fb = O.calc_mel_fb(args.sr, args.n_fft, args.n_mels)
+    pcm = [engine.synth_pcm_host(args.channels, i, n_samples, args.sr).astype(np.float32) / 32768.0
+           for i in range(n_tracks)]
+
+    def one(x):
+        mono = np.zeros(x.shape[0], np.float32)
+        for c in range(x.shape[1]):
+            mono = (mono + x[:, c]).astype(np.float32)
+        X = O.perform_stft(mono, args.n_fft, args.hop, args.n_fft)
+        db = O.amp_to_db_default(O.dot(O.norm(X), fb))
+        return db.shape[0]
+
+    t0 = time.perf_counter()
+    with ThreadPoolExecutor(workers) as ex:
+        frames = sum(ex.map(one, pcm))
+    dt = time.perf_counter() - t0
+    return {"value": frames / dt, "unit": "frames/s", "cores": workers, "kind": "port",
+            "sample": f"{n_tracks} tracks x {args.seconds:g} s x {args.channels} ch @ {args.sr} Hz "
+                      f"({frames} frames, {dt:.2f} s wall) through the C oracle, {workers} threads"}
+
+
+def traffic_from_profile(workload_key):
+    path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    try:
+        with open(path) as f:
+            d = json.load(f)
+        rec = d.get(workload_key)
+        return None if rec is None else rec.get("hbm_bytes_per_launch")
+    except (OSError, ValueError):
+        return None
+
+
+def main():
+    args = parse()
+    ws, rank, local, pg = dist_setup(args)
+    engine.set_device(local)
+    n_samples = int(round(args.seconds * args.sr))
+    kind = {"mel_db": engine.OUT_MEL_AMP_DB, "amp_db": engine.OUT_AMP_DB,
+            "power_db": engine.OUT_POWER_DB, "complex": engine.OUT_COMPLEX}[args.output]
+    fmt = engine.IN_F32 if args.input == "f32" else engine.IN_S16
+    plan = engine.Plan(args.n_fft, args.n_fft, args.hop, kind, sr=args.sr,
+                       n_mels=args.n_mels if kind == engine.OUT_MEL_AMP_DB else 0)
+    el = 4 if fmt == engine.IN_F32 else 2
+    per_track = n_samples * args.channels
+    din = engine.DeviceBuffer(args.tracks * per_track * el)
+    # distinct tracks per rank: the generator is seeded by the global track index
+    engine.synth_pcm_device(din, fmt, args.channels, args.tracks, n_samples, args.sr, seed=rank)
+    offs = np.arange(args.tracks, dtype=np.uint64) * per_track
+    lens = np.full(args.tracks, n_samples, np.uint64)
+    frames = engine.Batch.frames_for(plan, lens)
+    dout = engine.DeviceBuffer(frames * plan.row_bins * (8 if kind == engine.OUT_COMPLEX else 4))
+    batch = engine.Batch(plan, din, offs, lens, dout, input_format=fmt, channels=args.channels)
+    assert batch.total_frames == frames
+
+    for _ in range(args.warmup):
+        batch.run()
+    engine.synchronize()
+    barrier(pg)
+    engine.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        batch.run()
+    engine.synchronize()
+    barrier(pg)
+    t1 = time.perf_counter()
+    dt = max_over_ranks(pg, (t1 - t0) / args.steps)
+
+    # kernel duration from HIP events on the launch stream (roofline numerator / denominator)
+    kms = batch.run_timed(max(args.steps, 5)) / max(args.steps, 5)
+    kms = max_over_ranks(pg, kms)
+    abytes = algorithmic_bytes(args, n_samples, frames, plan.row_bins)
+    achieved = abytes / (kms * 1e-3) / 1e9
+
+    total_frames_all = frames * ws
+    result = {
+        "metric": "STFT frames/sec (n_fft=2048 hop=512) at 1/2/4/8 GPUs; % HBM roofline",
+        "value": total_frames_all / dt,
+        "unit": "frames/s",
+        "n_gpus": ws,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": dt * 1e3,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f32",
+        "data": "synthetic (int16-quantised chirp + noise, seeded per track), resident in HBM",
+        "config": {
+            "workload": f"C4 per-GPU shard: {args.tracks} x {args.sr/1000:g} kHz {args.seconds:g} s "
+                        f"{'stereo' if args.channels == 2 else str(args.channels) + '-ch'} tracks per GPU "
+                        f"({args.input} interleaved), n_fft {args.n_fft} hop {args.hop} Hann, "
+                        f"sum-downmix, {'mel-' + str(args.n_mels) + ' + amp dB' if kind == engine.OUT_MEL_AMP_DB else args.output}",
+            "tracks_per_gpu": args.tracks,
+            "frames_per_gpu": frames,
+            "parallelism": f"file-sharded x{ws}, no collective",
+        },
+    }
+    if rank == 0:
+        wkey = f"{args.output}_{args.input}_{args.channels}ch_{args.n_fft}_{args.hop}"
+        result["roofline"] = {
+            "bound": "hbm",
+            "achieved": achieved,
+            "peak": HBM_PEAK_GBS,
+            "unit": "GB/s",
+            "frac": achieved / HBM_PEAK_GBS,
+            "traffic": traffic_from_profile(wkey),
+            "kernel": "thesia::stft_kernel (fused downmix+frame+window+rFFT+|X|+mel MFMA+dB)",
+            "kernel_ms": kms,
+            "algorithmic_bytes_per_launch": abytes,
+        }
+        if ws == 1 and not args.no_cpu_baseline:
+            result["cpu_baseline"] = cpu_baseline(args, n_samples)
+        print(json.dumps(result), flush=True)
+    batch.close()
+    if pg is not None:
+        pg.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

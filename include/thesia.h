@@ -1,0 +1,233 @@
+/*
+ * thesia.h -- C ABI of libthesia, the MI355X-native spectrogram engine.
+ *
+ * Drop-in boundary for the reference's wasm-bindgen surface (src_rust/lib.rs:72-365,
+ * 473-480) and its Rust-level pub API used by benches/bench.rs (perform_stft, decibel,
+ * mel, windows, display). Every entry point cites the reference item it replaces.
+ *
+ * Conventions:
+ *   - every function returns int status (THESIA_OK = 0) unless it cannot fail;
+ *   - the reference panics (unwrap / assert) where this ABI returns an error code and sets
+ *     a thread-local message readable with thesia_last_error(); nothing aborts across FFI;
+ *   - outputs are caller-allocated; variable-size outputs take (out, cap, needed) and
+ *     return THESIA_ERR_BUFFER_TOO_SMALL with *needed set when cap is short (out may be
+ *     NULL for a size query);
+ *   - a handle is not thread-safe (mirrors &mut self); distinct handles are independent;
+ *   - "device" pointers are HBM pointers on the calling thread's current device
+ *     (thesia_set_device); host pointers are plain process memory.
+ */
+#ifndef THESIA_H
+#define THESIA_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define THESIA_OK 0
+#define THESIA_ERR_INVALID_ARG -1
+#define THESIA_ERR_IO -2           /* add_tracks Err(io::Error) -> JsValue string, lib.rs:176 */
+#define THESIA_ERR_UNKNOWN_ID -3   /* reference: unwrap() panic on a missing id, lib.rs:113,266,295 */
+#define THESIA_ERR_TOO_SHORT -4    /* reference: slice panic for n < win-1, lib.rs:413 */
+#define THESIA_ERR_UNSUPPORTED -5
+#define THESIA_ERR_DEVICE -6
+#define THESIA_ERR_BUFFER_TOO_SMALL -7
+#define THESIA_ERR_NEGATIVE -8     /* reference: assert!(x >= 0) in log_for_db, decibel.rs:34 */
+
+const char* thesia_last_error(void);
+const char* thesia_version(void);
+
+/* ---------------------------------------------------------------------------------- */
+/* runtime / device memory (plumbing for callers that keep data resident in HBM)       */
+/* ---------------------------------------------------------------------------------- */
+int thesia_device_count(int* n);
+int thesia_set_device(int device);
+int thesia_get_device(int* device);
+int thesia_device_malloc(void** ptr, size_t bytes);
+int thesia_device_free(void* ptr);
+int thesia_memcpy_h2d(void* dst_device, const void* src_host, size_t bytes);
+int thesia_memcpy_d2h(void* dst_host, const void* src_device, size_t bytes);
+int thesia_memset_device(void* dst_device, int value, size_t bytes);
+int thesia_device_synchronize(void);
+/* Device name / CU count of the current device (for reports). */
+int thesia_device_info(char* name, size_t cap, int* n_cu);
+
+/* ---------------------------------------------------------------------------------- */
+/* host tables (bit-exact f32 restatements; computed with the same libm the reference  */
+/* calls on Linux)                                                                     */
+/* ---------------------------------------------------------------------------------- */
+/* windows::hann(size, symmetric) -- windows.rs:21-30 */
+int thesia_hann(size_t size, int symmetric, float* out);
+/* utils::calc_proper_n_fft -- utils.rs:17-19 */
+size_t thesia_calc_proper_n_fft(size_t win_length);
+/* mel::hz_to_mel / mel_to_hz (f32) -- mel.rs:13-31 */
+float thesia_hz_to_mel(float hz);
+float thesia_mel_to_hz(float mel);
+/* mel::calc_mel_fb(sr, n_fft, n_mel, fmin, fmax, do_norm) -- mel.rs:33-85.
+ * fmax < 0 means None (Nyquist). out: [n_fft/2+1, n_mel] row-major f32. */
+int thesia_calc_mel_fb(uint32_t sr, size_t n_fft, size_t n_mel, float fmin, float fmax,
+                       int do_norm, float* out);
+/* mel::calc_mel_fb_default(sr, n_fft) -- mel.rs:87-99. Writes n_mel; out may be NULL
+ * (query) else needs (n_fft/2+1) * n_mel floats. */
+int thesia_calc_mel_fb_default(uint32_t sr, size_t n_fft, size_t* n_mel, float* out,
+                               size_t cap_floats);
+/* get_colormap() -- lib.rs:473-480: the 10 inferno stops as 30 RGB bytes. */
+void thesia_get_colormap(uint8_t out[30]);
+/* AudioTrack::new parameter derivation -- lib.rs:43-46 */
+int thesia_track_params(uint32_t sr, float win_ms, size_t t_overlap, size_t f_overlap,
+                        size_t* win_length, size_t* hop_length, size_t* n_fft);
+
+/* ---------------------------------------------------------------------------------- */
+/* perform_stft -- lib.rs:388-471 (host buffers in / out; runs on the device)          */
+/* ---------------------------------------------------------------------------------- */
+/* Frame count the reference yields for (n, win, hop); 0 where it panics. */
+size_t thesia_stft_n_frames(size_t n, size_t win_length, size_t hop_length);
+/* X[T, n_fft/2+1] complex64 interleaved (re, im). window may be NULL (hann/n_fft,
+ * lib.rs:407) else has win_length values (lib.rs:404 asserts the length). The `parallel`
+ * flag of the reference changes nothing numerically and is not needed. */
+int thesia_perform_stft(const float* input, size_t n, size_t win_length, size_t hop_length,
+                        size_t n_fft, const float* window, float* out, size_t out_cap_frames,
+                        size_t* n_frames);
+
+/* ---------------------------------------------------------------------------------- */
+/* batch engine: many tracks, one plan, one launch (the MI355X-native hot path)         */
+/* ---------------------------------------------------------------------------------- */
+typedef enum {
+    THESIA_OUT_COMPLEX = 0,    /* perform_stft output, lib.rs:436 */
+    THESIA_OUT_MAG = 1,        /* stft.mapv(|x| x.norm()), lib.rs:124 */
+    THESIA_OUT_POWER = 2,      /* x.norm_sqr() */
+    THESIA_OUT_AMP_DB = 3,     /* FreqScale::Linear: amp_to_db_default, lib.rs:126-129 */
+    THESIA_OUT_POWER_DB = 4,   /* power_to_db_default(|X|^2), decibel.rs:91-100 */
+    THESIA_OUT_MEL = 5,        /* linspec.dot(mel_fb), lib.rs:131 */
+    THESIA_OUT_MEL_AMP_DB = 6  /* FreqScale::Mel: dot then amp_to_db_default, lib.rs:130-134 */
+} thesia_output;
+
+typedef enum {
+    THESIA_IN_F32 = 0,  /* f32, channel-interleaved (audio.rs:33-35 [ch, n] view) */
+    THESIA_IN_S16 = 1   /* s16 PCM, channel-interleaved, value / 32768 (audio.rs:16-19) */
+} thesia_input_format;
+
+typedef struct thesia_plan_desc {
+    uint32_t sr;            /* sample rate (mel filterbank) */
+    size_t win_length;
+    size_t hop_length;
+    size_t n_fft;           /* power of two, 2..4096 */
+    const float* window;    /* NULL => hann(win, false) / n_fft (lib.rs:138-140) */
+    int output;             /* thesia_output */
+    size_t n_mels;          /* mel outputs: 0 => calc_mel_fb_default (mel.rs:87-99) */
+    float fmin;             /* mel fmin (0) */
+    float fmax;             /* mel fmax; < 0 => Nyquist */
+    const float* mel_fb;    /* optional custom [n_fft/2+1, n_mels] filterbank (host) */
+} thesia_plan_desc;
+
+typedef struct thesia_plan thesia_plan;
+int thesia_plan_create(const thesia_plan_desc* desc, thesia_plan** plan);
+int thesia_plan_destroy(thesia_plan* plan);
+/* Bins per output row: n_fft/2+1 (linear kinds) or n_mels (mel kinds). */
+int thesia_plan_row_bins(const thesia_plan* plan, size_t* bins);
+
+typedef struct thesia_batch_desc {
+    int input_format;             /* thesia_input_format */
+    uint32_t channels;            /* interleaved channels; summed (lib.rs:42) if > 1 */
+    int fold_mono;                /* 1: apply the channel-sum fold for mono too (0.0 + x) */
+    const void* d_input;          /* device base pointer */
+    const uint64_t* track_offset; /* host [n_tracks]: element offset of each track */
+    const uint64_t* track_len;    /* host [n_tracks]: samples per channel */
+    size_t n_tracks;
+    void* d_output;               /* device: rows packed track after track */
+} thesia_batch_desc;
+
+typedef struct thesia_batch thesia_batch;
+/* Validates tracks (THESIA_ERR_TOO_SHORT for n < win-1) and uploads descriptors. */
+int thesia_batch_create(thesia_plan* plan, const thesia_batch_desc* desc, thesia_batch** batch);
+int thesia_batch_destroy(thesia_batch* batch);
+/* Frame counts: total and per track (frame0 prefix, host array of n_tracks+1, may be NULL). */
+int thesia_batch_frames(const thesia_batch* batch, uint64_t* total_frames, uint64_t* frame0);
+/* Output bytes the batch writes (total_frames * row_bins * elem size). */
+int thesia_batch_output_bytes(const thesia_batch* batch, uint64_t* bytes);
+/* One pass of the hot path over the whole batch on `stream` (a hipStream_t; NULL => the
+ * library's stream of the current device). Asynchronous. */
+int thesia_batch_run(thesia_batch* batch, void* stream);
+/* Runs `iters` passes bracketed by HIP events on the launch stream; returns the elapsed
+ * milliseconds of all passes (synchronous). */
+int thesia_batch_run_timed(thesia_batch* batch, void* stream, int iters, float* ms);
+/* Kernel geometry report for roofline accounting. */
+int thesia_batch_kernel_info(const thesia_batch* batch, int* lds_bytes, int* tile_frames,
+                             int* grid);
+
+/* Deterministic synthetic PCM (int16-quantised chirp + noise) written on the device, and
+ * its bit-identical host twin. format: thesia_input_format. Layout [track][sample][ch]. */
+int thesia_synth_pcm_device(void* d_out, int format, uint32_t channels, uint64_t n_tracks,
+                            uint64_t n_samples, uint32_t sr, uint64_t seed);
+int thesia_synth_pcm_host(int16_t* out, uint32_t channels, uint64_t track, uint64_t n_samples,
+                          uint32_t sr, uint64_t seed);
+
+/* ---------------------------------------------------------------------------------- */
+/* display primitives on the device (host buffers in / out) -- display.rs               */
+/* ---------------------------------------------------------------------------------- */
+/* spec_to_grey -- display.rs:44-54. spec [T, bins]; grey [H, T], H = round(bins*up_ratio). */
+int thesia_spec_grey_height(size_t bins, float up_ratio, uint32_t* height);
+int thesia_spec_to_grey(const float* spec, size_t T, size_t bins, float up_ratio, float max,
+                        float min, float* grey, size_t cap_floats);
+/* grey_to_rgb -- display.rs:56-61 (Lanczos3 resize + colormap). out [nh, nw, 3]. */
+int thesia_grey_to_rgb(const float* grey, uint32_t width, uint32_t height, uint32_t nwidth,
+                       uint32_t nheight, uint8_t* out, size_t cap);
+/* wav_to_image -- display.rs:63-115. out [nheight, nwidth, 4] RGBA. */
+int thesia_wav_to_image(const float* wav, size_t n, uint32_t nwidth, uint32_t nheight,
+                        float amp_min, float amp_max, uint8_t* out, size_t cap);
+
+/* ---------------------------------------------------------------------------------- */
+/* MultiTrack -- lib.rs:72-365 (the viewer's stateful surface)                          */
+/* ---------------------------------------------------------------------------------- */
+typedef struct thesia_mt thesia_mt;
+/* MultiTrack::new -- lib.rs:89-110 (win_ms 40, t_overlap 4, f_overlap 1, Mel, 120 dB) */
+int thesia_mt_create(thesia_mt** mt);
+void thesia_mt_destroy(thesia_mt* mt);
+/* SpecSetting (lib.rs:64-70) has no setter in the reference; exposed for Linear-scale use.
+ * freq_scale: 0 = Linear, 1 = Mel. Must be called before any track is added. */
+int thesia_mt_set_setting(thesia_mt* mt, float win_ms, size_t t_overlap, size_t f_overlap,
+                          int freq_scale, float db_range);
+/* add_tracks(id_list, path_list) -> Result<bool, JsValue> -- lib.rs:170-191.
+ * paths are '\n'-separated; *changed = "global dB range / max sr changed: refetch all
+ * images". On error nothing is added (the reference would leave a half-added state). */
+int thesia_mt_add_tracks(thesia_mt* mt, const uint64_t* ids, size_t n_ids, const char* paths,
+                         int* changed);
+/* Same, from in-memory interleaved f32 PCM (what open_audio_file returns, audio.rs:9-37). */
+int thesia_mt_add_tracks_pcm(thesia_mt* mt, const uint64_t* ids, size_t n_ids,
+                             const float* const* pcm, const uint64_t* n_samples,
+                             const uint32_t* channels, const uint32_t* sr, const char* paths,
+                             int* changed);
+/* remove_track(id) -> bool -- lib.rs:265-292 */
+int thesia_mt_remove_track(thesia_mt* mt, uint64_t id, int* changed);
+/* get_spec_image(id, px_per_sec, nheight) -> Vec<u8> RGB -- lib.rs:294-298 */
+int thesia_mt_get_spec_image(thesia_mt* mt, uint64_t id, float px_per_sec, uint32_t nheight,
+                             uint8_t* out, size_t cap, size_t* needed);
+/* get_wav_image(id, px_per_sec, nheight, amp_min, amp_max) -> Vec<u8> RGBA -- lib.rs:300-313 */
+int thesia_mt_get_wav_image(thesia_mt* mt, uint64_t id, float px_per_sec, uint32_t nheight,
+                            float amp_min, float amp_max, uint8_t* out, size_t cap,
+                            size_t* needed);
+/* get_frequency_hz(id, relative_freq) -- lib.rs:315-322 */
+int thesia_mt_get_frequency_hz(thesia_mt* mt, uint64_t id, float relative_freq, float* hz);
+/* getters -- lib.rs:324-364 */
+float thesia_mt_get_max_db(const thesia_mt* mt);
+float thesia_mt_get_min_db(const thesia_mt* mt);
+float thesia_mt_get_max_sec(const thesia_mt* mt);
+int thesia_mt_get_sec(const thesia_mt* mt, uint64_t id, float* sec);
+int thesia_mt_get_sr(const thesia_mt* mt, uint64_t id, uint32_t* sr);
+int thesia_mt_get_path(const thesia_mt* mt, uint64_t id, char* out, size_t cap, size_t* needed);
+int thesia_mt_get_filename(const thesia_mt* mt, uint64_t id, char* out, size_t cap,
+                           size_t* needed);
+/* Introspection for parity tests (not in the reference surface): the dB spectrogram
+ * [T, bins] (lib.rs:112-136 calc_spec_of) and the grey image [H, T] (lib.rs:249-260). */
+int thesia_mt_get_spec(const thesia_mt* mt, uint64_t id, float* out, size_t cap_floats,
+                       size_t* n_frames, size_t* n_bins);
+int thesia_mt_get_grey(const thesia_mt* mt, uint64_t id, float* out, size_t cap_floats,
+                       uint32_t* width, uint32_t* height);
+int thesia_mt_track_count(const thesia_mt* mt, size_t* n);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* THESIA_H */

@@ -1,0 +1,523 @@
+// capi.cpp -- extern "C" entry points of libthesia (include/thesia.h). Every function
+// catches C++ exceptions and maps failures to status codes; nothing aborts across FFI.
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstring>
+#include <new>
+#include <string>
+#include <vector>
+
+#include "../../include/thesia.h"
+#include "engine.hpp"
+#include "host_tables.hpp"
+#include "multitrack.hpp"
+#include "wav.hpp"
+
+using namespace thesia;
+
+// The opaque handle types of thesia.h are never defined: handles are the C++ objects
+// themselves, reinterpret_cast at the boundary.
+
+#define GUARD_BEGIN try {
+#define GUARD_END                                                                       \
+    }                                                                                   \
+    catch (const std::bad_alloc&) {                                                     \
+        return set_error(THESIA_ERR_DEVICE, "host out of memory");                      \
+    }                                                                                   \
+    catch (const std::exception& e) {                                                   \
+        return set_error(THESIA_ERR_INVALID_ARG, e.what());                             \
+    }                                                                                   \
+    catch (...) {                                                                       \
+        return set_error(THESIA_ERR_INVALID_ARG, "unknown error");                      \
+    }
+
+static int copy_out(const void* src, size_t bytes, void* out, size_t cap, size_t* needed) {
+    if (needed) *needed = bytes;
+    if (!out || cap < bytes)
+        return set_error(THESIA_ERR_BUFFER_TOO_SMALL, "output buffer too small");
+    if (bytes) std::memcpy(out, src, bytes);
+    return THESIA_OK;
+}
+
+extern "C" {
+
+const char* thesia_last_error(void) { return last_error(); }
+const char* thesia_version(void) { return "thesia-hip 0.1.0 (gfx950)"; }
+
+// ---------------------------------------------------------------- runtime
+int thesia_device_count(int* n) {
+    THESIA_HIP(hipGetDeviceCount(n));
+    return THESIA_OK;
+}
+int thesia_set_device(int device) {
+    THESIA_HIP(hipSetDevice(device));
+    return THESIA_OK;
+}
+int thesia_get_device(int* device) {
+    THESIA_HIP(hipGetDevice(device));
+    return THESIA_OK;
+}
+int thesia_device_malloc(void** ptr, size_t bytes) {
+    THESIA_HIP(hipMalloc(ptr, bytes ? bytes : 16));
+    return THESIA_OK;
+}
+int thesia_device_free(void* ptr) {
+    THESIA_HIP(hipFree(ptr));
+    return THESIA_OK;
+}
+int thesia_memcpy_h2d(void* dst, const void* src, size_t bytes) {
+    THESIA_HIP(hipMemcpy(dst, src, bytes, hipMemcpyHostToDevice));
+    return THESIA_OK;
+}
+int thesia_memcpy_d2h(void* dst, const void* src, size_t bytes) {
+    THESIA_HIP(hipMemcpy(dst, src, bytes, hipMemcpyDeviceToHost));
+    return THESIA_OK;
+}
+int thesia_memset_device(void* dst, int value, size_t bytes) {
+    THESIA_HIP(hipMemset(dst, value, bytes));
+    return THESIA_OK;
+}
+int thesia_device_synchronize(void) {
+    THESIA_HIP(hipDeviceSynchronize());
+    return THESIA_OK;
+}
+int thesia_device_info(char* name, size_t cap, int* n_cu) {
+    int dev = 0;
+    THESIA_HIP(hipGetDevice(&dev));
+    hipDeviceProp_t prop;
+    THESIA_HIP(hipGetDeviceProperties(&prop, dev));
+    if (name && cap) {
+        std::strncpy(name, prop.gcnArchName, cap - 1);
+        name[cap - 1] = 0;
+    }
+    if (n_cu) *n_cu = prop.multiProcessorCount;
+    return THESIA_OK;
+}
+
+// ---------------------------------------------------------------- tables
+int thesia_hann(size_t size, int symmetric, float* out) {
+    GUARD_BEGIN
+    if (size < 2) return set_error(THESIA_ERR_INVALID_ARG, "windows.rs:8 asserts size > 1");
+    std::vector<float> w = hann(size, symmetric != 0);
+    std::memcpy(out, w.data(), size * sizeof(float));
+    return THESIA_OK;
+    GUARD_END
+}
+size_t thesia_calc_proper_n_fft(size_t win_length) { return calc_proper_n_fft(win_length); }
+float thesia_hz_to_mel(float hz) { return hz_to_mel(hz); }
+float thesia_mel_to_hz(float mel) { return mel_to_hz(mel); }
+
+int thesia_calc_mel_fb(uint32_t sr, size_t n_fft, size_t n_mel, float fmin, float fmax,
+                       int do_norm, float* out) {
+    GUARD_BEGIN
+    if (n_fft % 2 || n_mel == 0) return set_error(THESIA_ERR_INVALID_ARG, "mel.rs:52-53 asserts");
+    std::vector<float> fb = calc_mel_fb(sr, n_fft, n_mel, fmin, fmax, do_norm != 0);
+    std::memcpy(out, fb.data(), fb.size() * sizeof(float));
+    return THESIA_OK;
+    GUARD_END
+}
+
+int thesia_calc_mel_fb_default(uint32_t sr, size_t n_fft, size_t* n_mel, float* out, size_t cap) {
+    GUARD_BEGIN
+    size_t nm = 0;
+    std::vector<float> fb = calc_mel_fb_default(sr, n_fft, &nm);
+    *n_mel = nm;
+    if (!out) return THESIA_OK;
+    if (cap < fb.size()) return set_error(THESIA_ERR_BUFFER_TOO_SMALL, "mel_fb buffer too small");
+    std::memcpy(out, fb.data(), fb.size() * sizeof(float));
+    return THESIA_OK;
+    GUARD_END
+}
+
+void thesia_get_colormap(uint8_t out[30]) {
+    for (int i = 0; i < 10; ++i)
+        for (int k = 0; k < 3; ++k) out[i * 3 + k] = kColormap[i][k];
+}
+
+int thesia_track_params(uint32_t sr, float win_ms, size_t t_overlap, size_t f_overlap,
+                        size_t* win, size_t* hop, size_t* n_fft) {
+    if (t_overlap == 0) return set_error(THESIA_ERR_INVALID_ARG, "t_overlap must be > 0");
+    track_params(sr, win_ms, t_overlap, f_overlap, win, hop, n_fft);
+    return THESIA_OK;
+}
+
+// ---------------------------------------------------------------- perform_stft
+size_t thesia_stft_n_frames(size_t n, size_t win, size_t hop) { return stft_n_frames(n, win, hop); }
+
+int thesia_perform_stft(const float* input, size_t n, size_t win, size_t hop, size_t n_fft,
+                        const float* window, float* out, size_t out_cap_frames, size_t* n_frames) {
+    GUARD_BEGIN
+    const uint64_t T = stft_n_frames(n, win, hop);
+    if (T == 0) return set_error(THESIA_ERR_TOO_SHORT, "input shorter than win_length - 1 (lib.rs:413)");
+    if (n_frames) *n_frames = T;
+    if (!out || out_cap_frames < T) return set_error(THESIA_ERR_BUFFER_TOO_SMALL, "output too small");
+    thesia_plan_desc d{};
+    d.win_length = win;
+    d.hop_length = hop;
+    d.n_fft = n_fft;
+    d.window = window;
+    d.output = THESIA_OUT_COMPLEX;
+    Plan* plan = nullptr;
+    int rc = plan_create(d, &plan);
+    if (rc) return rc;
+    DevBuf din, dout;
+    rc = din.upload(input, n * sizeof(float));
+    const size_t F = n_fft / 2 + 1;
+    if (!rc) rc = dout.alloc((size_t)T * F * 8);
+    Batch* b = nullptr;
+    if (!rc) {
+        const uint64_t off = 0, len = n;
+        thesia_batch_desc bd{};
+        bd.input_format = THESIA_IN_F32;
+        bd.channels = 1;
+        bd.fold_mono = 0;
+        bd.d_input = din.p;
+        bd.track_offset = &off;
+        bd.track_len = &len;
+        bd.n_tracks = 1;
+        bd.d_output = dout.p;
+        rc = batch_create(plan, bd, &b);
+    }
+    if (!rc) rc = batch_run(b, default_stream());
+    if (!rc) {
+        hipError_t e = hipStreamSynchronize(default_stream());
+        if (e == hipSuccess) e = hipMemcpy(out, dout.p, (size_t)T * F * 8, hipMemcpyDeviceToHost);
+        if (e != hipSuccess) rc = set_error(THESIA_ERR_DEVICE, hipGetErrorString(e));
+    }
+    delete b;
+    delete plan;
+    return rc;
+    GUARD_END
+}
+
+// ---------------------------------------------------------------- batch engine
+int thesia_plan_create(const thesia_plan_desc* desc, thesia_plan** plan) {
+    GUARD_BEGIN
+    if (!desc || !plan) return set_error(THESIA_ERR_INVALID_ARG, "null argument");
+    Plan* p = nullptr;
+    int rc = plan_create(*desc, &p);
+    if (rc) return rc;
+    *plan = reinterpret_cast<thesia_plan*>(p);
+    return THESIA_OK;
+    GUARD_END
+}
+int thesia_plan_destroy(thesia_plan* plan) {
+    delete reinterpret_cast<Plan*>(plan);
+    return THESIA_OK;
+}
+int thesia_plan_row_bins(const thesia_plan* plan, size_t* bins) {
+    if (!plan || !bins) return set_error(THESIA_ERR_INVALID_ARG, "null argument");
+    *bins = reinterpret_cast<const Plan*>(plan)->row_bins();
+    return THESIA_OK;
+}
+
+int thesia_batch_create(thesia_plan* plan, const thesia_batch_desc* desc, thesia_batch** batch) {
+    GUARD_BEGIN
+    if (!plan || !desc || !batch) return set_error(THESIA_ERR_INVALID_ARG, "null argument");
+    Batch* b = nullptr;
+    int rc = batch_create(reinterpret_cast<Plan*>(plan), *desc, &b);
+    if (rc) return rc;
+    *batch = reinterpret_cast<thesia_batch*>(b);
+    return THESIA_OK;
+    GUARD_END
+}
+int thesia_batch_destroy(thesia_batch* batch) {
+    delete reinterpret_cast<Batch*>(batch);
+    return THESIA_OK;
+}
+int thesia_batch_frames(const thesia_batch* batch, uint64_t* total, uint64_t* frame0) {
+    if (!batch) return set_error(THESIA_ERR_INVALID_ARG, "null batch");
+    const Batch* b = reinterpret_cast<const Batch*>(batch);
+    if (total) *total = b->total_frames;
+    if (frame0) std::memcpy(frame0, b->frame0.data(), b->frame0.size() * 8);
+    return THESIA_OK;
+}
+int thesia_batch_output_bytes(const thesia_batch* batch, uint64_t* bytes) {
+    if (!batch || !bytes) return set_error(THESIA_ERR_INVALID_ARG, "null argument");
+    const Batch* b = reinterpret_cast<const Batch*>(batch);
+    *bytes = b->total_frames * b->plan->row_bins() * b->plan->out_elem_bytes();
+    return THESIA_OK;
+}
+int thesia_batch_run(thesia_batch* batch, void* stream) {
+    GUARD_BEGIN
+    if (!batch) return set_error(THESIA_ERR_INVALID_ARG, "null batch");
+    return batch_run(reinterpret_cast<Batch*>(batch), static_cast<hipStream_t>(stream));
+    GUARD_END
+}
+int thesia_batch_run_timed(thesia_batch* batch, void* stream, int iters, float* ms) {
+    GUARD_BEGIN
+    if (!batch || iters < 1) return set_error(THESIA_ERR_INVALID_ARG, "bad argument");
+    Batch* b = reinterpret_cast<Batch*>(batch);
+    hipStream_t s = stream ? static_cast<hipStream_t>(stream) : default_stream();
+    THESIA_HIP(hipEventRecord(b->ev0, s));
+    for (int i = 0; i < iters; ++i) {
+        int rc = batch_run(b, s);
+        if (rc) return rc;
+    }
+    THESIA_HIP(hipEventRecord(b->ev1, s));
+    THESIA_HIP(hipEventSynchronize(b->ev1));
+    float t = 0.f;
+    THESIA_HIP(hipEventElapsedTime(&t, b->ev0, b->ev1));
+    if (ms) *ms = t;
+    return THESIA_OK;
+    GUARD_END
+}
+int thesia_batch_kernel_info(const thesia_batch* batch, int* lds_bytes, int* tile_frames, int* grid) {
+    if (!batch) return set_error(THESIA_ERR_INVALID_ARG, "null batch");
+    const Batch* b = reinterpret_cast<const Batch*>(batch);
+    if (lds_bytes) *lds_bytes = b->plan->lds_bytes;
+    if (tile_frames) *tile_frames = b->plan->tile_frames;
+    if (grid) *grid = b->launch.grid;
+    return THESIA_OK;
+}
+
+int thesia_synth_pcm_device(void* d_out, int format, uint32_t channels, uint64_t n_tracks,
+                            uint64_t n_samples, uint32_t sr, uint64_t seed) {
+    GUARD_BEGIN
+    static DevBuf lut;  // per process (single device use in benches / tests)
+    static int lut_dev = -1;
+    int dev = 0;
+    THESIA_HIP(hipGetDevice(&dev));
+    if (lut_dev != dev) {
+        int rc = lut.upload(synth_lut_host(), 4096 * sizeof(int16_t));
+        if (rc) return rc;
+        lut_dev = dev;
+    }
+    if (launch_synth_pcm(d_out, format, channels, n_tracks, n_samples, sr, seed, lut.as<int16_t>(),
+                         default_stream()))
+        return set_error(THESIA_ERR_DEVICE, "synth launch failed");
+    THESIA_HIP(hipStreamSynchronize(default_stream()));
+    return THESIA_OK;
+    GUARD_END
+}
+int thesia_synth_pcm_host(int16_t* out, uint32_t channels, uint64_t track, uint64_t n_samples,
+                          uint32_t sr, uint64_t seed) {
+    GUARD_BEGIN
+    synth_host(out, channels, track, n_samples, sr, seed, synth_lut_host());
+    return THESIA_OK;
+    GUARD_END
+}
+
+// ---------------------------------------------------------------- display primitives
+int thesia_spec_grey_height(size_t bins, float up_ratio, uint32_t* height) {
+    const float h = roundf((float)bins * up_ratio);
+    *height = h > 0.f ? (h >= 4294967295.0f ? 4294967295u : (uint32_t)h) : 0u;
+    return THESIA_OK;
+}
+
+int thesia_spec_to_grey(const float* spec, size_t T, size_t bins, float up_ratio, float max,
+                        float min, float* grey, size_t cap) {
+    GUARD_BEGIN
+    uint32_t H = 0;
+    thesia_spec_grey_height(bins, up_ratio, &H);
+    if (H < bins) return set_error(THESIA_ERR_INVALID_ARG, "up_ratio < 1 (display.rs:47 underflows)");
+    if (cap < (size_t)H * T) return set_error(THESIA_ERR_BUFFER_TOO_SMALL, "grey buffer too small");
+    DevBuf ds, dg;
+    int rc = ds.upload(spec, T * bins * sizeof(float));
+    if (!rc) rc = dg.alloc((size_t)H * T * sizeof(float));
+    if (rc) return rc;
+    if (launch_spec_to_grey(ds.as<float>(), (uint32_t)T, (uint32_t)bins, H, max, min, dg.as<float>(), default_stream()))
+        return set_error(THESIA_ERR_DEVICE, "spec_to_grey launch failed");
+    THESIA_HIP(hipStreamSynchronize(default_stream()));
+    THESIA_HIP(hipMemcpy(grey, dg.p, (size_t)H * T * sizeof(float), hipMemcpyDeviceToHost));
+    return THESIA_OK;
+    GUARD_END
+}
+
+int thesia_grey_to_rgb(const float* grey, uint32_t w, uint32_t h, uint32_t nw, uint32_t nh,
+                       uint8_t* out, size_t cap) {
+    GUARD_BEGIN
+    const size_t bytes = (size_t)nw * nh * 3;
+    if (cap < bytes) return set_error(THESIA_ERR_BUFFER_TOO_SMALL, "rgb buffer too small");
+    if (bytes == 0) return THESIA_OK;
+    DevBuf dg, drgb;
+    int rc = dg.upload(grey, (size_t)w * h * sizeof(float));
+    if (!rc) rc = drgb.alloc(bytes);
+    if (!rc) rc = grey_to_rgb_device(dg.as<float>(), w, h, nw, nh, drgb.as<uint8_t>(), default_stream());
+    if (rc) return rc;
+    THESIA_HIP(hipMemcpy(out, drgb.p, bytes, hipMemcpyDeviceToHost));
+    return THESIA_OK;
+    GUARD_END
+}
+
+int thesia_wav_to_image(const float* wav, size_t n, uint32_t nwidth, uint32_t nheight,
+                        float amp_min, float amp_max, uint8_t* out, size_t cap) {
+    GUARD_BEGIN
+    const size_t bytes = (size_t)nwidth * nheight * 4;
+    if (cap < bytes) return set_error(THESIA_ERR_BUFFER_TOO_SMALL, "rgba buffer too small");
+    if (bytes == 0) return THESIA_OK;
+    DevBuf dw, dimg;
+    int rc = dw.upload(wav, n * sizeof(float));
+    if (!rc) rc = dimg.alloc(bytes);
+    int panicked = 0;
+    if (!rc) rc = wav_to_image_device(dw.as<float>(), n, nwidth, nheight, amp_min, amp_max,
+                                      dimg.as<uint8_t>(), &panicked, default_stream());
+    if (rc) return rc;
+    THESIA_HIP(hipMemcpy(out, dimg.p, bytes, hipMemcpyDeviceToHost));
+    return THESIA_OK;
+    GUARD_END
+}
+
+// ---------------------------------------------------------------- MultiTrack
+int thesia_mt_create(thesia_mt** mt) {
+    GUARD_BEGIN
+    *mt = reinterpret_cast<thesia_mt*>(new MultiTrack());
+    return THESIA_OK;
+    GUARD_END
+}
+void thesia_mt_destroy(thesia_mt* mt) { delete reinterpret_cast<MultiTrack*>(mt); }
+
+static MultiTrack* M(thesia_mt* mt) { return reinterpret_cast<MultiTrack*>(mt); }
+static const MultiTrack* M(const thesia_mt* mt) { return reinterpret_cast<const MultiTrack*>(mt); }
+
+int thesia_mt_set_setting(thesia_mt* mt, float win_ms, size_t t_overlap, size_t f_overlap,
+                          int freq_scale, float db_range) {
+    GUARD_BEGIN
+    return M(mt)->set_setting(win_ms, t_overlap, f_overlap, freq_scale, db_range);
+    GUARD_END
+}
+
+static std::vector<std::string> split_paths(const char* paths) {
+    std::vector<std::string> out;
+    std::string s(paths ? paths : "");
+    size_t start = 0;
+    while (true) {  // path_list.split("\n"), lib.rs:173
+        const size_t e = s.find('\n', start);
+        out.push_back(s.substr(start, e == std::string::npos ? std::string::npos : e - start));
+        if (e == std::string::npos) break;
+        start = e + 1;
+    }
+    return out;
+}
+
+int thesia_mt_add_tracks(thesia_mt* mt, const uint64_t* ids, size_t n_ids, const char* paths,
+                         int* changed) {
+    GUARD_BEGIN
+    std::vector<std::string> pl = split_paths(paths);
+    const size_t n = std::min(n_ids, pl.size());  // zip stops at the shorter list
+    std::vector<WavData> wavs(n);
+    std::vector<uint64_t> idv(ids, ids + n);
+    std::vector<PcmIn> pcm(n);
+    for (size_t i = 0; i < n; ++i) {
+        std::string err;
+        int rc = read_wav(pl[i], &wavs[i], &err);
+        if (rc) return set_error(rc, err);
+        pcm[i].samples = wavs[i].samples.data();
+        pcm[i].channels = wavs[i].channels;
+        pcm[i].n_samples = wavs[i].samples.size() / wavs[i].channels;
+        pcm[i].sr = wavs[i].sr;
+        pcm[i].path = pl[i];
+    }
+    return M(mt)->add_tracks(idv, pcm, changed);
+    GUARD_END
+}
+
+int thesia_mt_add_tracks_pcm(thesia_mt* mt, const uint64_t* ids, size_t n_ids,
+                             const float* const* pcm_in, const uint64_t* n_samples,
+                             const uint32_t* channels, const uint32_t* sr, const char* paths,
+                             int* changed) {
+    GUARD_BEGIN
+    std::vector<std::string> pl = split_paths(paths);
+    std::vector<uint64_t> idv(ids, ids + n_ids);
+    std::vector<PcmIn> pcm(n_ids);
+    for (size_t i = 0; i < n_ids; ++i) {
+        pcm[i].samples = pcm_in[i];
+        pcm[i].n_samples = n_samples[i];
+        pcm[i].channels = channels[i];
+        pcm[i].sr = sr[i];
+        pcm[i].path = i < pl.size() ? pl[i] : std::string();
+    }
+    return M(mt)->add_tracks(idv, pcm, changed);
+    GUARD_END
+}
+
+int thesia_mt_remove_track(thesia_mt* mt, uint64_t id, int* changed) {
+    GUARD_BEGIN
+    return M(mt)->remove_track(id, changed);
+    GUARD_END
+}
+
+int thesia_mt_get_spec_image(thesia_mt* mt, uint64_t id, float px_per_sec, uint32_t nheight,
+                             uint8_t* out, size_t cap, size_t* needed) {
+    GUARD_BEGIN
+    std::vector<uint8_t> img;
+    int rc = M(mt)->spec_image(id, px_per_sec, nheight, &img);
+    if (rc) return rc;
+    return copy_out(img.data(), img.size(), out, cap, needed);
+    GUARD_END
+}
+
+int thesia_mt_get_wav_image(thesia_mt* mt, uint64_t id, float px_per_sec, uint32_t nheight,
+                            float amp_min, float amp_max, uint8_t* out, size_t cap, size_t* needed) {
+    GUARD_BEGIN
+    std::vector<uint8_t> img;
+    int rc = M(mt)->wav_image(id, px_per_sec, nheight, amp_min, amp_max, &img);
+    if (rc) return rc;
+    return copy_out(img.data(), img.size(), out, cap, needed);
+    GUARD_END
+}
+
+int thesia_mt_get_frequency_hz(thesia_mt* mt, uint64_t id, float rel, float* hz) {
+    return M(mt)->frequency_hz(id, rel, hz);
+}
+float thesia_mt_get_max_db(const thesia_mt* mt) { return M(mt)->max_db(); }
+float thesia_mt_get_min_db(const thesia_mt* mt) { return M(mt)->min_db(); }
+float thesia_mt_get_max_sec(const thesia_mt* mt) { return M(mt)->max_sec(); }
+
+int thesia_mt_get_sec(const thesia_mt* mt, uint64_t id, float* sec) {
+    const Track* t = M(mt)->find(id);
+    if (!t) return set_error(THESIA_ERR_UNKNOWN_ID, "unknown track id");
+    *sec = (float)t->n / (float)t->sr;  // lib.rs:336-339
+    return THESIA_OK;
+}
+int thesia_mt_get_sr(const thesia_mt* mt, uint64_t id, uint32_t* sr) {
+    const Track* t = M(mt)->find(id);
+    if (!t) return set_error(THESIA_ERR_UNKNOWN_ID, "unknown track id");
+    *sr = t->sr;
+    return THESIA_OK;
+}
+int thesia_mt_get_path(const thesia_mt* mt, uint64_t id, char* out, size_t cap, size_t* needed) {
+    const Track* t = M(mt)->find(id);
+    if (!t) return set_error(THESIA_ERR_UNKNOWN_ID, "unknown track id");
+    std::string s = t->path;
+    s.push_back('\0');
+    return copy_out(s.data(), s.size(), out, cap, needed);
+}
+int thesia_mt_get_filename(const thesia_mt* mt, uint64_t id, char* out, size_t cap, size_t* needed) {
+    const Track* t = M(mt)->find(id);
+    if (!t) return set_error(THESIA_ERR_UNKNOWN_ID, "unknown track id");
+    std::string s = MultiTrack::filename_of(*t);
+    s.push_back('\0');
+    return copy_out(s.data(), s.size(), out, cap, needed);
+}
+int thesia_mt_get_spec(const thesia_mt* mt, uint64_t id, float* out, size_t cap, size_t* T,
+                       size_t* bins) {
+    GUARD_BEGIN
+    std::vector<float> v;
+    int rc = M(mt)->spec_host(id, &v, T, bins);
+    if (rc) return rc;
+    if (!out) return THESIA_OK;
+    if (cap < v.size()) return set_error(THESIA_ERR_BUFFER_TOO_SMALL, "spec buffer too small");
+    std::memcpy(out, v.data(), v.size() * 4);
+    return THESIA_OK;
+    GUARD_END
+}
+int thesia_mt_get_grey(const thesia_mt* mt, uint64_t id, float* out, size_t cap, uint32_t* w,
+                       uint32_t* h) {
+    GUARD_BEGIN
+    std::vector<float> v;
+    int rc = M(mt)->grey_host(id, &v, w, h);
+    if (rc) return rc;
+    if (!out) return THESIA_OK;
+    if (cap < v.size()) return set_error(THESIA_ERR_BUFFER_TOO_SMALL, "grey buffer too small");
+    std::memcpy(out, v.data(), v.size() * 4);
+    return THESIA_OK;
+    GUARD_END
+}
+int thesia_mt_track_count(const thesia_mt* mt, size_t* n) {
+    *n = M(mt)->size();
+    return THESIA_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,368 @@
+// display_kernels.hip -- the display half of the path (display.rs) and small helpers.
+//
+//   K3 minmax        : per-track max/min of a dB spectrogram (lib.rs:194-207; ndarray-stats
+//                      max/min error -> (-inf, +inf) on NaN)
+//   K4 spec_to_grey  : transpose + vertical flip + normalise + zero top fill (display.rs:44-54)
+//   K5 resize        : separable Lanczos3 (image 0.23.12 resize: vertical pass into an f32
+//                      image, then horizontal), weights from the host (same f32 formulas)
+//   K6 colormap      : fused into the horizontal pass epilogue (display.rs:24-42, 56-61)
+//   wav image        : min/max envelope raster in WAVECOLOR (display.rs:63-115)
+//   downmix          : channel sum in ndarray's unrolled_fold order (lib.rs:42)
+//   synth            : deterministic integer PCM generator for benches / tests
+// All accumulations run in the reference's order with -ffp-contract=off, so given the
+// same f32 input these kernels reproduce the oracle bit for bit.
+#include "kernels.hpp"
+
+#include <cmath>
+#include <cstdint>
+
+namespace thesia {
+
+// ------------------------------------------------------------------------------------
+// downmix (lib.rs:42 sum_axis over channels -> unrolled_fold)
+// ------------------------------------------------------------------------------------
+template <int INF>
+__device__ __forceinline__ float chan_at(const void* in, uint64_t idx) {
+    if constexpr (INF == IN_S16) return (float)static_cast<const int16_t*>(in)[idx] / 32768.0f;
+    else return static_cast<const float*>(in)[idx];
+}
+
+template <int INF>
+__global__ void downmix_kernel(const void* in, int C, uint64_t n, float* out) {
+    for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n;
+         i += (uint64_t)gridDim.x * blockDim.x) {
+        const uint64_t p = i * (uint64_t)C;
+        float acc = 0.0f;
+        if (C < 8) {
+            for (int c = 0; c < C; ++c) acc = acc + chan_at<INF>(in, p + c);
+        } else {
+            float q[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+            int c = 0;
+            for (; C - c >= 8; c += 8)
+                for (int u = 0; u < 8; ++u) q[u] = q[u] + chan_at<INF>(in, p + c + u);
+            acc = acc + (q[0] + q[4]);
+            acc = acc + (q[1] + q[5]);
+            acc = acc + (q[2] + q[6]);
+            acc = acc + (q[3] + q[7]);
+            for (; c < C; ++c) acc = acc + chan_at<INF>(in, p + c);
+        }
+        out[i] = acc;
+    }
+}
+
+int launch_downmix(const void* in, int in_format, int channels, uint64_t n, float* out,
+                   hipStream_t s) {
+    if (n == 0) return 0;
+    uint64_t blocks = (n + 255) / 256;
+    if (blocks > 8192) blocks = 8192;
+    if (in_format == IN_S16)
+        hipLaunchKernelGGL(downmix_kernel<IN_S16>, dim3((unsigned)blocks), dim3(256), 0, s, in, channels, n, out);
+    else
+        hipLaunchKernelGGL(downmix_kernel<IN_F32>, dim3((unsigned)blocks), dim3(256), 0, s, in, channels, n, out);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+// ------------------------------------------------------------------------------------
+// K3 per-track max/min (NaN -> flag)
+// ------------------------------------------------------------------------------------
+__global__ void minmax_kernel(const float* x, uint64_t n, float* partial, int* nan_flag) {
+    float mx = -INFINITY, mn = INFINITY;
+    int nan = 0;
+    for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n;
+         i += (uint64_t)gridDim.x * blockDim.x) {
+        const float v = x[i];
+        if (v != v) nan = 1;
+        mx = fmaxf(mx, v);
+        mn = fminf(mn, v);
+    }
+    __shared__ float smx[256], smn[256];
+    __shared__ int snan;
+    if (threadIdx.x == 0) snan = 0;
+    __syncthreads();
+    smx[threadIdx.x] = mx;
+    smn[threadIdx.x] = mn;
+    if (nan) snan = 1;
+    __syncthreads();
+    for (int st = 128; st > 0; st >>= 1) {
+        if ((int)threadIdx.x < st) {
+            smx[threadIdx.x] = fmaxf(smx[threadIdx.x], smx[threadIdx.x + st]);
+            smn[threadIdx.x] = fminf(smn[threadIdx.x], smn[threadIdx.x + st]);
+        }
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) {
+        partial[2 * blockIdx.x] = smx[0];
+        partial[2 * blockIdx.x + 1] = smn[0];
+        if (snan) atomicOr(nan_flag, 1);
+    }
+}
+
+int launch_minmax(const float* x, uint64_t n, float* partial, int* nan_flag, int nblk,
+                  hipStream_t s) {
+    hipLaunchKernelGGL(minmax_kernel, dim3(nblk), dim3(256), 0, s, x, n, partial, nan_flag);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+// ------------------------------------------------------------------------------------
+// K4 spec_to_grey (display.rs:44-54): grey[y][x], y < H, x < T
+// ------------------------------------------------------------------------------------
+__global__ void spec_to_grey_kernel(const float* spec, uint32_t T, uint32_t bins, uint32_t H,
+                                    float max, float min, float* grey) {
+    const uint32_t x = blockIdx.x * blockDim.x + threadIdx.x;
+    const uint32_t y = blockIdx.y;
+    if (x >= T || y >= H) return;
+    float v = 0.0f;
+    if (y >= H - bins) {
+        const float db = spec[(uint64_t)x * bins + (H - 1 - y)];
+        v = (db - min) / (max - min);
+        v = fmaxf(v, 0.0f);  // Rust f32::max / min: NaN-ignoring, like fmaxf/fminf
+        v = fminf(v, 1.0f);
+    }
+    grey[(uint64_t)y * T + x] = v;
+}
+
+int launch_spec_to_grey(const float* spec, uint32_t T, uint32_t bins, uint32_t H, float max,
+                        float min, float* grey, hipStream_t s) {
+    if (T == 0 || H == 0) return 0;
+    dim3 grid((T + 255) / 256, H);
+    hipLaunchKernelGGL(spec_to_grey_kernel, grid, dim3(256), 0, s, spec, T, bins, H, max, min, grey);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+// ------------------------------------------------------------------------------------
+// K5 vertical Lanczos3 pass: out[oy][x] = sum_i in[left+i][x] * w[i] (sequential order)
+// ------------------------------------------------------------------------------------
+__global__ void resize_v_kernel(const float* in, uint32_t w, uint32_t nh, const int32_t* left,
+                                const int32_t* cnt, const int32_t* woff, const float* wts,
+                                float* out) {
+    const uint32_t x = blockIdx.x * blockDim.x + threadIdx.x;
+    const uint32_t oy = blockIdx.y;
+    if (x >= w || oy >= nh) return;
+    const int32_t l = left[oy], n = cnt[oy];
+    const float* wr = wts + woff[oy];
+    float t = 0.0f;
+    for (int32_t i = 0; i < n; ++i) t += in[(uint64_t)(l + i) * w + x] * wr[i];
+    out[(uint64_t)oy * w + x] = t;
+}
+
+int launch_resize_v(const float* in, uint32_t w, uint32_t h, uint32_t nh, const int32_t* left,
+                    const int32_t* cnt, const int32_t* woff, const float* wts, int max_taps,
+                    float* out, hipStream_t s) {
+    (void)h;
+    (void)max_taps;
+    if (w == 0 || nh == 0) return 0;
+    dim3 grid((w + 255) / 256, nh);
+    hipLaunchKernelGGL(resize_v_kernel, grid, dim3(256), 0, s, in, w, nh, left, cnt, woff, wts, out);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+// ------------------------------------------------------------------------------------
+// K5 horizontal pass + K6 colormap (display.rs:24-42): RGB u8 [nh][nw][3]
+// ------------------------------------------------------------------------------------
+__device__ __forceinline__ uint8_t sat_u8(float v) {  // Rust `as u8`
+    if (!(v == v)) return 0;
+    if (v <= 0.0f) return 0;
+    if (v >= 255.0f) return 255;
+    return (uint8_t)v;
+}
+
+__global__ void resize_h_rgb_kernel(const float* in, uint32_t w, uint32_t nh, uint32_t nw,
+                                    const int32_t* left, const int32_t* cnt, const int32_t* woff,
+                                    const float* wts, const uint8_t* cmap, uint8_t* out) {
+    const uint32_t ox = blockIdx.x * blockDim.x + threadIdx.x;
+    const uint32_t y = blockIdx.y;
+    if (ox >= nw || y >= nh) return;
+    const int32_t l = left[ox], n = cnt[ox];
+    const float* wr = wts + woff[ox];
+    const float* row = in + (uint64_t)y * w;
+    float t = 0.0f;
+    for (int32_t i = 0; i < n; ++i) t += row[l + i] * wr[i];
+    // convert_grey_to_color; the reference asserts x >= 0 (a panic on Lanczos undershoot):
+    // product policy treats x < 0 (and NaN) as 0 -- bit-identical wherever it does not panic.
+    float x = t;
+    if (!(x >= 0.0f)) x = 0.0f;
+    const float position = 10.0f * x;
+    const float fl = floorf(position);
+    uint8_t* o = out + ((uint64_t)y * nw + ox) * 3;
+    if (fl >= 9.0f) {
+        o[0] = cmap[27];
+        o[1] = cmap[28];
+        o[2] = cmap[29];
+        return;
+    }
+    const int index = (int)fl;
+    const float ratio = position - (float)index;
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+        const float av = (float)cmap[index * 3 + c], bv = (float)cmap[(index + 1) * 3 + c];
+        o[c] = sat_u8(roundf(ratio * bv + (1.0f - ratio) * av));
+    }
+}
+
+int launch_resize_h_rgb(const float* in, uint32_t w, uint32_t nh, uint32_t nw,
+                        const int32_t* left, const int32_t* cnt, const int32_t* woff,
+                        const float* wts, int max_taps, const uint8_t* cmap, uint8_t* out,
+                        hipStream_t s) {
+    (void)max_taps;
+    if (nw == 0 || nh == 0) return 0;
+    dim3 grid((nw + 255) / 256, nh);
+    hipLaunchKernelGGL(resize_h_rgb_kernel, grid, dim3(256), 0, s, in, w, nh, nw, left, cnt, woff,
+                       wts, cmap, out);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+// ------------------------------------------------------------------------------------
+// waveform image (display.rs:63-115)
+// ------------------------------------------------------------------------------------
+__global__ void wav_upsample_kernel(const float* wav, uint64_t n, uint32_t factor, float* out) {
+    const uint64_t total = (uint64_t)factor * n;
+    for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < total;
+         i += (uint64_t)gridDim.x * blockDim.x) {
+        const uint64_t q = i / factor, r = i % factor;
+        const float b = (q + 1 < n) ? wav[q + 1] : 0.0f;
+        out[i] = b * ((float)r / (float)factor) + wav[q] * (1.0f - (float)r / (float)factor);
+    }
+}
+
+int launch_wav_upsample(const float* wav, uint64_t n, uint32_t factor, float* out, hipStream_t s) {
+    const uint64_t total = (uint64_t)factor * n;
+    if (total == 0) return 0;
+    uint64_t blocks = (total + 255) / 256;
+    if (blocks > 8192) blocks = 8192;
+    hipLaunchKernelGGL(wav_upsample_kernel, dim3((unsigned)blocks), dim3(256), 0, s, wav, n, factor, out);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+// one thread per pixel column: envelope extent, then paint the column
+__global__ void wav_image_kernel(const float* wav, uint64_t wlen, uint32_t nwidth, uint32_t nheight,
+                                 float spp, float amp_min, float amp_max, uint8_t* out,
+                                 int* panicked) {
+    const uint32_t ipx = blockIdx.x * blockDim.x + threadIdx.x;
+    if (ipx >= nwidth) return;
+    float s = roundf(((float)ipx - 1.5f) * spp);
+    s = fmaxf(s, 0.0f);
+    const uint64_t i_start = (uint64_t)s;
+    const float e = roundf(((float)ipx + 1.5f) * spp);
+    uint64_t i_end = e <= 0.0f ? 0 : (uint64_t)e;
+    if (i_end > wlen) i_end = wlen;
+    for (uint32_t y = 0; y < nheight; ++y) {
+        uint8_t* o = out + ((uint64_t)y * nwidth + ipx) * 4;
+        o[0] = 0; o[1] = 0; o[2] = 0; o[3] = 0;
+    }
+    if (i_start >= i_end) { atomicOr(panicked, 1); return; }
+    float mx = wav[i_start], mn = wav[i_start];
+    bool nan = false;
+    for (uint64_t i = i_start; i < i_end; ++i) {
+        const float v = wav[i];
+        if (v != v) nan = true;
+        if (v > mx) mx = v;
+        if (v < mn) mn = v;
+    }
+    if (nan) { atomicOr(panicked, 1); return; }
+    const float fh = (float)nheight, rng = amp_max - amp_min;
+    long long top = (long long)roundf((amp_max - mx) * fh / rng);
+    long long bottom = (long long)roundf((amp_max - mn) * fh / rng);
+    if (bottom - top < 3) {
+        const float d = (float)(3 - bottom + top) / 2.0f;
+        const long long pad_bottom = (long long)ceilf(d), pad_top = (long long)floorf(d);
+        top -= pad_top;
+        bottom += pad_bottom;
+    }
+    if (top < 0) top = 0;
+    if (bottom > (long long)nheight) bottom = (long long)nheight;
+    if (bottom + 1 > (long long)nheight) { atomicOr(panicked, 1); bottom = (long long)nheight - 1; }
+    if (top > bottom + 1) { atomicOr(panicked, 1); return; }
+    for (long long y = top; y <= bottom; ++y) {
+        uint8_t* o = out + ((uint64_t)y * nwidth + ipx) * 4;
+        o[0] = 200; o[1] = 21; o[2] = 103; o[3] = 255;  // WAVECOLOR display.rs:22
+    }
+}
+
+int launch_wav_image(const float* wav, uint64_t n, const float* wav_up, uint64_t n_up,
+                     uint32_t nwidth, uint32_t nheight, float spp, float amp_min, float amp_max,
+                     uint8_t* out, int* panicked, hipStream_t s) {
+    if (nwidth == 0) return 0;
+    const float* src = wav_up ? wav_up : wav;
+    const uint64_t len = wav_up ? n_up : n;
+    hipLaunchKernelGGL(wav_image_kernel, dim3((nwidth + 127) / 128), dim3(128), 0, s, src, len,
+                       nwidth, nheight, spp, amp_min, amp_max, out, panicked);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+// ------------------------------------------------------------------------------------
+// deterministic integer PCM generator (bench / tests): chirp from an int16 sine LUT with a
+// 64-bit fixed-point phase, plus Irwin-Hall noise from a splitmix64 hash. Host and device
+// produce identical int16 samples (host twin in engine.cpp).
+// ------------------------------------------------------------------------------------
+__host__ __device__ inline uint64_t splitmix64(uint64_t x) {
+    x += 0x9E3779B97F4A7C15ull;
+    x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ull;
+    x = (x ^ (x >> 27)) * 0x94D049BB133111EBull;
+    return x ^ (x >> 31);
+}
+
+__host__ __device__ inline int16_t synth_sample(uint64_t track, uint32_t ch, uint64_t i,
+                                                uint64_t ph_a, uint64_t ph_b, uint64_t seed,
+                                                const int16_t* lut /*4096*/) {
+    // chirp phase in Q64 turns: ph = A*i + B*i^2 (mod 2^64), A, B from synth_phase_coeffs()
+    const uint64_t ph = ph_a * i + ph_b * (i * i);
+    const int32_t chirp = lut[ph >> 52] / 4;  // 0.25 full scale
+    const uint64_t h = splitmix64(seed ^ splitmix64(track * 0x100000001B3ull + ch) ^ (i * 0xD6E8FEB86659FD93ull));
+    // Irwin-Hall (4 x 16-bit uniforms): mean 2*65535, sd ~ 37837 -> scale to ~0.05 FS
+    const int64_t u = (int64_t)(h & 0xFFFF) + (int64_t)((h >> 16) & 0xFFFF) +
+                      (int64_t)((h >> 32) & 0xFFFF) + (int64_t)((h >> 48) & 0xFFFF) - 131070;
+    const int64_t noise = (u * 1638) / 37837;
+    int64_t v = (int64_t)chirp + noise;
+    if (v > 32767) v = 32767;
+    if (v < -32768) v = -32768;
+    return (int16_t)v;
+}
+
+__global__ void synth_kernel(void* out, int out_format, uint32_t C, uint64_t n_tracks,
+                             uint64_t n, uint64_t ph_a, uint64_t ph_b, uint64_t seed,
+                             const int16_t* lut) {
+    const uint64_t total = n_tracks * n * C;
+    for (uint64_t e = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; e < total;
+         e += (uint64_t)gridDim.x * blockDim.x) {
+        const uint64_t track = e / (n * C);
+        const uint64_t rem = e % (n * C);
+        const uint64_t i = rem / C;
+        const uint32_t ch = (uint32_t)(rem % C);
+        const int16_t v = synth_sample(track, ch, i, ph_a, ph_b, seed, lut);
+        if (out_format == IN_S16) static_cast<int16_t*>(out)[e] = v;
+        else static_cast<float*>(out)[e] = (float)v / 32768.0f;
+    }
+}
+
+void synth_phase_coeffs(uint64_t n, uint32_t sr, uint64_t* ph_a, uint64_t* ph_b) {
+    // f(t) sweeps 50 Hz -> 0.45 sr linearly over the track: phase(i) = a*i + b*i^2 turns
+    const double f0 = 50.0, f1 = 0.45 * (double)sr;
+    const double b = (f1 - f0) / (2.0 * (double)n * (double)sr);
+    const double a = f0 / (double)sr - b;
+    const double two64 = 18446744073709551616.0;
+    *ph_a = (uint64_t)(int64_t)(a * two64 / 4.0) * 4u;
+    *ph_b = (uint64_t)(b * two64);
+}
+
+int launch_synth_pcm(void* out, int out_format, uint32_t channels, uint64_t n_tracks,
+                     uint64_t n_samples, uint32_t sr, uint64_t seed, const int16_t* sine_lut,
+                     hipStream_t s) {
+    uint64_t pa = 0, pb = 0;
+    synth_phase_coeffs(n_samples, sr, &pa, &pb);
+    hipLaunchKernelGGL(synth_kernel, dim3(16384), dim3(256), 0, s, out, out_format, channels,
+                       n_tracks, n_samples, pa, pb, seed, sine_lut);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+}  // namespace thesia
+
+// host twin of the generator (same integer arithmetic)
+namespace thesia {
+void synth_host(int16_t* out, uint32_t C, uint64_t track, uint64_t n, uint32_t sr, uint64_t seed,
+                const int16_t* lut) {
+    uint64_t pa = 0, pb = 0;
+    synth_phase_coeffs(n, sr, &pa, &pb);
+    for (uint64_t i = 0; i < n; ++i)
+        for (uint32_t c = 0; c < C; ++c) out[i * C + c] = synth_sample(track, c, i, pa, pb, seed, lut);
+}
+}  // namespace thesia

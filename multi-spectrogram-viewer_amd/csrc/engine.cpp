@@ -1,0 +1,399 @@
+// engine.cpp -- plans, batches, streams, device buffers and display helpers of libthesia.
+#include "engine.hpp"
+
+#include <algorithm>
+#include <cmath>
+#include <map>
+#include <mutex>
+
+#include "host_tables.hpp"
+
+namespace thesia {
+
+// ------------------------------------------------------------------------------------
+// errors
+// ------------------------------------------------------------------------------------
+static thread_local std::string g_err;
+
+int set_error(int code, const std::string& msg) {
+    g_err = msg;
+    return code;
+}
+void clear_error() { g_err.clear(); }
+const char* last_error() { return g_err.c_str(); }
+
+// ------------------------------------------------------------------------------------
+// device buffers / streams
+// ------------------------------------------------------------------------------------
+void DevBuf::release() {
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    bytes = 0;
+}
+
+int DevBuf::alloc(size_t n) {
+    release();
+    if (n == 0) n = 16;
+    hipError_t e = hipMalloc(&p, n);
+    if (e != hipSuccess) {
+        p = nullptr;
+        return set_error(THESIA_ERR_DEVICE, std::string("hipMalloc: ") + hipGetErrorString(e));
+    }
+    bytes = n;
+    return THESIA_OK;
+}
+
+int DevBuf::upload(const void* host, size_t n) {
+    int rc = alloc(n);
+    if (rc) return rc;
+    if (n && host) THESIA_HIP(hipMemcpy(p, host, n, hipMemcpyHostToDevice));
+    return THESIA_OK;
+}
+
+hipStream_t default_stream() {
+    static std::mutex mu;
+    static std::map<int, hipStream_t> streams;
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    std::lock_guard<std::mutex> lk(mu);
+    auto it = streams.find(dev);
+    if (it != streams.end()) return it->second;
+    hipStream_t s = nullptr;
+    if (hipStreamCreateWithFlags(&s, hipStreamNonBlocking) != hipSuccess) s = nullptr;
+    streams[dev] = s;
+    return s;
+}
+
+// ------------------------------------------------------------------------------------
+// plans
+// ------------------------------------------------------------------------------------
+size_t Plan::row_bins() const {
+    if (out_kind == OUT_MEL || out_kind == OUT_MEL_AMP_DB) return n_mels;
+    return NC + 1;
+}
+
+static bool is_pow2(size_t v) { return v && !(v & (v - 1)); }
+
+// mel filterbank -> 16-mel tiles with their bin bands, packed MFMA B operands and a
+// longest-processing-time assignment of (tile, row block) jobs to the 8 waves.
+static int build_mel(Plan* p) {
+    const size_t F = p->NC + 1, M = p->n_mels;
+    const int row = stft_mel_row_stride((int)p->n_fft);
+    const int n_tiles = (int)((M + 15) / 16);
+    std::vector<MelTile> tiles(n_tiles);
+    std::vector<float> packed;
+    for (int t = 0; t < n_tiles; ++t) {
+        long lo = (long)F, hi = 0;
+        for (size_t m = (size_t)t * 16; m < std::min(M, (size_t)t * 16 + 16); ++m)
+            for (size_t k = 0; k < F; ++k)
+                if (p->mel_fb[k * M + m] != 0.0f) {
+                    lo = std::min(lo, (long)k);
+                    hi = std::max(hi, (long)k + 1);
+                }
+        if (hi <= lo) { lo = 0; hi = 0; }
+        const int klo = (int)(lo & ~3L);
+        const int n_kg = hi > lo ? (int)((hi - klo + 15) / 16) : 0;
+        if (klo + 16 * n_kg > row)
+            return set_error(THESIA_ERR_INVALID_ARG, "mel band exceeds the LDS row");
+        tiles[t] = MelTile{klo, n_kg, (int)(packed.size() / 4), 0};
+        for (int kg = 0; kg < n_kg; ++kg)
+            for (int l = 0; l < 64; ++l)
+                for (int s = 0; s < 4; ++s) {
+                    const size_t k = (size_t)klo + 16 * kg + 4 * s + (l >> 4);
+                    const size_t m = (size_t)t * 16 + (l & 15);
+                    packed.push_back((k < F && m < M) ? p->mel_fb[k * M + m] : 0.0f);
+                }
+    }
+    if (packed.empty()) packed.assign(4, 0.0f);
+    const int rb_count = p->tile_frames / 16;
+    struct Job { int id, cost; };
+    std::vector<Job> jobs;
+    for (int t = 0; t < n_tiles; ++t)
+        for (int rb = 0; rb < rb_count; ++rb) jobs.push_back({t * rb_count + rb, tiles[t].n_kg + 2});
+    std::stable_sort(jobs.begin(), jobs.end(), [](const Job& a, const Job& b) { return a.cost > b.cost; });
+    const int W = 8;
+    std::vector<std::vector<int>> lists(W);
+    std::vector<long> load(W, 0);
+    for (const Job& jb : jobs) {
+        int w = (int)(std::min_element(load.begin(), load.end()) - load.begin());
+        lists[w].push_back(jb.id);
+        load[w] += jb.cost;
+    }
+    size_t mx = 0;
+    for (auto& l : lists) mx = std::max(mx, l.size());
+    const int max_jobs = (int)mx + 1;
+    std::vector<int> flat((size_t)W * max_jobs, -1);
+    for (int w = 0; w < W; ++w)
+        for (size_t i = 0; i < lists[w].size(); ++i) flat[(size_t)w * max_jobs + i] = lists[w][i];
+    int rc = p->mel_tiles.upload(tiles.data(), tiles.size() * sizeof(MelTile));
+    if (!rc) rc = p->mel_w.upload(packed.data(), packed.size() * sizeof(float));
+    if (!rc) rc = p->wave_jobs.upload(flat.data(), flat.size() * sizeof(int));
+    p->n_mel_tiles = n_tiles;
+    p->max_jobs = max_jobs;
+    return rc;
+}
+
+int plan_create(const thesia_plan_desc& d, Plan** out) {
+    *out = nullptr;
+    if (!is_pow2(d.n_fft) || d.n_fft < 2 || d.n_fft > 4096)
+        return set_error(THESIA_ERR_UNSUPPORTED, "n_fft must be a power of two in [2, 4096]");
+    if (d.win_length == 0 || d.win_length > d.n_fft)
+        return set_error(THESIA_ERR_INVALID_ARG, "win_length must be in [1, n_fft]");
+    if (d.hop_length == 0) return set_error(THESIA_ERR_INVALID_ARG, "hop_length must be > 0");
+    if (d.output < THESIA_OUT_COMPLEX || d.output > THESIA_OUT_MEL_AMP_DB)
+        return set_error(THESIA_ERR_INVALID_ARG, "unknown output kind");
+    Plan* p = new Plan();
+    p->desc = d;
+    p->desc.window = nullptr;
+    p->desc.mel_fb = nullptr;
+    p->out_kind = d.output;
+    p->n_fft = d.n_fft;
+    p->NC = d.n_fft / 2;
+    p->win = d.win_length;
+    p->hop = d.hop_length;
+    p->pad_left = (d.n_fft - d.win_length) / 2;  // lib.rs:400
+    // window: given, or hann(win, false) / n_fft (lib.rs:138-140, :407)
+    if (d.window) {
+        p->window.assign(d.window, d.window + d.win_length);
+    } else {
+        p->window = hann(d.win_length, false);
+        for (auto& w : p->window) w = w / (float)d.n_fft;
+    }
+    std::vector<float> wpad(d.n_fft, 0.0f);
+    for (size_t k = 0; k < d.win_length; ++k) wpad[p->pad_left + k] = p->window[k];
+    // W_NC^m, m < NC (f64-evaluated like rustfft's twiddles) and the realfft sin_cos table
+    std::vector<float> tw(2 * std::max<size_t>(p->NC, 1));
+    for (size_t m = 0; m < p->NC; ++m) {
+        const double ang = -2.0 * 3.14159265358979323846 * (double)m / (double)p->NC;
+        tw[2 * m] = (float)std::cos(ang);
+        tw[2 * m + 1] = (float)std::sin(ang);
+    }
+    std::vector<float> sc = rfft_sin_cos(d.n_fft);
+    const bool power = d.output == THESIA_OUT_POWER || d.output == THESIA_OUT_POWER_DB;
+    p->log_amin = power ? log10f(1e-36f) : log10f(1e-18f);  // decibel.rs:7-8, :43
+    stft_kernel_info((int)d.n_fft, d.output, 0, &p->lds_bytes, &p->tile_frames, nullptr);
+    int rc = p->wpad.upload(wpad.data(), wpad.size() * sizeof(float));
+    if (!rc) rc = p->tw.upload(tw.data(), tw.size() * sizeof(float));
+    if (!rc) rc = p->sincos.upload(sc.data(), sc.size() * sizeof(float));
+    if (!rc && (d.output == THESIA_OUT_MEL || d.output == THESIA_OUT_MEL_AMP_DB)) {
+        const size_t F = p->NC + 1;
+        if (d.mel_fb) {
+            if (d.n_mels == 0) rc = set_error(THESIA_ERR_INVALID_ARG, "custom mel_fb needs n_mels");
+            else { p->n_mels = d.n_mels; p->mel_fb.assign(d.mel_fb, d.mel_fb + F * d.n_mels); }
+        } else if (d.n_mels == 0) {
+            size_t nm = 0;
+            p->mel_fb = calc_mel_fb_default(d.sr, d.n_fft, &nm);  // mel.rs:87-99
+            p->n_mels = nm;
+            if (nm == 0) rc = set_error(THESIA_ERR_INVALID_ARG, "no valid mel filterbank");
+        } else {
+            p->n_mels = d.n_mels;
+            p->mel_fb = calc_mel_fb(d.sr, d.n_fft, d.n_mels, d.fmin, d.fmax, true);
+        }
+        if (!rc) rc = build_mel(p);
+    }
+    if (rc) {
+        delete p;
+        return rc;
+    }
+    *out = p;
+    return THESIA_OK;
+}
+
+// ------------------------------------------------------------------------------------
+// batches
+// ------------------------------------------------------------------------------------
+Batch::~Batch() {
+    if (ev0) (void)hipEventDestroy(ev0);
+    if (ev1) (void)hipEventDestroy(ev1);
+}
+
+int batch_create(Plan* plan, const thesia_batch_desc& d, Batch** out) {
+    *out = nullptr;
+    if (!plan) return set_error(THESIA_ERR_INVALID_ARG, "null plan");
+    if (d.channels == 0) return set_error(THESIA_ERR_INVALID_ARG, "channels must be > 0");
+    if (d.input_format != THESIA_IN_F32 && d.input_format != THESIA_IN_S16)
+        return set_error(THESIA_ERR_INVALID_ARG, "unknown input format");
+    if (d.n_tracks == 0 || d.n_tracks > (size_t)0x7fffffff)
+        return set_error(THESIA_ERR_INVALID_ARG, "n_tracks must be in [1, 2^31)");
+    if (!d.d_input || !d.d_output || !d.track_offset || !d.track_len)
+        return set_error(THESIA_ERR_INVALID_ARG, "null pointer in batch description");
+    Batch* b = new Batch();
+    b->plan = plan;
+    b->desc = d;
+    b->in_off.assign(d.track_offset, d.track_offset + d.n_tracks);
+    b->len.assign(d.track_len, d.track_len + d.n_tracks);
+    b->frame0.resize(d.n_tracks + 1);
+    uint64_t acc = 0;
+    for (size_t i = 0; i < d.n_tracks; ++i) {
+        b->frame0[i] = acc;
+        const uint64_t T = stft_n_frames(b->len[i], plan->win, plan->hop);
+        if (T == 0) {
+            delete b;
+            return set_error(THESIA_ERR_TOO_SHORT,
+                             "track " + std::to_string(i) + " is too short for win_length " +
+                                 std::to_string(plan->win) + " (the reference panics, lib.rs:413)");
+        }
+        acc += T;
+    }
+    b->frame0[d.n_tracks] = acc;
+    b->total_frames = acc;
+    int rc = b->d_in_off.upload(b->in_off.data(), b->in_off.size() * 8);
+    if (!rc) rc = b->d_len.upload(b->len.data(), b->len.size() * 8);
+    if (!rc) rc = b->d_frame0.upload(b->frame0.data(), b->frame0.size() * 8);
+    if (rc) {
+        delete b;
+        return rc;
+    }
+    StftLaunch& L = b->launch;
+    L.n_fft = (int)plan->n_fft;
+    L.win = (int)plan->win;
+    L.hop = (int)plan->hop;
+    L.pad_left = (int)plan->pad_left;
+    L.out_kind = plan->out_kind;
+    L.in_format = d.input_format;
+    L.channels = (int)d.channels;
+    L.fold = (d.channels > 1 || d.fold_mono || d.input_format == THESIA_IN_S16) ? 1 : 0;
+    L.in = d.d_input;
+    L.trk_in_off = b->d_in_off.as<uint64_t>();
+    L.trk_len = b->d_len.as<uint64_t>();
+    L.trk_frame0 = b->d_frame0.as<uint64_t>();
+    L.n_tracks = (int)d.n_tracks;
+    L.total_frames = b->total_frames;
+    L.wpad = plan->wpad.as<float>();
+    L.tw1 = plan->tw.as<float2>();
+    L.sincos = plan->sincos.as<float2>();
+    L.log_amin = plan->log_amin;
+    L.n_mels = (int)plan->n_mels;
+    L.n_mel_tiles = plan->n_mel_tiles;
+    L.mel_tiles = plan->mel_tiles.as<MelTile>();
+    L.mel_w = plan->mel_w.as<float4>();
+    L.wave_jobs = plan->wave_jobs.as<int>();
+    L.max_jobs = plan->max_jobs;
+    L.out = d.d_output;
+    if (hipEventCreate(&b->ev0) != hipSuccess || hipEventCreate(&b->ev1) != hipSuccess) {
+        delete b;
+        return set_error(THESIA_ERR_DEVICE, "hipEventCreate failed");
+    }
+    *out = b;
+    return THESIA_OK;
+}
+
+int batch_run(Batch* b, hipStream_t s) {
+    if (!s) s = default_stream();
+    const int rc = launch_stft(b->launch, s);
+    if (rc == -2) return set_error(THESIA_ERR_UNSUPPORTED, "unsupported n_fft");
+    if (rc) return set_error(THESIA_ERR_DEVICE, std::string("stft launch failed: ") +
+                                                    hipGetErrorString(hipGetLastError()));
+    return THESIA_OK;
+}
+
+// ------------------------------------------------------------------------------------
+// display helpers
+// ------------------------------------------------------------------------------------
+int minmax_device(const float* d_x, uint64_t n, float* mx, float* mn, bool* nan, hipStream_t s) {
+    if (n == 0) {  // ndarray-stats EmptyInput -> unwrap_or(-inf / +inf), lib.rs:198-199
+        *mx = -INFINITY;
+        *mn = INFINITY;
+        *nan = false;
+        return THESIA_OK;
+    }
+    int nblk = (int)std::min<uint64_t>((n + 255) / 256, 1024);
+    DevBuf part, flag;
+    int rc = part.alloc((size_t)nblk * 2 * sizeof(float));
+    if (!rc) rc = flag.alloc(sizeof(int));
+    if (rc) return rc;
+    THESIA_HIP(hipMemsetAsync(flag.p, 0, sizeof(int), s));
+    if (launch_minmax(d_x, n, part.as<float>(), flag.as<int>(), nblk, s))
+        return set_error(THESIA_ERR_DEVICE, "minmax launch failed");
+    std::vector<float> h((size_t)nblk * 2);
+    int hf = 0;
+    THESIA_HIP(hipMemcpyAsync(h.data(), part.p, h.size() * sizeof(float), hipMemcpyDeviceToHost, s));
+    THESIA_HIP(hipMemcpyAsync(&hf, flag.p, sizeof(int), hipMemcpyDeviceToHost, s));
+    THESIA_HIP(hipStreamSynchronize(s));
+    float a = -INFINITY, b = INFINITY;
+    for (int i = 0; i < nblk; ++i) {
+        a = fmaxf(a, h[2 * i]);
+        b = fminf(b, h[2 * i + 1]);
+    }
+    *mx = a;
+    *mn = b;
+    *nan = hf != 0;
+    return THESIA_OK;
+}
+
+static std::vector<uint8_t> colormap_bytes() {
+    std::vector<uint8_t> c(30);
+    for (int i = 0; i < 10; ++i)
+        for (int k = 0; k < 3; ++k) c[i * 3 + k] = kColormap[i][k];
+    return c;
+}
+
+int grey_to_rgb_device(const float* d_grey, uint32_t w, uint32_t h, uint32_t nw, uint32_t nh,
+                       uint8_t* d_rgb, hipStream_t s) {
+    if (nw == 0 || nh == 0) return THESIA_OK;
+    if (w == 0 || h == 0) return set_error(THESIA_ERR_INVALID_ARG, "empty grey image");
+    // image 0.23.12 resize: vertical_sample (h -> nh) into f32, then horizontal (w -> nw)
+    Taps vt = lanczos3_taps(h, nh), ht = lanczos3_taps(w, nw);
+    DevBuf vl, vc, vo, vw, hl, hc, ho, hw, tmp, cmap;
+    std::vector<uint8_t> cm = colormap_bytes();
+    int rc = vl.upload(vt.left.data(), vt.left.size() * 4);
+    if (!rc) rc = vc.upload(vt.count.data(), vt.count.size() * 4);
+    if (!rc) rc = vo.upload(vt.offset.data(), vt.offset.size() * 4);
+    if (!rc) rc = vw.upload(vt.weights.data(), vt.weights.size() * 4);
+    if (!rc) rc = hl.upload(ht.left.data(), ht.left.size() * 4);
+    if (!rc) rc = hc.upload(ht.count.data(), ht.count.size() * 4);
+    if (!rc) rc = ho.upload(ht.offset.data(), ht.offset.size() * 4);
+    if (!rc) rc = hw.upload(ht.weights.data(), ht.weights.size() * 4);
+    if (!rc) rc = tmp.alloc((size_t)w * nh * sizeof(float));
+    if (!rc) rc = cmap.upload(cm.data(), cm.size());
+    if (rc) return rc;
+    if (launch_resize_v(d_grey, w, h, nh, vl.as<int32_t>(), vc.as<int32_t>(), vo.as<int32_t>(),
+                        vw.as<float>(), vt.max_taps, tmp.as<float>(), s))
+        return set_error(THESIA_ERR_DEVICE, "resize_v launch failed");
+    if (launch_resize_h_rgb(tmp.as<float>(), w, nh, nw, hl.as<int32_t>(), hc.as<int32_t>(),
+                            ho.as<int32_t>(), hw.as<float>(), ht.max_taps, cmap.as<uint8_t>(),
+                            d_rgb, s))
+        return set_error(THESIA_ERR_DEVICE, "resize_h launch failed");
+    THESIA_HIP(hipStreamSynchronize(s));
+    return THESIA_OK;
+}
+
+int wav_to_image_device(const float* d_wav, uint64_t n, uint32_t nwidth, uint32_t nheight,
+                        float amp_min, float amp_max, uint8_t* d_out, int* panicked,
+                        hipStream_t s) {
+    *panicked = 0;
+    if (nwidth == 0 || nheight == 0) return THESIA_OK;
+    const float spp = (float)n / (float)nwidth;  // display.rs:74
+    DevBuf up, flag;
+    uint64_t n_up = 0;
+    int rc = flag.alloc(sizeof(int));
+    if (rc) return rc;
+    THESIA_HIP(hipMemsetAsync(flag.p, 0, sizeof(int), s));
+    if (spp < 1.0f) {  // display.rs:76-91 linear upsampling by factor
+        const uint32_t factor = (uint32_t)ceilf(1.0f / spp);
+        n_up = (uint64_t)factor * n;
+        rc = up.alloc(n_up * sizeof(float));
+        if (rc) return rc;
+        if (launch_wav_upsample(d_wav, n, factor, up.as<float>(), s))
+            return set_error(THESIA_ERR_DEVICE, "wav upsample launch failed");
+    }
+    if (launch_wav_image(d_wav, n, up.p ? up.as<float>() : nullptr, n_up, nwidth, nheight, spp,
+                         amp_min, amp_max, d_out, flag.as<int>(), s))
+        return set_error(THESIA_ERR_DEVICE, "wav image launch failed");
+    THESIA_HIP(hipMemcpyAsync(panicked, flag.p, sizeof(int), hipMemcpyDeviceToHost, s));
+    THESIA_HIP(hipStreamSynchronize(s));
+    return THESIA_OK;
+}
+
+const int16_t* synth_lut_host() {
+    static std::vector<int16_t> lut;
+    static std::once_flag once;
+    std::call_once(once, [] {
+        lut.resize(4096);
+        for (int i = 0; i < 4096; ++i)
+            lut[i] = (int16_t)std::lround(32767.0 * std::sin(2.0 * 3.14159265358979323846 * i / 4096.0));
+    });
+    return lut.data();
+}
+
+}  // namespace thesia

@@ -1,0 +1,93 @@
+// engine.hpp -- internal C++ runtime of libthesia: errors, device buffers, streams, plans
+// (per-(sr, win, hop, n_fft, output) tables resident in HBM) and batches (track
+// descriptors resident in HBM, one launch per pass).
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <string>
+#include <vector>
+
+#include "../../include/thesia.h"
+#include "kernels.hpp"
+
+namespace thesia {
+
+// ---- errors: thread-local message + status code (never abort across the C ABI) ----
+int set_error(int code, const std::string& msg);
+void clear_error();
+const char* last_error();
+
+#define THESIA_HIP(expr)                                                                 \
+    do {                                                                                 \
+        hipError_t e_ = (expr);                                                          \
+        if (e_ != hipSuccess)                                                            \
+            return ::thesia::set_error(THESIA_ERR_DEVICE,                                \
+                                       std::string(#expr ": ") + hipGetErrorString(e_)); \
+    } while (0)
+
+// ---- device buffer (move-only RAII) ----
+struct DevBuf {
+    void* p = nullptr;
+    size_t bytes = 0;
+    DevBuf() = default;
+    DevBuf(const DevBuf&) = delete;
+    DevBuf& operator=(const DevBuf&) = delete;
+    DevBuf(DevBuf&& o) noexcept : p(o.p), bytes(o.bytes) { o.p = nullptr; o.bytes = 0; }
+    DevBuf& operator=(DevBuf&& o) noexcept {
+        if (this != &o) { release(); p = o.p; bytes = o.bytes; o.p = nullptr; o.bytes = 0; }
+        return *this;
+    }
+    ~DevBuf() { release(); }
+    void release();
+    int alloc(size_t n);
+    int upload(const void* host, size_t n);  // alloc + copy (synchronous)
+    template <class T> T* as() const { return static_cast<T*>(p); }
+};
+
+hipStream_t default_stream();  // library stream of the current device
+
+// ---- plan ----
+struct Plan {
+    thesia_plan_desc desc{};
+    int out_kind = 0;
+    size_t n_fft = 0, NC = 0, win = 0, hop = 0, pad_left = 0;
+    size_t n_mels = 0;
+    std::vector<float> window;  // [win]
+    std::vector<float> mel_fb;  // [F, n_mels]
+    float log_amin = 0.f;
+    int tile_frames = 0, lds_bytes = 0;
+    DevBuf wpad, tw, sincos, mel_tiles, mel_w, wave_jobs;
+    int n_mel_tiles = 0, max_jobs = 0;
+    size_t row_bins() const;
+    size_t out_elem_bytes() const { return out_kind == OUT_COMPLEX ? 8 : 4; }
+};
+int plan_create(const thesia_plan_desc& d, Plan** out);
+
+// ---- batch ----
+struct Batch {
+    Plan* plan = nullptr;
+    thesia_batch_desc desc{};
+    std::vector<uint64_t> in_off, len, frame0;
+    DevBuf d_in_off, d_len, d_frame0;
+    uint64_t total_frames = 0;
+    StftLaunch launch{};
+    hipEvent_t ev0 = nullptr, ev1 = nullptr;
+    ~Batch();
+};
+int batch_create(Plan* plan, const thesia_batch_desc& d, Batch** out);
+int batch_run(Batch* b, hipStream_t s);
+
+// ---- display helpers on device buffers (used by MultiTrack and the C ABI) ----
+int grey_to_rgb_device(const float* d_grey, uint32_t w, uint32_t h, uint32_t nw, uint32_t nh,
+                       uint8_t* d_rgb, hipStream_t s);
+int wav_to_image_device(const float* d_wav, uint64_t n, uint32_t nwidth, uint32_t nheight,
+                        float amp_min, float amp_max, uint8_t* d_out, int* panicked,
+                        hipStream_t s);
+int minmax_device(const float* d_x, uint64_t n, float* mx, float* mn, bool* nan, hipStream_t s);
+
+// sine LUT for the synthetic generator (host copy + lazily uploaded device copy)
+const int16_t* synth_lut_host();
+
+}  // namespace thesia

@@ -1,0 +1,99 @@
+// kernels.hpp -- host-visible launch descriptors for the HIP kernels (no HIP types leak
+// out of libthesia's C ABI; these structs are internal to the library).
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstddef>
+#include <cstdint>
+
+namespace thesia {
+
+enum OutKind : int {
+    OUT_COMPLEX = 0,   // X[t, k] complex (perform_stft, lib.rs:388-471)
+    OUT_MAG = 1,       // |X| (lib.rs:124)
+    OUT_POWER = 2,     // |X|^2 (num-complex norm_sqr)
+    OUT_AMP_DB = 3,    // amp_to_db_default(|X|) (lib.rs:127, decibel.rs:79-88)
+    OUT_POWER_DB = 4,  // power_to_db_default(|X|^2) (decibel.rs:91-100)
+    OUT_MEL = 5,       // |X| . mel_fb (lib.rs:131)
+    OUT_MEL_AMP_DB = 6 // amp_to_db_default(|X| . mel_fb) (lib.rs:131-132)
+};
+
+enum InFormat : int {
+    IN_F32 = 0,  // f32 samples, channel-interleaved (audio.rs:33-35 layout)
+    IN_S16 = 1   // s16 PCM, channel-interleaved; value / 2^15 (audio.rs:16-19)
+};
+
+// One mel tile = 16 consecutive mel bands with the bin range their filters touch.
+struct MelTile {
+    int32_t klo;      // first bin (multiple of 4)
+    int32_t n_kg;     // number of 16-bin groups (4 MFMA k-steps each)
+    int32_t w_off;    // offset (in float4) of this tile's packed weights
+    int32_t pad;
+};
+
+struct StftLaunch {
+    // geometry
+    int n_fft = 0, win = 0, hop = 0, pad_left = 0;
+    int out_kind = OUT_AMP_DB;
+    int in_format = IN_F32;
+    int channels = 1;
+    int fold = 0;  // apply the reference's channel-sum fold even for mono (AudioTrack::new)
+    // input / tracks (device pointers)
+    const void* in = nullptr;
+    const uint64_t* trk_in_off = nullptr;  // element offset of each track's first sample
+    const uint64_t* trk_len = nullptr;     // samples per channel
+    const uint64_t* trk_frame0 = nullptr;  // [n_tracks + 1] prefix sum of frame counts
+    int n_tracks = 0;
+    uint64_t total_frames = 0;
+    // tables (device pointers)
+    const float* wpad = nullptr;     // [n_fft] window zero-padded to n_fft
+    const float2* tw1 = nullptr;     // [NC] W_NC^m, m < NC (stage-1 twiddle bases)
+    const float2* sincos = nullptr;  // [NC] realfft untangle table (sin, cos)
+    float log_amin = 0.f;            // log10f(amin), host-computed
+    // mel
+    int n_mels = 0;
+    int n_mel_tiles = 0;
+    const MelTile* mel_tiles = nullptr;
+    const float4* mel_w = nullptr;
+    const int* wave_jobs = nullptr;  // [4][max_jobs], -1 terminated
+    int max_jobs = 0;
+    // output
+    void* out = nullptr;  // packed rows: frame g at out + g * row_elems
+    // scheduling
+    int grid = 0;  // 0 => computed from occupancy
+};
+
+// Returns 0 on success; fills the LDS bytes a block of the chosen kernel uses.
+int launch_stft(const StftLaunch& a, hipStream_t stream);
+int stft_kernel_info(int n_fft, int out_kind, int in_format, int* lds_bytes, int* tile_frames,
+                     int* blocks_per_cu);
+int stft_mel_row_stride(int n_fft);
+
+// ---- display / misc kernels (display_kernels.hip) ----
+int launch_downmix(const void* in, int in_format, int channels, uint64_t n, float* out,
+                   hipStream_t s);
+int launch_minmax(const float* x, uint64_t n, float* partial /*[2*nblk]*/, int* nan_flag,
+                  int nblk, hipStream_t s);
+int launch_spec_to_grey(const float* spec, uint32_t T, uint32_t bins, uint32_t H, float max,
+                        float min, float* grey, hipStream_t s);
+int launch_resize_v(const float* in, uint32_t w, uint32_t h, uint32_t nh, const int32_t* left,
+                    const int32_t* cnt, const int32_t* woff, const float* wts, int max_taps,
+                    float* out, hipStream_t s);
+int launch_resize_h_rgb(const float* in, uint32_t w, uint32_t nh, uint32_t nw,
+                        const int32_t* left, const int32_t* cnt, const int32_t* woff,
+                        const float* wts, int max_taps, const uint8_t* cmap, uint8_t* out,
+                        hipStream_t s);
+int launch_wav_image(const float* wav, uint64_t n, const float* wav_up, uint64_t n_up,
+                     uint32_t nwidth, uint32_t nheight, float spp, float amp_min, float amp_max,
+                     uint8_t* out, int* panicked, hipStream_t s);
+int launch_wav_upsample(const float* wav, uint64_t n, uint32_t factor, float* out,
+                        hipStream_t s);
+int launch_synth_pcm(void* out, int out_format, uint32_t channels, uint64_t n_tracks,
+                     uint64_t n_samples, uint32_t sr, uint64_t seed, const int16_t* sine_lut,
+                     hipStream_t s);
+void synth_phase_coeffs(uint64_t n, uint32_t sr, uint64_t* ph_a, uint64_t* ph_b);
+void synth_host(int16_t* out, uint32_t C, uint64_t track, uint64_t n, uint32_t sr, uint64_t seed,
+                const int16_t* lut);
+
+}  // namespace thesia

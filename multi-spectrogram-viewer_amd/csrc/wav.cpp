@@ -1,0 +1,103 @@
+// wav.cpp -- WAV decoding with hound 3.4 semantics (audio.rs:9-37): integer PCM becomes
+// (x as f32) / 2^(bits-1), float PCM is taken as is, samples stay channel-interleaved.
+// The reference's rodio fallback (FLAC / Vorbis, audio.rs:21-31) is out of scope: such
+// files return THESIA_ERR_UNSUPPORTED.
+#include "wav.hpp"
+
+#include <algorithm>
+#include <cerrno>
+#include <cstdio>
+#include <cstring>
+
+#include "../../include/thesia.h"
+
+namespace thesia {
+
+static uint32_t rd32(const uint8_t* p) { return p[0] | (p[1] << 8) | (p[2] << 16) | ((uint32_t)p[3] << 24); }
+static uint16_t rd16(const uint8_t* p) { return (uint16_t)(p[0] | (p[1] << 8)); }
+
+int read_wav(const std::string& path, WavData* out, std::string* err) {
+    FILE* f = std::fopen(path.c_str(), "rb");
+    if (!f) {
+        const int e = errno;
+        *err = std::string(std::strerror(e)) + " (os error " + std::to_string(e) + ")";
+        return THESIA_ERR_IO;
+    }
+    std::vector<uint8_t> buf;
+    {
+        uint8_t tmp[1 << 16];
+        size_t n;
+        while ((n = std::fread(tmp, 1, sizeof(tmp), f)) > 0) buf.insert(buf.end(), tmp, tmp + n);
+    }
+    std::fclose(f);
+    if (buf.size() < 12 || std::memcmp(buf.data(), "RIFF", 4) || std::memcmp(buf.data() + 8, "WAVE", 4)) {
+        *err = "not a WAV file: the reference's rodio fallback (FLAC/Vorbis) is not supported";
+        return THESIA_ERR_UNSUPPORTED;
+    }
+    size_t pos = 12;
+    bool have_fmt = false;
+    uint16_t fmt_tag = 0, channels = 0, block_align = 0, bits = 0;
+    uint32_t sr = 0;
+    const uint8_t* data = nullptr;
+    size_t data_len = 0;
+    while (pos + 8 <= buf.size()) {
+        const uint8_t* ck = buf.data() + pos;
+        const uint32_t len = rd32(ck + 4);
+        const size_t body = pos + 8;
+        if (!std::memcmp(ck, "fmt ", 4)) {
+            if (len < 16 || body + 16 > buf.size()) break;
+            fmt_tag = rd16(buf.data() + body);
+            channels = rd16(buf.data() + body + 2);
+            sr = rd32(buf.data() + body + 4);
+            block_align = rd16(buf.data() + body + 12);
+            bits = rd16(buf.data() + body + 14);
+            if (fmt_tag == 0xFFFE && len >= 40 && body + 40 <= buf.size())
+                fmt_tag = rd16(buf.data() + body + 24);  // WAVE_FORMAT_EXTENSIBLE sub-format
+            have_fmt = true;
+        } else if (!std::memcmp(ck, "data", 4)) {
+            data = buf.data() + body;
+            data_len = std::min<size_t>(len, buf.size() - body);
+            break;
+        }
+        pos = body + len + (len & 1);
+    }
+    if (!have_fmt || !data || channels == 0 || block_align == 0) {
+        *err = "malformed WAV file (missing fmt or data chunk)";
+        return THESIA_ERR_IO;
+    }
+    const size_t bps = block_align / channels;  // bytes per sample
+    const size_t n_samp = data_len / bps;
+    out->sr = sr;
+    out->channels = channels;
+    out->samples.resize(n_samp);
+    if (fmt_tag == 3) {  // IEEE float
+        if (bits != 32 || bps != 4) {
+            *err = "unsupported float WAV bit depth";
+            return THESIA_ERR_UNSUPPORTED;
+        }
+        std::memcpy(out->samples.data(), data, n_samp * 4);
+    } else if (fmt_tag == 1) {  // integer PCM: (x as f32) / 2^(bits-1), audio.rs:15-19
+        if (bits == 0 || bits > 32 || bps > 4 || bps * 8 < bits) {
+            *err = "unsupported integer WAV bit depth";
+            return THESIA_ERR_UNSUPPORTED;
+        }
+        const float scale = (float)(1u << (bits - 1));
+        for (size_t i = 0; i < n_samp; ++i) {
+            const uint8_t* p = data + i * bps;
+            int32_t v;
+            if (bps == 1) v = (int32_t)p[0] - 128;  // 8-bit WAV is unsigned
+            else if (bps == 2) v = (int16_t)rd16(p);
+            else if (bps == 3) v = (int32_t)((uint32_t)p[0] << 8 | (uint32_t)p[1] << 16 | (uint32_t)p[2] << 24) >> 8;
+            else v = (int32_t)rd32(p);
+            out->samples[i] = (float)v / scale;
+        }
+    } else {
+        *err = "unsupported WAV format tag " + std::to_string(fmt_tag);
+        return THESIA_ERR_UNSUPPORTED;
+    }
+    // audio.rs:32-34: truncate to whole frames
+    out->samples.resize((out->samples.size() / channels) * channels);
+    return THESIA_OK;
+}
+
+}  // namespace thesia

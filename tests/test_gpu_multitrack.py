@@ -1,0 +1,121 @@
+"""MultiTrack (lib.rs:72-365) on the GPU vs the oracle pipeline, on the reference's own
+sample WAVs (excerpts committed under tests/golden) and synthetic audio."""
+import os
+import wave
+
+import numpy as np
+import pytest
+
+import oracle_ffi as O
+import thesia
+from tolerances import DB_MAX, DB_P9999, db_clamped_err
+
+pytestmark = pytest.mark.gpu
+
+TAGS = ["8k", "16k", "22k05", "24k", "44k1"]
+
+
+@pytest.fixture(scope="module")
+def excerpts(golden_dir):
+    z = np.load(os.path.join(golden_dir, "samples_excerpt.npz"))
+    out = {t: (z[f"pcm_{t}"].astype(np.float32) / 32768.0, int(z[f"sr_{t}"])) for t in TAGS}
+    from scipy.signal import resample_poly  # the 48 kHz substitute
+    x24 = z["pcm_24k"].astype(np.float64)
+    x48 = np.clip(np.round(resample_poly(x24, 2, 1)), -32768, 32767).astype(np.int16)
+    out["48k"] = (x48.astype(np.float32) / 32768.0, 48000)
+    return out
+
+
+def _write_wav(path, pcm_f32, sr):
+    i16 = np.round(pcm_f32 * 32768.0).astype(np.int16)
+    with wave.open(path, "wb") as w:
+        w.setnchannels(1)
+        w.setsampwidth(2)
+        w.setframerate(sr)
+        w.writeframes(i16.tobytes())
+
+
+def _oracle_spec(x, sr, freq_scale):
+    win, hop, n_fft = O.track_params(sr)
+    w = O.hann(win) / np.float32(n_fft)
+    X = O.perform_stft(x, win, hop, n_fft, window=w.astype(np.float32))
+    mag = O.norm(X)
+    if freq_scale == thesia.FreqScale.Mel:
+        mag = O.dot(mag, O.calc_mel_fb_default(sr, n_fft))
+    return O.amp_to_db_default(mag)
+
+
+@pytest.mark.parametrize("scale", [thesia.FreqScale.Mel, thesia.FreqScale.Linear])
+def test_multitrack_specs_and_images(excerpts, tmp_path, scale):
+    mt = thesia.MultiTrack(freq_scale=scale)
+    tags = list(excerpts)
+    paths = []
+    for t in tags:
+        p = str(tmp_path / f"sample_{t}.wav")
+        _write_wav(p, *excerpts[t])
+        paths.append(p)
+    changed = mt.add_tracks(list(range(len(tags))), "\n".join(paths))
+    assert changed and len(mt) == len(tags)
+    specs = {}
+    for i, t in enumerate(tags):
+        x, sr = excerpts[t]
+        assert mt.get_sr(i) == sr and mt.get_path(i) == paths[i]
+        assert mt.get_filename(i) == f"sample_{t}.wav"
+        got = mt.get_spec(i)
+        ref = _oracle_spec(x, sr, scale)
+        assert got.shape == ref.shape
+        mx, p = db_clamped_err(got, ref)
+        assert mx <= DB_MAX and p <= DB_P9999, (t, mx, p)
+        specs[i] = got
+    # global range (lib.rs:194-209) from the device specs
+    gmax = min(max(float(s.max()) for s in specs.values()), 0.0)
+    gmin = max(min(float(s.min()) for s in specs.values()), gmax - 120.0)
+    assert mt.get_max_db() == np.float32(gmax) and mt.get_min_db() == np.float32(gmin)
+    max_sr = max(sr for _, sr in excerpts.values())
+    for i, t in enumerate(tags):
+        sr = excerpts[t][1]
+        if scale == thesia.FreqScale.Mel:
+            up = np.float32(O.hz_to_mel(max_sr / 2.0)) / np.float32(O.hz_to_mel(sr / 2.0))
+        else:
+            up = np.float32(max_sr) / np.float32(sr)
+        grey = mt.get_grey(i)
+        ref_grey = O.spec_to_grey(specs[i], float(up), float(mt.get_max_db()), float(mt.get_min_db()))
+        assert np.array_equal(grey, ref_grey)
+        img = np.frombuffer(mt.get_spec_image(i, 100.0, 250), np.uint8)
+        nwidth = int(np.float32(100.0) * np.float32(len(excerpts[t][0])) / np.float32(sr))
+        ref_img, _ = O.grey_to_rgb(grey, nwidth, 250)
+        assert img.size == ref_img.size and np.array_equal(img.reshape(ref_img.shape), ref_img)
+        wimg = np.frombuffer(mt.get_wav_image(i, 100.0, 120, -1.0, 1.0), np.uint8)
+        ref_w, _ = O.wav_to_image(excerpts[t][0], nwidth, 120, -1.0, 1.0)
+        assert np.array_equal(wimg.reshape(ref_w.shape), ref_w)
+    hz = mt.get_frequency_hz(0, 0.5)
+    assert np.isfinite(hz) and hz > 0
+    assert mt.get_max_sec() == max(np.float32(len(x)) / np.float32(sr) for x, sr in excerpts.values())
+
+
+def test_remove_track_and_changed_semantics(excerpts):
+    mt = thesia.MultiTrack()
+    x8, sr8 = excerpts["8k"]
+    x44, sr44 = excerpts["44k1"]
+    assert mt.add_tracks_pcm([0], [x8], [sr8])
+    # re-adding the same audio under another id changes neither range nor max sr; the new
+    # track must still get a grey image (the reference forgets it, lib.rs:230 -> :297 panic)
+    changed = mt.add_tracks_pcm([1], [x8], [sr8])
+    assert not changed
+    assert mt.get_grey(1).shape == mt.get_grey(0).shape
+    assert mt.add_tracks_pcm([2], [x44], [sr44])  # higher sr -> up_ratio change
+    assert mt.remove_track(2)
+    with pytest.raises(thesia.ThesiaError):
+        mt.remove_track(2)
+    with pytest.raises(thesia.ThesiaError):
+        mt.get_spec_image(7, 100.0, 100)
+
+
+def test_add_tracks_error_leaves_state_unchanged(tmp_path, excerpts):
+    mt = thesia.MultiTrack()
+    p = str(tmp_path / "a.wav")
+    _write_wav(p, *excerpts["16k"])
+    with pytest.raises(thesia.ThesiaError) as e:
+        mt.add_tracks([0, 1], p + "\n" + str(tmp_path / "missing.wav"))
+    assert e.value.code == -2 and "os error" in str(e.value)
+    assert len(mt) == 0
