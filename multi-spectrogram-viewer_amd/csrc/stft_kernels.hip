@@ -137,6 +137,7 @@ stft_kernel(StftLaunch a, uint64_t tiles_per_block) {
     constexpr int TILE = MEL ? G::MEL_TILE : G::PASS_FRAMES;
     constexpr int PASSES = MEL ? G::MEL_PASSES : 1;
     constexpr int TB = G::TB, TA = G::TA;
+    constexpr int LCH = P < 8 ? P : 8;  // fast-path load chunk (registers pinned per chunk)
 
     extern __shared__ __attribute__((aligned(16))) float lds[];
     float* wtab = lds;                    // [2*NC] window zero-padded to n_fft
@@ -194,29 +195,29 @@ stft_kernel(StftLaunch a, uint64_t tiles_per_block) {
                 if (interior && INF == IN_F32 && C == 1 && !fold && ((base + start) & 1) == 0) {
                     const float2* src = reinterpret_cast<const float2*>(
                         static_cast<const float*>(a.in) + base + start) + j;
-                    static_for<0, P / 8>([&](auto gc) {
+                    static_for<0, P / LCH>([&](auto gc) {
                         constexpr int g8 = decltype(gc)::value;
-                        static_for<0, 8>([&](auto ic) {
-                            constexpr int n1 = 8 * g8 + decltype(ic)::value;
+                        static_for<0, LCH>([&](auto ic) {
+                            constexpr int n1 = LCH * g8 + decltype(ic)::value;
                             const int m = L * n1 + j;
                             const float2 x = src[L * n1];
                             v[n1] = make_float2(x.x * wtab[2 * m], x.y * wtab[2 * m + 1]);
                         });
-                        pin_range<8 * g8, 8 * g8 + 8>(v);
+                        pin_range<LCH * g8, LCH * g8 + LCH>(v);
                     });
                 } else if (interior && INF == IN_F32 && C == 2 && fold && ((base + 2 * start) & 3) == 0) {
                     const float4* src = reinterpret_cast<const float4*>(
                         static_cast<const float*>(a.in) + base + 2 * start) + j;
-                    static_for<0, P / 8>([&](auto gc) {
+                    static_for<0, P / LCH>([&](auto gc) {
                         constexpr int g8 = decltype(gc)::value;
-                        static_for<0, 8>([&](auto ic) {
-                            constexpr int n1 = 8 * g8 + decltype(ic)::value;
+                        static_for<0, LCH>([&](auto ic) {
+                            constexpr int n1 = LCH * g8 + decltype(ic)::value;
                             const int m = L * n1 + j;
                             const float4 x = src[L * n1];
                             const float s0 = (0.0f + x.x) + x.y, s1 = (0.0f + x.z) + x.w;
                             v[n1] = make_float2(s0 * wtab[2 * m], s1 * wtab[2 * m + 1]);
                         });
-                        pin_range<8 * g8, 8 * g8 + 8>(v);
+                        pin_range<LCH * g8, LCH * g8 + LCH>(v);
                     });
                 } else {
                     // edge / unaligned / generic-format frames: a runtime loop writes the
