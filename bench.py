@@ -5,7 +5,7 @@ Workload ("C4 per-GPU shard", BASELINE.json configs[3]): every rank owns 1000 sy
 reference's in-memory format after open_audio_file, audio.rs:9-37), resident in HBM before
 timing. One step = one pass of the hot path over the rank's whole shard: channel-sum
 downmix (lib.rs:42) -> reflect framing + Hann/n_fft (lib.rs:367-440) -> real FFT
-(realfft.rs) -> |X| (lib.rs:124) -> 128-band mel MFMA projection (lib.rs:131) -> amp dB
+(realfft.rs) -> |X| (lib.rs:124) -> 128-band mel projection (per-lane fma rounds) (lib.rs:131) -> amp dB
 (decibel.rs:79-88), n_fft 2048 / hop 512 / win 2048, one kernel launch. Files shard across
 ranks with no data-path collective ("weak" scaling: per-GPU work is fixed).
 
@@ -48,6 +48,8 @@ def parse():
     p.add_argument("--output", choices=["mel_db", "amp_db", "power_db", "complex"], default="mel_db")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-workers", type=int, default=16)
+    p.add_argument("--variants", default="", help="experiment: comma list of THESIA_STFT_VARIANT "
+                   "values to A/B (interleaved rounds, one process); prints per-variant kernel ms")
     return p.parse_args()
 
 
@@ -161,6 +163,19 @@ def main():
     t1 = time.perf_counter()
     dt = max_over_ranks(pg, (t1 - t0) / args.steps)
 
+    if args.variants:
+        vs = [int(v) for v in args.variants.split(",")]
+        res = {v: [] for v in vs}
+        for _ in range(5):  # interleaved rounds (methodology rule 24)
+            for v in vs:
+                os.environ["THESIA_STFT_VARIANT"] = str(v)
+                batch.run_timed(1)
+                res[v].append(batch.run_timed(3) / 3)
+        os.environ["THESIA_STFT_VARIANT"] = "0"
+        if rank == 0:
+            print(json.dumps({"variants_kernel_ms": {str(v): {"median": float(np.median(t)), "min": float(min(t))}
+                                                     for v, t in res.items()}}), flush=True)
+
     # kernel duration from HIP events on the launch stream (roofline numerator / denominator)
     kms = batch.run_timed(max(args.steps, 5)) / max(args.steps, 5)
     kms = max_over_ranks(pg, kms)
@@ -200,7 +215,7 @@ def main():
             "unit": "GB/s",
             "frac": achieved / HBM_PEAK_GBS,
             "traffic": traffic_from_profile(wkey),
-            "kernel": "thesia::stft_kernel (fused downmix+frame+window+rFFT+|X|+mel MFMA+dB)",
+            "kernel": "thesia::stft_kernel (fused downmix+frame+window+rFFT+|X|+mel+dB)",
             "kernel_ms": kms,
             "algorithmic_bytes_per_launch": abytes,
         }

@@ -74,62 +74,53 @@ size_t Plan::row_bins() const {
 
 static bool is_pow2(size_t v) { return v && !(v & (v - 1)); }
 
-// mel filterbank -> 16-mel tiles with their bin bands, packed MFMA B operands and a
-// longest-processing-time assignment of (tile, row block) jobs to the 8 waves.
+// mel filterbank -> per-lane fma rounds (stft_kernels.hip mel_rounds). Round r gives lane j
+// of a frame mel r*L + j; the round runs len_r = the longest nonzero band among its mels,
+// each lane from k0 = min(band start, F - len_r) so the window stays inside the |X| row.
+// The weights are the filterbank's own f32 values (zeros outside the band), so the lane's
+// fma chain over k ascending matches the dense k-ascending dot term for term.
 static int build_mel(Plan* p) {
     const size_t F = p->NC + 1, M = p->n_mels;
-    const int row = stft_mel_row_stride((int)p->n_fft);
-    const int n_tiles = (int)((M + 15) / 16);
-    std::vector<MelTile> tiles(n_tiles);
-    std::vector<float> packed;
-    for (int t = 0; t < n_tiles; ++t) {
-        long lo = (long)F, hi = 0;
-        for (size_t m = (size_t)t * 16; m < std::min(M, (size_t)t * 16 + 16); ++m)
+    int L = 0;
+    if (stft_kernel_info((int)p->n_fft, nullptr, nullptr, &L) != 0 || L <= 0)
+        return set_error(THESIA_ERR_UNSUPPORTED, "unsupported n_fft");
+    const size_t R = (M + L - 1) / L;
+    std::vector<int2> rounds(R);
+    std::vector<int> k0((size_t)R * L, 0);
+    std::vector<float> wt;
+    size_t rows = 0;
+    for (size_t r = 0; r < R; ++r) {
+        std::vector<long> lo(L, 0), hi(L, 0);
+        long len = 0;
+        for (int j = 0; j < L; ++j) {
+            const size_t m = r * L + j;
+            if (m >= M) continue;
+            long l0 = -1, h0 = -1;
             for (size_t k = 0; k < F; ++k)
                 if (p->mel_fb[k * M + m] != 0.0f) {
-                    lo = std::min(lo, (long)k);
-                    hi = std::max(hi, (long)k + 1);
+                    if (l0 < 0) l0 = (long)k;
+                    h0 = (long)k + 1;
                 }
-        if (hi <= lo) { lo = 0; hi = 0; }
-        const int klo = (int)(lo & ~3L);
-        const int n_kg = hi > lo ? (int)((hi - klo + 15) / 16) : 0;
-        if (klo + 16 * n_kg > row)
-            return set_error(THESIA_ERR_INVALID_ARG, "mel band exceeds the LDS row");
-        tiles[t] = MelTile{klo, n_kg, (int)(packed.size() / 4), 0};
-        for (int kg = 0; kg < n_kg; ++kg)
-            for (int l = 0; l < 64; ++l)
-                for (int s = 0; s < 4; ++s) {
-                    const size_t k = (size_t)klo + 16 * kg + 4 * s + (l >> 4);
-                    const size_t m = (size_t)t * 16 + (l & 15);
-                    packed.push_back((k < F && m < M) ? p->mel_fb[k * M + m] : 0.0f);
-                }
+            if (l0 >= 0) { lo[j] = l0; hi[j] = h0; len = std::max(len, h0 - l0); }
+        }
+        rounds[r] = int2{(int)rows, (int)len};
+        wt.resize((rows + (size_t)len) * L, 0.0f);
+        for (int j = 0; j < L; ++j) {
+            const size_t m = r * L + j;
+            const long s = std::min(lo[j], (long)F - len);
+            k0[r * L + j] = (int)s;
+            if (m >= M) continue;
+            for (long it = 0; it < len; ++it)
+                wt[(rows + (size_t)it) * L + j] = p->mel_fb[(size_t)(s + it) * M + m];
+        }
+        rows += (size_t)len;
     }
-    if (packed.empty()) packed.assign(4, 0.0f);
-    const int rb_count = p->tile_frames / 16;
-    struct Job { int id, cost; };
-    std::vector<Job> jobs;
-    for (int t = 0; t < n_tiles; ++t)
-        for (int rb = 0; rb < rb_count; ++rb) jobs.push_back({t * rb_count + rb, tiles[t].n_kg + 2});
-    std::stable_sort(jobs.begin(), jobs.end(), [](const Job& a, const Job& b) { return a.cost > b.cost; });
-    const int W = 8;
-    std::vector<std::vector<int>> lists(W);
-    std::vector<long> load(W, 0);
-    for (const Job& jb : jobs) {
-        int w = (int)(std::min_element(load.begin(), load.end()) - load.begin());
-        lists[w].push_back(jb.id);
-        load[w] += jb.cost;
-    }
-    size_t mx = 0;
-    for (auto& l : lists) mx = std::max(mx, l.size());
-    const int max_jobs = (int)mx + 1;
-    std::vector<int> flat((size_t)W * max_jobs, -1);
-    for (int w = 0; w < W; ++w)
-        for (size_t i = 0; i < lists[w].size(); ++i) flat[(size_t)w * max_jobs + i] = lists[w][i];
-    int rc = p->mel_tiles.upload(tiles.data(), tiles.size() * sizeof(MelTile));
-    if (!rc) rc = p->mel_w.upload(packed.data(), packed.size() * sizeof(float));
-    if (!rc) rc = p->wave_jobs.upload(flat.data(), flat.size() * sizeof(int));
-    p->n_mel_tiles = n_tiles;
-    p->max_jobs = max_jobs;
+    if (wt.empty()) wt.assign(1, 0.0f);
+    int rc = p->mel_round.upload(rounds.data(), std::max<size_t>(R, 1) * sizeof(int2));
+    if (!rc) rc = p->mel_k0.upload(k0.data(), std::max<size_t>(k0.size(), 1) * sizeof(int));
+    if (!rc) rc = p->mel_wt.upload(wt.data(), wt.size() * sizeof(float));
+    p->mel_rounds = (int)R;
+    p->mel_wt_rows = rows;
     return rc;
 }
 
@@ -171,7 +162,6 @@ int plan_create(const thesia_plan_desc& d, Plan** out) {
     std::vector<float> sc = rfft_sin_cos(d.n_fft);
     const bool power = d.output == THESIA_OUT_POWER || d.output == THESIA_OUT_POWER_DB;
     p->log_amin = power ? log10f(1e-36f) : log10f(1e-18f);  // decibel.rs:7-8, :43
-    stft_kernel_info((int)d.n_fft, d.output, 0, &p->lds_bytes, &p->tile_frames, nullptr);
     int rc = p->wpad.upload(wpad.data(), wpad.size() * sizeof(float));
     if (!rc) rc = p->tw.upload(tw.data(), tw.size() * sizeof(float));
     if (!rc) rc = p->sincos.upload(sc.data(), sc.size() * sizeof(float));
@@ -190,6 +180,9 @@ int plan_create(const thesia_plan_desc& d, Plan** out) {
             p->mel_fb = calc_mel_fb(d.sr, d.n_fft, d.n_mels, d.fmin, d.fmax, true);
         }
         if (!rc) rc = build_mel(p);
+    }
+    if (!rc) {
+        stft_kernel_info((int)d.n_fft, &p->lds_bytes, &p->tile_frames, nullptr);
     }
     if (rc) {
         delete p;
@@ -264,11 +257,10 @@ int batch_create(Plan* plan, const thesia_batch_desc& d, Batch** out) {
     L.sincos = plan->sincos.as<float2>();
     L.log_amin = plan->log_amin;
     L.n_mels = (int)plan->n_mels;
-    L.n_mel_tiles = plan->n_mel_tiles;
-    L.mel_tiles = plan->mel_tiles.as<MelTile>();
-    L.mel_w = plan->mel_w.as<float4>();
-    L.wave_jobs = plan->wave_jobs.as<int>();
-    L.max_jobs = plan->max_jobs;
+    L.mel_rounds = plan->mel_rounds;
+    L.mel_round = plan->mel_round.as<int2>();
+    L.mel_k0 = plan->mel_k0.as<int>();
+    L.mel_wt = plan->mel_wt.as<float>();
     L.out = d.d_output;
     if (hipEventCreate(&b->ev0) != hipSuccess || hipEventCreate(&b->ev1) != hipSuccess) {
         delete b;

@@ -58,8 +58,9 @@ struct Plan {
     std::vector<float> mel_fb;  // [F, n_mels]
     float log_amin = 0.f;
     int tile_frames = 0, lds_bytes = 0;
-    DevBuf wpad, tw, sincos, mel_tiles, mel_w, wave_jobs;
-    int n_mel_tiles = 0, max_jobs = 0;
+    DevBuf wpad, tw, sincos, mel_round, mel_k0, mel_wt;
+    int mel_rounds = 0;
+    size_t mel_wt_rows = 0;  // padded band lengths summed over the rounds
     size_t row_bins() const;
     size_t out_elem_bytes() const { return out_kind == OUT_COMPLEX ? 8 : 4; }
 };

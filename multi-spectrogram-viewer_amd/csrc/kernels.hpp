@@ -24,14 +24,6 @@ enum InFormat : int {
     IN_S16 = 1   // s16 PCM, channel-interleaved; value / 2^15 (audio.rs:16-19)
 };
 
-// One mel tile = 16 consecutive mel bands with the bin range their filters touch.
-struct MelTile {
-    int32_t klo;      // first bin (multiple of 4)
-    int32_t n_kg;     // number of 16-bin groups (4 MFMA k-steps each)
-    int32_t w_off;    // offset (in float4) of this tile's packed weights
-    int32_t pad;
-};
-
 struct StftLaunch {
     // geometry
     int n_fft = 0, win = 0, hop = 0, pad_left = 0;
@@ -51,24 +43,24 @@ struct StftLaunch {
     const float2* tw1 = nullptr;     // [NC] W_NC^m, m < NC (stage-1 twiddle bases)
     const float2* sincos = nullptr;  // [NC] realfft untangle table (sin, cos)
     float log_amin = 0.f;            // log10f(amin), host-computed
-    // mel
+    // mel (lib.rs:131): round r gives lane j of a frame mel r*L + j (L = lanes per frame);
+    // the lane runs bins mel_k0[r*L + j] + it, it < mel_round[r].y, with weights
+    // mel_wt[(mel_round[r].x + it) * L + j] (zero outside the filter's band)
     int n_mels = 0;
-    int n_mel_tiles = 0;
-    const MelTile* mel_tiles = nullptr;
-    const float4* mel_w = nullptr;
-    const int* wave_jobs = nullptr;  // [4][max_jobs], -1 terminated
-    int max_jobs = 0;
+    int mel_rounds = 0;
+    const int2* mel_round = nullptr;  // [rounds] {first weight row, band length}
+    const int* mel_k0 = nullptr;      // [rounds][L]
+    const float* mel_wt = nullptr;    // [sum of band lengths][L]
     // output
     void* out = nullptr;  // packed rows: frame g at out + g * row_elems
     // scheduling
     int grid = 0;  // 0 => computed from occupancy
 };
 
-// Returns 0 on success; fills the LDS bytes a block of the chosen kernel uses.
+// Returns 0 on success, -2 for an unsupported n_fft.
 int launch_stft(const StftLaunch& a, hipStream_t stream);
-int stft_kernel_info(int n_fft, int out_kind, int in_format, int* lds_bytes, int* tile_frames,
-                     int* blocks_per_cu);
-int stft_mel_row_stride(int n_fft);
+// LDS bytes / frames per block pass / lanes per frame of the kernel for n_fft.
+int stft_kernel_info(int n_fft, int* lds_bytes, int* tile_frames, int* lanes_per_frame);
 
 // ---- display / misc kernels (display_kernels.hip) ----
 int launch_downmix(const void* in, int in_format, int channels, uint64_t n, float* out,
