@@ -3,6 +3,7 @@
 
 #include <algorithm>
 #include <cmath>
+#include <cstdlib>
 #include <map>
 #include <mutex>
 
@@ -124,6 +125,62 @@ static int build_mel(Plan* p) {
     return rc;
 }
 
+// The same projection in stft2_kernel's float4 layout (stft2_kernels.hip mel4): lane j of
+// round r starts at k0 = a multiple of 4 (its band start rounded down, moved left so that the
+// round's len4 float4 steps stay inside the zero-padded row of F4 = ceil4(F) bins).
+static int build_mel4(Plan* p) {
+    const long F = (long)p->NC + 1, F4 = (F + 3) / 4 * 4;
+    const size_t M = p->n_mels;
+    int L = 0;
+    if (stft_kernel_info((int)p->n_fft, nullptr, nullptr, &L) != 0 || L <= 0)
+        return set_error(THESIA_ERR_UNSUPPORTED, "unsupported n_fft");
+    const size_t R = (M + L - 1) / L;
+    std::vector<int2> rounds(R);
+    std::vector<int> k0((size_t)R * L, 0);
+    std::vector<float> wt;
+    size_t rows = 0;
+    for (size_t r = 0; r < R; ++r) {
+        std::vector<long> lo(L, 0), hi(L, 0);
+        long len4 = 0;
+        for (int j = 0; j < L; ++j) {
+            const size_t m = r * L + j;
+            if (m >= M) continue;
+            long l0 = -1, h0 = -1;
+            for (long k = 0; k < F; ++k)
+                if (p->mel_fb[(size_t)k * M + m] != 0.0f) {
+                    if (l0 < 0) l0 = k;
+                    h0 = k + 1;
+                }
+            if (l0 >= 0) {
+                lo[j] = l0 / 4 * 4;
+                hi[j] = h0;
+                len4 = std::max(len4, (h0 - lo[j] + 3) / 4);
+            }
+        }
+        rounds[r] = int2{(int)rows, (int)len4};
+        wt.resize((rows + (size_t)len4) * L * 4, 0.0f);
+        for (int j = 0; j < L; ++j) {
+            const size_t m = r * L + j;
+            const long s = std::min(lo[j], F4 - 4 * len4);
+            k0[r * L + j] = (int)s;
+            if (m >= M) continue;
+            for (long it = 0; it < len4; ++it)
+                for (int u = 0; u < 4; ++u) {
+                    const long k = s + 4 * it + u;
+                    wt[((rows + (size_t)it) * L + j) * 4 + u] = k < F ? p->mel_fb[(size_t)k * M + m] : 0.0f;
+                }
+        }
+        rows += (size_t)len4;
+    }
+    if (wt.empty()) wt.assign(4, 0.0f);
+    int rc = p->mel4_round.upload(rounds.data(), std::max<size_t>(R, 1) * sizeof(int2));
+    if (!rc) rc = p->mel4_k0.upload(k0.data(), std::max<size_t>(k0.size(), 1) * sizeof(int));
+    if (!rc) rc = p->mel4_wt.upload(wt.data(), wt.size() * sizeof(float));
+    p->mel4_rounds = (int)R;
+    p->mel4_wt_rows = rows;
+    return rc;
+}
+
 int plan_create(const thesia_plan_desc& d, Plan** out) {
     *out = nullptr;
     if (!is_pow2(d.n_fft) || d.n_fft < 2 || d.n_fft > 4096)
@@ -159,11 +216,29 @@ int plan_create(const thesia_plan_desc& d, Plan** out) {
         tw[2 * m] = (float)std::cos(ang);
         tw[2 * m + 1] = (float)std::sin(ang);
     }
+    // stft2's lane-major stage-1 twiddle bases: row b < TB holds W_NC^{j*b}, row TB + a holds
+    // W_NC^{j*TB*a}, column j < L (the same f64-rounded values as tw)
+    std::vector<float> tw2;
+    {
+        int L = 0;
+        if (stft_kernel_info((int)d.n_fft, nullptr, nullptr, &L) == 0 && L > 0 && p->NC >= (size_t)L) {
+            const size_t P = p->NC / (size_t)L, TB = P < 8 ? P : 8, TA = P / TB;
+            tw2.resize(2 * (TB + TA) * (size_t)L);
+            for (size_t row = 0; row < TB + TA; ++row)
+                for (size_t j = 0; j < (size_t)L; ++j) {
+                    const size_t e = (row < TB ? j * row : j * TB * (row - TB)) % p->NC;
+                    tw2[2 * (row * L + j)] = tw[2 * e];
+                    tw2[2 * (row * L + j) + 1] = tw[2 * e + 1];
+                }
+        }
+        if (tw2.empty()) tw2.assign(2, 0.0f);
+    }
     std::vector<float> sc = rfft_sin_cos(d.n_fft);
     const bool power = d.output == THESIA_OUT_POWER || d.output == THESIA_OUT_POWER_DB;
     p->log_amin = power ? log10f(1e-36f) : log10f(1e-18f);  // decibel.rs:7-8, :43
     int rc = p->wpad.upload(wpad.data(), wpad.size() * sizeof(float));
     if (!rc) rc = p->tw.upload(tw.data(), tw.size() * sizeof(float));
+    if (!rc) rc = p->tw2.upload(tw2.data(), tw2.size() * sizeof(float));
     if (!rc) rc = p->sincos.upload(sc.data(), sc.size() * sizeof(float));
     if (!rc && (d.output == THESIA_OUT_MEL || d.output == THESIA_OUT_MEL_AMP_DB)) {
         const size_t F = p->NC + 1;
@@ -180,9 +255,13 @@ int plan_create(const thesia_plan_desc& d, Plan** out) {
             p->mel_fb = calc_mel_fb(d.sr, d.n_fft, d.n_mels, d.fmin, d.fmax, true);
         }
         if (!rc) rc = build_mel(p);
+        if (!rc) rc = build_mel4(p);
     }
     if (!rc) {
-        stft_kernel_info((int)d.n_fft, &p->lds_bytes, &p->tile_frames, nullptr);
+        const char* v1 = getenv("THESIA_STFT_V1");  // experiment: force the general kernel
+        p->use_v2 = stft2_supports((int)d.n_fft) && !(v1 && atoi(v1) != 0);
+        if (p->use_v2) stft2_kernel_info((int)d.n_fft, &p->lds_bytes, &p->tile_frames, nullptr);
+        else stft_kernel_info((int)d.n_fft, &p->lds_bytes, &p->tile_frames, nullptr);
     }
     if (rc) {
         delete p;
@@ -255,13 +334,31 @@ int batch_create(Plan* plan, const thesia_batch_desc& d, Batch** out) {
     L.wpad = plan->wpad.as<float>();
     L.tw1 = plan->tw.as<float2>();
     L.sincos = plan->sincos.as<float2>();
+    L.tw2 = plan->tw2.as<float2>();
     L.log_amin = plan->log_amin;
     L.n_mels = (int)plan->n_mels;
     L.mel_rounds = plan->mel_rounds;
     L.mel_round = plan->mel_round.as<int2>();
     L.mel_k0 = plan->mel_k0.as<int>();
     L.mel_wt = plan->mel_wt.as<float>();
+    L.mel4_rounds = plan->mel4_rounds;
+    L.mel4_rows = (int)plan->mel4_wt_rows;
+    L.mel4_round = plan->mel4_round.as<int2>();
+    L.mel4_k0 = plan->mel4_k0.as<int>();
+    L.mel4_wt = plan->mel4_wt.as<float4>();
     L.out = d.d_output;
+    // kernel choice: the streaming kernel for its geometry, else the 4-waves/SIMD kernel for
+    // its sizes, else the general one. THESIA_STFT_KERNEL=1|2|3 forces one (experiments).
+    b->kernel = plan->use_v2 ? 2 : 1;
+    if (plan->use_v2 && stft3_supports((int)plan->n_fft, (int)plan->win, (int)plan->hop,
+                                       d.input_format, (int)d.channels))
+        b->kernel = 3;
+    if (const char* e = getenv("THESIA_STFT_KERNEL")) {
+        const int k = atoi(e);
+        if (k == 1 || (k == 2 && stft2_supports((int)plan->n_fft))) b->kernel = k;
+        if (k == 3 && stft3_supports((int)plan->n_fft, (int)plan->win, (int)plan->hop,
+                                     d.input_format, (int)d.channels)) b->kernel = 3;
+    }
     if (hipEventCreate(&b->ev0) != hipSuccess || hipEventCreate(&b->ev1) != hipSuccess) {
         delete b;
         return set_error(THESIA_ERR_DEVICE, "hipEventCreate failed");
@@ -272,7 +369,10 @@ int batch_create(Plan* plan, const thesia_batch_desc& d, Batch** out) {
 
 int batch_run(Batch* b, hipStream_t s) {
     if (!s) s = default_stream();
-    const int rc = launch_stft(b->launch, s);
+    int rc = -2;
+    if (b->kernel == 3) rc = launch_stft3(b->launch, s);
+    if (rc == -2 && b->kernel >= 2) rc = launch_stft2(b->launch, s);
+    if (rc == -2) rc = launch_stft(b->launch, s);
     if (rc == -2) return set_error(THESIA_ERR_UNSUPPORTED, "unsupported n_fft");
     if (rc) return set_error(THESIA_ERR_DEVICE, std::string("stft launch failed: ") +
                                                     hipGetErrorString(hipGetLastError()));

@@ -58,9 +58,13 @@ struct Plan {
     std::vector<float> mel_fb;  // [F, n_mels]
     float log_amin = 0.f;
     int tile_frames = 0, lds_bytes = 0;
-    DevBuf wpad, tw, sincos, mel_round, mel_k0, mel_wt;
+    DevBuf wpad, tw, tw2, sincos, mel_round, mel_k0, mel_wt;
     int mel_rounds = 0;
     size_t mel_wt_rows = 0;  // padded band lengths summed over the rounds
+    DevBuf mel4_round, mel4_k0, mel4_wt;  // stft2_kernel layout (float4 steps)
+    int mel4_rounds = 0;
+    size_t mel4_wt_rows = 0;
+    bool use_v2 = false;  // stft2_kernel runs this plan (n_fft 256..2048)
     size_t row_bins() const;
     size_t out_elem_bytes() const { return out_kind == OUT_COMPLEX ? 8 : 4; }
 };
@@ -74,6 +78,7 @@ struct Batch {
     DevBuf d_in_off, d_len, d_frame0;
     uint64_t total_frames = 0;
     StftLaunch launch{};
+    int kernel = 1;  // 1 stft_kernel, 2 stft2_kernel, 3 stft3_kernel (streaming)
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     ~Batch();
 };

@@ -42,6 +42,7 @@ struct StftLaunch {
     const float* wpad = nullptr;     // [n_fft] window zero-padded to n_fft
     const float2* tw1 = nullptr;     // [NC] W_NC^m, m < NC (stage-1 twiddle bases)
     const float2* sincos = nullptr;  // [NC] realfft untangle table (sin, cos)
+    const float2* tw2 = nullptr;     // stft2: [TB + TA][L] W_NC^{j*b}, W_NC^{j*TB*a} (lane-major)
     float log_amin = 0.f;            // log10f(amin), host-computed
     // mel (lib.rs:131): round r gives lane j of a frame mel r*L + j (L = lanes per frame);
     // the lane runs bins mel_k0[r*L + j] + it, it < mel_round[r].y, with weights
@@ -51,6 +52,14 @@ struct StftLaunch {
     const int2* mel_round = nullptr;  // [rounds] {first weight row, band length}
     const int* mel_k0 = nullptr;      // [rounds][L]
     const float* mel_wt = nullptr;    // [sum of band lengths][L]
+    // the same projection for stft2_kernel (4 bins per step): lane j runs float4 steps
+    // it < mel4_round[r].y from bin mel4_k0[r*L + j] (a multiple of 4), weights
+    // mel4_wt[(mel4_round[r].x + it) * L + j] (float4, zero outside the band)
+    int mel4_rounds = 0;
+    int mel4_rows = 0;  // float4 rows of mel4_wt (x L lanes)
+    const int2* mel4_round = nullptr;
+    const int* mel4_k0 = nullptr;
+    const float4* mel4_wt = nullptr;
     // output
     void* out = nullptr;  // packed rows: frame g at out + g * row_elems
     // scheduling
@@ -59,6 +68,14 @@ struct StftLaunch {
 
 // Returns 0 on success, -2 for an unsupported n_fft.
 int launch_stft(const StftLaunch& a, hipStream_t stream);
+// stft2_kernel (n_fft 256..2048): 0 on success, -2 when n_fft is not one of its sizes.
+int launch_stft2(const StftLaunch& a, hipStream_t stream);
+bool stft2_supports(int n_fft);
+int stft2_kernel_info(int n_fft, int* lds_bytes, int* tile_frames, int* lanes_per_frame);
+// stft3_kernel (streaming; win = n_fft, hop = n_fft/4, f32 mono/stereo): 0 on success, -2 when
+// the geometry is not its own (or the mel rows do not fit LDS).
+int launch_stft3(const StftLaunch& a, hipStream_t stream);
+bool stft3_supports(int n_fft, int win, int hop, int in_format, int channels);
 // LDS bytes / frames per block pass / lanes per frame of the kernel for n_fft.
 int stft_kernel_info(int n_fft, int* lds_bytes, int* tile_frames, int* lanes_per_frame);
 

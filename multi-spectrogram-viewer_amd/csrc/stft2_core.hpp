@@ -1,0 +1,245 @@
+// stft2_core.hpp -- building blocks of the 4-waves/SIMD and streaming STFT kernels
+// (stft2_kernels.hip, stft3_kernels.hip): geometry, in-place two-stage FFT with the b64
+// transpose, paired realfft untangle, float4 mel projection. Design notes: stft2_kernels.hip.
+#pragma once
+
+#include "stft_common.hpp"
+
+namespace thesia {
+
+constexpr int round_up_mod64(int v, int r) {
+    while (v % 64 != r) ++v;
+    return v;
+}
+
+template <int NC>
+struct Geo2 {
+    static constexpr int L = geo_L(NC);
+    static constexpr int P = NC / L;
+    static constexpr int CPL = P / L;
+    static constexpr int FPW = 64 / L;
+    static constexpr int F = NC + 1;
+    static constexpr int F4 = (F + 3) / 4 * 4;
+    static constexpr int S = L + 2;  // transpose row stride
+    static constexpr int XREG = P * S;
+    // frames of one 32-lane group sit 2L floats apart mod 64: their b64 reads interleave
+    static constexpr int RS = round_up_mod64(XREG, L >= 32 ? 0 : (2 * L) % 64);
+    static constexpr int PASS_FRAMES = kWaves * FPW;
+    static constexpr int WIN_FLOATS = 2 * NC;
+    static constexpr int TB = Geo<NC>::TB, TA = Geo<NC>::TA;
+    static constexpr int LDS_BYTES = (WIN_FLOATS + PASS_FRAMES * RS) * 4;
+    static_assert(P % L == 0 && L >= 8, "stft2 geometry");
+    static_assert(XREG >= F4 && XREG >= NC, "the |X| row and the load staging must fit a region");
+    static_assert(RS % 4 == 0, "16-byte aligned regions");
+    static_assert(2 * LDS_BYTES <= 163840, "two blocks per CU");
+};
+
+// Interior frames of f32 mono / stereo input straight from HBM (8 / 16 B per lane); the
+// stereo sum is x[ch0] + x[ch1] (lib.rs:42; the fold's leading 0.0 + only differs for -0).
+template <int NC, int INF>
+__device__ __forceinline__ bool load_direct2(const StftLaunch& a, int j, int64_t start, int64_t n,
+                                             uint64_t base, int C, bool fold, const float* wtab,
+                                             float2 (&v)[Geo2<NC>::P]) {
+    constexpr int L = Geo2<NC>::L, P = Geo2<NC>::P;
+    if constexpr (INF != IN_F32) {
+        return false;
+    } else {
+        if (!(a.pad_left == 0 && a.win == 2 * NC && start >= 0 && start + 2 * NC <= n)) return false;
+        if (C == 1 && !fold && ((base + start) & 1) == 0) {
+            const float2* src = reinterpret_cast<const float2*>(static_cast<const float*>(a.in) + base + start) + j;
+            const float2* wp = reinterpret_cast<const float2*>(wtab) + j;
+            static_for<0, P / 8>([&](auto gc) {  // 8 loads in flight per chunk (VGPR budget)
+                constexpr int g8 = decltype(gc)::value;
+                static_for<0, 8>([&](auto ic) {
+                    constexpr int n1 = 8 * g8 + decltype(ic)::value;
+                    const float2 x = src[L * n1];
+                    const float2 w = wp[L * n1];
+                    v[n1] = make_float2(x.x * w.x, x.y * w.y);
+                });
+                pin_range<8 * g8, 8 * g8 + 8>(v);
+            });
+            return true;
+        }
+        if (C == 2 && fold && ((base + 2 * start) & 3) == 0) {
+            const float4* src = reinterpret_cast<const float4*>(static_cast<const float*>(a.in) + base + 2 * start) + j;
+            const float2* wp = reinterpret_cast<const float2*>(wtab) + j;
+            static_for<0, P / 8>([&](auto gc) {
+                constexpr int g8 = decltype(gc)::value;
+                static_for<0, 8>([&](auto ic) {
+                    constexpr int n1 = 8 * g8 + decltype(ic)::value;
+                    const float4 x = src[L * n1];
+                    const float2 w = wp[L * n1];
+                    v[n1] = make_float2((x.x + x.y) * w.x, (x.z + x.w) * w.y);
+                });
+                pin_range<8 * g8, 8 * g8 + 8>(v);
+            });
+            return true;
+        }
+        return false;
+    }
+}
+
+// Stage-1 DFT_P + twiddles W_NC^{j k1}, LDS transpose (re then im), stage-2 DFT_L, in place.
+// On return v[c*L + ce_pos(L, k2)] = Z[k1 + P*k2] / 2 with k1 = j + c*L.
+template <int NC>
+__device__ __forceinline__ void fft2(float2 (&v)[Geo2<NC>::P], float* region, int j,
+                                     const float2 (&twb)[Geo2<NC>::TB],
+                                     const float2 (&twa)[Geo2<NC>::TA]) {
+    using G = Geo2<NC>;
+    constexpr int L = G::L, P = G::P, TB = G::TB, S = G::S, CPL = G::CPL;
+    pin(v);
+    dif_fft<P, 1, 0, P>(v);
+    pin(v);
+    static_for<0, P>([&](auto kc) {
+        constexpr int k1 = decltype(kc)::value;
+        constexpr int b = k1 % TB, aa = k1 / TB;
+        constexpr int pk = ce_pos(P, k1);
+        float2 x = v[pk];
+        if constexpr (b != 0) x = cmul(x, twb[b]);
+        if constexpr (aa != 0) x = cmul(x, twa[aa]);
+        v[pk] = x;
+    });
+#pragma unroll
+    for (int e = 0; e < 2; ++e) {
+        wave_lds_sync();
+        static_for<0, P>([&](auto kc) {
+            constexpr int k1 = decltype(kc)::value;
+            constexpr int pk = ce_pos(P, k1);
+            region[k1 * S + j] = e == 0 ? v[pk].x : v[pk].y;
+        });
+        wave_lds_sync();
+        static_for<0, CPL>([&](auto cc) {
+            constexpr int c = decltype(cc)::value;
+            const float2* row = reinterpret_cast<const float2*>(region + (j + c * L) * S);
+            static_for<0, L / 2>([&](auto qc) {
+                constexpr int q = 2 * decltype(qc)::value;
+                const float2 t = row[q / 2];
+                if (e == 0) { v[c * L + q].x = t.x; v[c * L + q + 1].x = t.y; }
+                else        { v[c * L + q].y = t.x; v[c * L + q + 1].y = t.y; }
+            });
+        });
+    }
+    wave_lds_sync();
+    pin(v);
+    static_for<0, CPL>([&](auto cc) {
+        constexpr int c = decltype(cc)::value;
+        dif_fft<L, 1, c * L, P>(v);
+    });
+    pin(v);
+}
+
+// W_NC^{j*b}, W_NC^{j*TB*aa} from the lane-major table a.tw2 ([TB + TA][L]: one base and
+// immediate offsets).
+template <int NC>
+__device__ __forceinline__ void load_tw2(const StftLaunch& a, int j, float2 (&twb)[Geo2<NC>::TB],
+                                         float2 (&twa)[Geo2<NC>::TA]) {
+    constexpr int L = Geo2<NC>::L, TB = Geo2<NC>::TB, TA = Geo2<NC>::TA;
+    const float2* twp = a.tw2 + j;
+#pragma unroll
+    for (int b = 0; b < TB; ++b) twb[b] = twp[b * L];
+#pragma unroll
+    for (int aa = 0; aa < TA; ++aa) twa[aa] = twp[(TB + aa) * L];
+}
+
+// realfft untangle on bin pairs; calls epi(k, re, im) for every bin this lane produces
+// (k = j + c*L + P*t and NC - k for t < L/2; lane 0 also the self-paired bin NC/2).
+template <int NC, class Epi>
+__device__ __forceinline__ void untangle2(const float2 (&v)[Geo2<NC>::P], int j, int partner,
+                                          const float2 (&ub)[Geo2<NC>::CPL], Epi&& epi) {
+    using G = Geo2<NC>;
+    constexpr int L = G::L, P = G::P, CPL = G::CPL;
+    const bool lane0 = j == 0;
+    auto pair = [&](float2 b, float2 r, float s, float co, int k, bool both) {
+        const float ar = b.x + r.x, ai = b.y - r.y;  // A = Z_k + conj Z_{NC-k}
+        const float br = b.x - r.x, bi = b.y + r.y;  // B = Z_k - conj Z_{NC-k}
+        const float p = __builtin_fmaf(co, br, s * bi);     // (p, q) = (co - i s) B
+        const float q = __builtin_fmaf(co, bi, -(s * br));
+        epi(k, ar + q, ai - p);
+        if (both) epi(NC - k, ar - q, -ai - p);
+    };
+    static_for<0, CPL>([&](auto cc) {
+        constexpr int c = decltype(cc)::value;
+        static_for<0, L / 2>([&](auto tc) {
+            constexpr int t = decltype(tc)::value;
+            constexpr int pb = c * L + ce_pos(L, t);
+            constexpr int ps = (CPL - 1 - c) * L + ce_pos(L, L - 1 - t);
+            const float2 b = v[pb];
+            const float2 send = v[ps];
+            float2 r;
+            r.x = __shfl(send.x, partner, 64);
+            r.y = __shfl(send.y, partner, 64);
+            // lane 0 pairs inside its own registers: Z[(CPL-c) % CPL][c ? L-1-t : (L-t) % L]
+            constexpr int c0 = (CPL - c) % CPL;
+            constexpr int k20 = c == 0 ? (L - t) % L : L - 1 - t;
+            constexpr int po = c0 * L + ce_pos(L, k20);
+            const float2 own = v[po];
+            r.x = lane0 ? own.x : r.x;
+            r.y = lane0 ? own.y : r.y;
+            // (sin, cos)(pi k / NC) = base(j + cL) rotated by pi t / L
+            float s, co;
+            if constexpr (t == 0) {
+                s = ub[c].x;
+                co = ub[c].y;
+            } else {
+                constexpr float cb = ce_tw_re(t, 2 * L);
+                constexpr float sb = -ce_tw_im(t, 2 * L);
+                s = __builtin_fmaf(ub[c].x, cb, ub[c].y * sb);
+                co = __builtin_fmaf(ub[c].y, cb, -(ub[c].x * sb));
+            }
+            pair(b, r, s, co, j + c * L + P * t, true);
+        });
+    });
+    if (lane0) {  // k = NC/2 pairs with itself: (sin, cos)(pi/2) from the base sin_cos[0]
+        constexpr int ph = ce_pos(L, L / 2);
+        const float2 b = v[ph];
+        constexpr float cb = ce_tw_re(L / 2, 2 * L);
+        constexpr float sb = -ce_tw_im(L / 2, 2 * L);
+        const float s = __builtin_fmaf(ub[0].x, cb, ub[0].y * sb);
+        const float co = __builtin_fmaf(ub[0].y, cb, -(ub[0].x * sb));
+        pair(b, b, s, co, NC / 2, false);
+    }
+}
+
+// lib.rs:131-132 on the |X| row in `region`: round r gives lane j mel r*L + j.
+// wt: the float4 weight rows (a.mel4_wt in HBM, or its copy in LDS).
+template <int NC>
+__device__ __forceinline__ void mel4(const StftLaunch& a, const float* region, const float4* wt,
+                                     int j, uint64_t g, bool valid) {
+    constexpr int L = Geo2<NC>::L;
+    constexpr int U = 4;
+    const int n_mels = a.n_mels;
+    const bool db = a.out_kind == OUT_MEL_AMP_DB;
+    float* out = static_cast<float*>(a.out) + g * (uint64_t)n_mels;
+    for (int r = 0; r < a.mel4_rounds; ++r) {
+        const int2 rd = a.mel4_round[r];  // {first float4 row, float4 steps}: wave-uniform
+        const float4* xp = reinterpret_cast<const float4*>(region + a.mel4_k0[r * L + j]);
+        const float4* wp = wt + (size_t)rd.x * L + j;
+        float acc = 0.0f;
+        int it = 0;
+        for (; it + U <= rd.y; it += U) {
+            float4 w[U], x[U];
+#pragma unroll
+            for (int u = 0; u < U; ++u) w[u] = wp[(it + u) * L];
+#pragma unroll
+            for (int u = 0; u < U; ++u) x[u] = xp[it + u];
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                acc = __builtin_fmaf(x[u].x, w[u].x, acc);
+                acc = __builtin_fmaf(x[u].y, w[u].y, acc);
+                acc = __builtin_fmaf(x[u].z, w[u].z, acc);
+                acc = __builtin_fmaf(x[u].w, w[u].w, acc);
+            }
+        }
+        for (; it < rd.y; ++it) {
+            const float4 w = wp[it * L], x = xp[it];
+            acc = __builtin_fmaf(x.x, w.x, acc);
+            acc = __builtin_fmaf(x.y, w.y, acc);
+            acc = __builtin_fmaf(x.z, w.z, acc);
+            acc = __builtin_fmaf(x.w, w.w, acc);
+        }
+        const int m = r * L + j;
+        if (valid && m < n_mels) out[m] = db ? db_of(acc, a.log_amin, 1e-18f, 20.0f) : acc;
+    }
+}
+
+}  // namespace thesia

@@ -1,0 +1,267 @@
+// stft3_kernels.hip -- the streaming STFT kernel for the canonical geometry of the batch
+// configs (win = n_fft, hop = n_fft/4, f32 mono or stereo input).
+//
+// Contract as stft_kernel / stft2_kernel (one launch = downmix -> reflect framing x Hann/n_fft
+// -> real FFT -> |X| -> linear kinds or mel + dB for every frame of a batch). What changes is
+// how frames meet their input: each 64-lane wave runs FPW independent frame STREAMS, and a
+// stream walks consecutive frames g0..g1 of the batch. Lane j of a frame holds the points
+// m = L*n1 + j (samples 2m, 2m+1 from the frame start), and the frame start moves by
+// hop = 2*L*SH samples (SH = P/4) from one frame to the next, so the next frame's point n1 is
+// this frame's point n1 + SH in the SAME lane. The downmixed, unwindowed samples of the
+// current frame stay in registers (raw[P]); a new frame shifts them by SH and needs only its
+// hop of new samples: SH loads per lane (16 B stereo / 8 B mono), issued one frame ahead.
+// HBM and L2 then see each input byte once (not n_fft/hop = 4 times), and the loads' latency
+// hides under the previous frame's FFT. Frames whose new samples cross a track end (reflect
+// padding, lib.rs:410-435) or start a stream / track reload all n_fft samples (direct or
+// reflected). The mel weights are copied into LDS once per block.
+#include "stft2_core.hpp"
+
+namespace thesia {
+
+template <int NC>
+struct Geo3 {
+    using G2 = Geo2<NC>;
+    static constexpr int L = G2::L, P = G2::P, FPW = G2::FPW, RS = G2::RS;
+    static constexpr int SH = P / 4;                      // points per lane a hop moves
+    static constexpr int STREAMS = kWaves * FPW;          // streams (= frames in flight) per block
+    static constexpr int BASE_FLOATS = G2::WIN_FLOATS + STREAMS * RS;
+    static_assert(P % 4 == 0, "hop = n_fft/4 must move whole points per lane");
+};
+
+// Reflect-padded, downmixed samples of a frame (no window): the uniform rule of
+// load_frame_generic (stft_common.hpp) for win = n_fft.
+template <int NC>
+__device__ __forceinline__ void load_raw_generic(const StftLaunch& a, float* region, int j,
+                                                 int64_t start, int64_t n, uint64_t base, int C,
+                                                 bool fold, float2 (&raw)[Geo2<NC>::P]) {
+    constexpr int L = Geo2<NC>::L, P = Geo2<NC>::P;
+#pragma unroll
+    for (int e = 0; e < 2; ++e) {
+        wave_lds_sync();
+        for (int n1 = 0; n1 < P; ++n1) {
+            const int m = L * n1 + j;
+            int64_t i = start + 2 * m + e;
+            if (i < 0) i = -i;
+            if (i > n - 1) i = 2 * (n - 1) - i;
+            i = i < 0 ? 0 : (i > n - 1 ? n - 1 : i);
+            region[m] = read_sample<IN_F32>(a.in, base, i, C, fold);
+        }
+        wave_lds_sync();
+        static_for<0, P>([&](auto ic) {
+            constexpr int n1 = decltype(ic)::value;
+            const float r = region[L * n1 + j];
+            if (e == 0) raw[n1].x = r; else raw[n1].y = r;
+        });
+    }
+}
+
+template <int C>
+struct Chunk;  // one point's worth of input per lane: C interleaved channels x 2 samples
+template <>
+struct Chunk<1> {
+    using T = float2;
+    __device__ static float2 mix(T x) { return x; }
+};
+template <>
+struct Chunk<2> {
+    using T = float4;
+    __device__ static float2 mix(T x) { return make_float2(x.x + x.y, x.z + x.w); }  // lib.rs:42
+};
+
+// OK: 0 complex, 1 linear kinds, 2 mel kinds. C: 1 mono, 2 stereo (f32, interleaved).
+template <int NC, int OK, int C>
+__global__ void __launch_bounds__(kBlock, 2)
+stft3_kernel(StftLaunch a, uint64_t fps) {
+    using G = Geo2<NC>;
+    using G3 = Geo3<NC>;
+    using CT = typename Chunk<C>::T;
+    constexpr int P = G::P, L = G::L, FPW = G::FPW, F = G::F, SH = G3::SH;
+
+    extern __shared__ __attribute__((aligned(16))) float lds[];
+    float* wtab = lds;
+    float* work = lds + G::WIN_FLOATS;
+    float4* mel_lds = reinterpret_cast<float4*>(lds + G3::BASE_FLOATS);
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int slot = lane / L, j = lane % L;
+    const int partner = slot * L + ((L - j) % L);
+
+    for (int i = threadIdx.x; i < 2 * NC; i += kBlock) wtab[i] = a.wpad[i] * 0.5f;  // exact
+    if constexpr (OK == 2) {
+        const int nw = a.mel4_rows * L;
+        for (int i = threadIdx.x; i < nw; i += kBlock) mel_lds[i] = a.mel4_wt[i];
+    }
+    float2 twb[G::TB], twa[G::TA];
+    load_tw2<NC>(a, j, twb, twa);
+    float2 ub[G::CPL];
+#pragma unroll
+    for (int c = 0; c < G::CPL; ++c) ub[c] = a.sincos[j + c * L];
+    __syncthreads();
+
+    const uint64_t total = a.total_frames;
+    const uint64_t stream = ((uint64_t)blockIdx.x * kWaves + wave) * FPW + slot;
+    const uint64_t g0 = stream * fps;
+    const uint64_t g1 = g0 + fps < total ? g0 + fps : total;
+    const int hop = a.hop;
+    float* region = work + (wave * FPW + slot) * G::RS;
+    const float* in = static_cast<const float*>(a.in);
+
+    float2 raw[P];
+    CT pre[SH];
+    bool pre_ok = false;
+    int hint = -1;
+    for (uint64_t it = 0; it < fps; ++it) {  // wave-uniform trip count
+        const uint64_t g = g0 + it;
+        const bool valid = g < g1;
+        // opaque per frame: keeps the untangle rotations (from ub) and the window reads (from
+        // wj) inside the loop instead of hoisted as loop invariants into 100+ VGPRs
+#pragma unroll
+        for (int c = 0; c < G::CPL; ++c) asm volatile("" : "+v"(ub[c].x), "+v"(ub[c].y));
+        int wj = j;
+        asm volatile("" : "+v"(wj));
+        const float2* wrow = reinterpret_cast<const float2*>(wtab) + wj;
+        int64_t start = 0, n = 0;
+        uint64_t base = 0, g_end = 0;
+        if (valid) {
+            hint = find_track(a.trk_frame0, a.n_tracks, g, hint);
+            const uint64_t t = g - a.trk_frame0[hint];
+            n = (int64_t)a.trk_len[hint];
+            base = a.trk_in_off[hint];
+            g_end = a.trk_frame0[hint + 1];
+            start = (int64_t)t * hop - NC;  // half_win = NC, pad_left = 0
+        }
+        // ---- the frame's raw samples ----
+        if (pre_ok) {
+            // shift by one hop, then the prefetched new points (same lane, SH further on)
+#pragma unroll
+            for (int n1 = 0; n1 < P - SH; ++n1) raw[n1] = raw[n1 + SH];
+#pragma unroll
+            for (int q = 0; q < SH; ++q) raw[P - SH + q] = Chunk<C>::mix(pre[q]);
+        } else if (valid && start >= 0 && start + 2 * NC <= n && ((base + (uint64_t)start * C) % (2 * C)) == 0) {
+            const CT* src = reinterpret_cast<const CT*>(in + base + (uint64_t)start * C) + j;
+            static_for<0, P / 8>([&](auto gc) {  // 8 loads in flight per chunk
+                constexpr int g8 = decltype(gc)::value;
+                static_for<0, 8>([&](auto ic) {
+                    constexpr int n1 = 8 * g8 + decltype(ic)::value;
+                    raw[n1] = Chunk<C>::mix(src[L * n1]);
+                });
+                pin_range<8 * g8, 8 * g8 + 8>(raw);
+            });
+        } else if (valid) {
+            load_raw_generic<NC>(a, region, j, start, n, base, C, C > 1, raw);
+        } else {
+#pragma unroll
+            for (int n1 = 0; n1 < P; ++n1) raw[n1] = make_float2(0.f, 0.f);
+        }
+        // ---- prefetch the next frame's hop of new samples (its points P-SH .. P-1) ----
+        {
+            const int64_t nstart = start + hop;
+            const bool nxt = valid && g + 1 < g1 && g + 1 < g_end && nstart + 2 * NC <= n &&
+                             nstart + 2 * L * (P - SH) >= 0 &&
+                             ((base + (uint64_t)(nstart + 2 * L * (P - SH)) * C) % (2 * C)) == 0;
+            if (nxt) {
+                const CT* src = reinterpret_cast<const CT*>(in + base + (uint64_t)(nstart + 2 * L * (P - SH)) * C) + j;
+#pragma unroll
+                for (int q = 0; q < SH; ++q) pre[q] = src[L * q];
+            }
+            pre_ok = nxt;
+        }
+        // ---- window (lib.rs:379, the 1/2 of realfft.rs:148-154 folded in) and the FFT ----
+        float2 v[P];
+#pragma unroll
+        for (int n1 = 0; n1 < P; ++n1) {
+            const float2 w = wrow[L * n1];
+            v[n1] = make_float2(raw[n1].x * w.x, raw[n1].y * w.y);
+        }
+        fft2<NC>(v, region, j, twb, twa);
+        if constexpr (OK == 2) {
+            untangle2<NC>(v, j, partner, ub, [&](int k, float xr, float xi) {
+                region[k] = __builtin_amdgcn_sqrtf(xr * xr + xi * xi);  // |X| (lib.rs:124)
+            });
+            if (j == 0) {
+#pragma unroll
+                for (int k = F; k < G::F4; ++k) region[k] = 0.0f;
+            }
+            wave_lds_sync();
+            mel4<NC>(a, region, mel_lds, j, g, valid);
+        } else if constexpr (OK == 0) {
+            float2* crow = reinterpret_cast<float2*>(a.out) + g * F;
+            untangle2<NC>(v, j, partner, ub, [&](int k, float xr, float xi) {
+                if (valid) crow[k] = make_float2(xr, xi);
+            });
+        } else {
+            const int kind = a.out_kind;
+            const bool power = kind == OUT_POWER || kind == OUT_POWER_DB;
+            const bool db = kind == OUT_AMP_DB || kind == OUT_POWER_DB;
+            untangle2<NC>(v, j, partner, ub, [&](int k, float xr, float xi) {
+                const float p2 = xr * xr + xi * xi;
+                region[k] = power ? p2 : __builtin_amdgcn_sqrtf(p2);
+            });
+            wave_lds_sync();
+            float* frow = static_cast<float*>(a.out) + g * F;
+            if (valid) {
+                for (int k = j; k < F; k += L) {
+                    float val = region[k];
+                    if (db) val = power ? db_of(val, a.log_amin, 1e-36f, 10.0f)
+                                        : db_of(val, a.log_amin, 1e-18f, 20.0f);
+                    frow[k] = val;
+                }
+            }
+        }
+    }
+}
+
+// --------------------------------------------------------------------------------------
+// host-side dispatch
+// --------------------------------------------------------------------------------------
+template <int NC>
+static int lds3_bytes(const StftLaunch& a, bool mel) {
+    return (Geo3<NC>::BASE_FLOATS + (mel ? a.mel4_rows * Geo2<NC>::L * 4 : 0)) * 4;
+}
+
+template <int NC, int OK, int C>
+static int launch3_k(const StftLaunch& a, hipStream_t stream) {
+    const int lds = lds3_bytes<NC>(a, OK == 2);
+    if (lds > 163840) return -2;
+    auto kern = stft3_kernel<NC, OK, C>;
+    if (hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
+                            hipFuncAttributeMaxDynamicSharedMemorySize, lds) != hipSuccess)
+        return -1;
+    if (a.total_frames == 0) return 0;
+    constexpr uint64_t per_block = Geo3<NC>::STREAMS;
+    int grid = grid_for(reinterpret_cast<const void*>(kern), kBlock, lds,
+                        (a.total_frames + per_block - 1) / per_block, a.grid);
+    const uint64_t streams = (uint64_t)grid * per_block;
+    const uint64_t fps = (a.total_frames + streams - 1) / streams;
+    grid = (int)((a.total_frames + fps * per_block - 1) / (fps * per_block));
+    hipLaunchKernelGGL(kern, dim3(grid), dim3(kBlock), lds, stream, a, fps);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+template <int NC, int C>
+static int launch3_c(const StftLaunch& a, hipStream_t s) {
+    if (a.out_kind == OUT_COMPLEX) return launch3_k<NC, 0, C>(a, s);
+    if (a.out_kind == OUT_MEL || a.out_kind == OUT_MEL_AMP_DB) return launch3_k<NC, 2, C>(a, s);
+    return launch3_k<NC, 1, C>(a, s);
+}
+
+template <int NC>
+static int launch3_nc(const StftLaunch& a, hipStream_t s) {
+    return a.channels == 2 ? launch3_c<NC, 2>(a, s) : launch3_c<NC, 1>(a, s);
+}
+
+bool stft3_supports(int n_fft, int win, int hop, int in_format, int channels) {
+    return (n_fft == 256 || n_fft == 512 || n_fft == 1024 || n_fft == 2048) && win == n_fft &&
+           hop * 4 == n_fft && in_format == IN_F32 && (channels == 1 || channels == 2);
+}
+
+int launch_stft3(const StftLaunch& a, hipStream_t s) {
+    switch (a.n_fft / 2) {
+        case 128: return launch3_nc<128>(a, s);
+        case 256: return launch3_nc<256>(a, s);
+        case 512: return launch3_nc<512>(a, s);
+        case 1024: return launch3_nc<1024>(a, s);
+        default: return -2;
+    }
+}
+
+}  // namespace thesia
