@@ -233,12 +233,29 @@ int plan_create(const thesia_plan_desc& d, Plan** out) {
         }
         if (tw2.empty()) tw2.assign(2, 0.0f);
     }
+    // stft3's lane-major full stage-1 twiddles: [k1][j] = W_NC^{j*k1} (f64-rounded)
+    std::vector<float> tw3;
+    {
+        int L = 0;
+        if (stft_kernel_info((int)d.n_fft, nullptr, nullptr, &L) == 0 && L > 0 && p->NC >= (size_t)L) {
+            const size_t P = p->NC / (size_t)L;
+            tw3.resize(2 * P * (size_t)L);
+            for (size_t k1 = 0; k1 < P; ++k1)
+                for (size_t j = 0; j < (size_t)L; ++j) {
+                    const size_t e = (j * k1) % p->NC;
+                    tw3[2 * (k1 * L + j)] = tw[2 * e];
+                    tw3[2 * (k1 * L + j) + 1] = tw[2 * e + 1];
+                }
+        }
+        if (tw3.empty()) tw3.assign(2, 0.0f);
+    }
     std::vector<float> sc = rfft_sin_cos(d.n_fft);
     const bool power = d.output == THESIA_OUT_POWER || d.output == THESIA_OUT_POWER_DB;
     p->log_amin = power ? log10f(1e-36f) : log10f(1e-18f);  // decibel.rs:7-8, :43
     int rc = p->wpad.upload(wpad.data(), wpad.size() * sizeof(float));
     if (!rc) rc = p->tw.upload(tw.data(), tw.size() * sizeof(float));
     if (!rc) rc = p->tw2.upload(tw2.data(), tw2.size() * sizeof(float));
+    if (!rc) rc = p->tw3.upload(tw3.data(), tw3.size() * sizeof(float));
     if (!rc) rc = p->sincos.upload(sc.data(), sc.size() * sizeof(float));
     if (!rc && (d.output == THESIA_OUT_MEL || d.output == THESIA_OUT_MEL_AMP_DB)) {
         const size_t F = p->NC + 1;
@@ -335,6 +352,7 @@ int batch_create(Plan* plan, const thesia_batch_desc& d, Batch** out) {
     L.tw1 = plan->tw.as<float2>();
     L.sincos = plan->sincos.as<float2>();
     L.tw2 = plan->tw2.as<float2>();
+    L.tw3 = plan->tw3.as<float2>();
     L.log_amin = plan->log_amin;
     L.n_mels = (int)plan->n_mels;
     L.mel_rounds = plan->mel_rounds;

@@ -58,7 +58,7 @@ struct Plan {
     std::vector<float> mel_fb;  // [F, n_mels]
     float log_amin = 0.f;
     int tile_frames = 0, lds_bytes = 0;
-    DevBuf wpad, tw, tw2, sincos, mel_round, mel_k0, mel_wt;
+    DevBuf wpad, tw, tw2, tw3, sincos, mel_round, mel_k0, mel_wt;
     int mel_rounds = 0;
     size_t mel_wt_rows = 0;  // padded band lengths summed over the rounds
     DevBuf mel4_round, mel4_k0, mel4_wt;  // stft2_kernel layout (float4 steps)

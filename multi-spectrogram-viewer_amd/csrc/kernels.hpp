@@ -43,6 +43,7 @@ struct StftLaunch {
     const float2* tw1 = nullptr;     // [NC] W_NC^m, m < NC (stage-1 twiddle bases)
     const float2* sincos = nullptr;  // [NC] realfft untangle table (sin, cos)
     const float2* tw2 = nullptr;     // stft2: [TB + TA][L] W_NC^{j*b}, W_NC^{j*TB*a} (lane-major)
+    const float2* tw3 = nullptr;     // stft3: [P][L] W_NC^{j*k1} (lane-major)
     float log_amin = 0.f;            // log10f(amin), host-computed
     // mel (lib.rs:131): round r gives lane j of a frame mel r*L + j (L = lanes per frame);
     // the lane runs bins mel_k0[r*L + j] + it, it < mel_round[r].y, with weights

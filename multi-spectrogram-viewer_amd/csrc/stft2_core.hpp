@@ -81,23 +81,17 @@ __device__ __forceinline__ bool load_direct2(const StftLaunch& a, int j, int64_t
 
 // Stage-1 DFT_P + twiddles W_NC^{j k1}, LDS transpose (re then im), stage-2 DFT_L, in place.
 // On return v[c*L + ce_pos(L, k2)] = Z[k1 + P*k2] / 2 with k1 = j + c*L.
-template <int NC>
-__device__ __forceinline__ void fft2(float2 (&v)[Geo2<NC>::P], float* region, int j,
-                                     const float2 (&twb)[Geo2<NC>::TB],
-                                     const float2 (&twa)[Geo2<NC>::TA]) {
+// twf(k1c, x): applies the stage-1 twiddle W_NC^{j*k1} to x (k1c an integral_constant).
+template <int NC, class TwF>
+__device__ __forceinline__ void fft2(float2 (&v)[Geo2<NC>::P], float* region, int j, TwF&& twf) {
     using G = Geo2<NC>;
-    constexpr int L = G::L, P = G::P, TB = G::TB, S = G::S, CPL = G::CPL;
+    constexpr int L = G::L, P = G::P, S = G::S, CPL = G::CPL;
     pin(v);
     dif_fft<P, 1, 0, P>(v);
     pin(v);
-    static_for<0, P>([&](auto kc) {
-        constexpr int k1 = decltype(kc)::value;
-        constexpr int b = k1 % TB, aa = k1 / TB;
-        constexpr int pk = ce_pos(P, k1);
-        float2 x = v[pk];
-        if constexpr (b != 0) x = cmul(x, twb[b]);
-        if constexpr (aa != 0) x = cmul(x, twa[aa]);
-        v[pk] = x;
+    static_for<1, P>([&](auto kc) {
+        constexpr int pk = ce_pos(P, decltype(kc)::value);
+        v[pk] = twf(kc, v[pk]);
     });
 #pragma unroll
     for (int e = 0; e < 2; ++e) {
@@ -140,6 +134,32 @@ __device__ __forceinline__ void load_tw2(const StftLaunch& a, int j, float2 (&tw
 #pragma unroll
     for (int aa = 0; aa < TA; ++aa) twa[aa] = twp[(TB + aa) * L];
 }
+
+// Stage-1 twiddles as two products W_NC^{j*b} * W_NC^{j*TB*aa} (k1 = TB*aa + b) from bases in
+// registers.
+template <int NC>
+struct TwBases {
+    float2 b[Geo2<NC>::TB], a[Geo2<NC>::TA];
+    template <class K>
+    __device__ __forceinline__ float2 operator()(K, float2 x) const {
+        constexpr int TB = Geo2<NC>::TB;
+        constexpr int k1 = K::value, bb = k1 % TB, aa = k1 / TB;
+        if constexpr (bb != 0) x = cmul(x, b[bb]);
+        if constexpr (aa != 0) x = cmul(x, a[aa]);
+        return x;
+    }
+};
+
+// Stage-1 twiddles as one product with W_NC^{j*k1} from a lane-major [P][L] table (LDS):
+// conflict-free ds_read_b64 (consecutive lanes, consecutive entries).
+struct TwTable {
+    const float2* row;  // table + j
+    int L;
+    template <class K>
+    __device__ __forceinline__ float2 operator()(K, float2 x) const {
+        return cmul(x, row[K::value * L]);
+    }
+};
 
 // realfft untangle on bin pairs; calls epi(k, re, im) for every bin this lane produces
 // (k = j + c*L + P*t and NC - k for t < L/2; lane 0 also the self-paired bin NC/2).
@@ -201,18 +221,20 @@ __device__ __forceinline__ void untangle2(const float2 (&v)[Geo2<NC>::P], int j,
 }
 
 // lib.rs:131-132 on the |X| row in `region`: round r gives lane j mel r*L + j.
-// wt: the float4 weight rows (a.mel4_wt in HBM, or its copy in LDS).
+// wt / rounds / k0: the float4 weight rows, the per-round {row, steps} and the per-lane start
+// bins (a.mel4_* in HBM, or their copies in LDS).
 template <int NC>
 __device__ __forceinline__ void mel4(const StftLaunch& a, const float* region, const float4* wt,
-                                     int j, uint64_t g, bool valid) {
+                                     const int2* rounds, const int* k0, int j, uint64_t g,
+                                     bool valid) {
     constexpr int L = Geo2<NC>::L;
     constexpr int U = 4;
     const int n_mels = a.n_mels;
     const bool db = a.out_kind == OUT_MEL_AMP_DB;
     float* out = static_cast<float*>(a.out) + g * (uint64_t)n_mels;
     for (int r = 0; r < a.mel4_rounds; ++r) {
-        const int2 rd = a.mel4_round[r];  // {first float4 row, float4 steps}: wave-uniform
-        const float4* xp = reinterpret_cast<const float4*>(region + a.mel4_k0[r * L + j]);
+        const int2 rd = rounds[r];  // {first float4 row, float4 steps}: wave-uniform
+        const float4* xp = reinterpret_cast<const float4*>(region + k0[r * L + j]);
         const float4* wp = wt + (size_t)rd.x * L + j;
         float acc = 0.0f;
         int it = 0;

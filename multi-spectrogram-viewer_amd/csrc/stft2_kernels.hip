@@ -77,9 +77,9 @@ stft2_kernel(StftLaunch a, uint64_t tiles_per_block) {
         }
         {
             // twiddle bases re-read every pass (24 VGPRs the 4-waves/SIMD budget lacks)
-            float2 twb[G::TB], twa[G::TA];
-            load_tw2<NC>(a, j, twb, twa);
-            fft2<NC>(v, region, j, twb, twa);
+            TwBases<NC> tw;
+            load_tw2<NC>(a, j, tw.b, tw.a);
+            fft2<NC>(v, region, j, tw);
         }
         if constexpr (OK == 2) {
             untangle2<NC>(v, j, partner, ub, [&](int k, float xr, float xi) {
@@ -90,7 +90,7 @@ stft2_kernel(StftLaunch a, uint64_t tiles_per_block) {
                 for (int k = F; k < G::F4; ++k) region[k] = 0.0f;
             }
             wave_lds_sync();
-            mel4<NC>(a, region, a.mel4_wt, j, g, valid);
+            mel4<NC>(a, region, a.mel4_wt, a.mel4_round, a.mel4_k0, j, g, valid);
             continue;
         }
         if constexpr (OK == 0) {

@@ -16,6 +16,8 @@
 // reflected). The mel weights are copied into LDS once per block.
 #include "stft2_core.hpp"
 
+#include <type_traits>
+
 namespace thesia {
 
 template <int NC>
@@ -24,13 +26,14 @@ struct Geo3 {
     static constexpr int L = G2::L, P = G2::P, FPW = G2::FPW, RS = G2::RS;
     static constexpr int SH = P / 4;                      // points per lane a hop moves
     static constexpr int STREAMS = kWaves * FPW;          // streams (= frames in flight) per block
-    static constexpr int BASE_FLOATS = G2::WIN_FLOATS + STREAMS * RS;
+    static constexpr int TW_FLOATS = 2 * P * L;           // W_NC^{j*k1}, [P][L] float2
+    static constexpr int BASE_FLOATS = G2::WIN_FLOATS + TW_FLOATS + STREAMS * RS;
     static_assert(P % 4 == 0, "hop = n_fft/4 must move whole points per lane");
 };
 
 // Reflect-padded, downmixed samples of a frame (no window): the uniform rule of
 // load_frame_generic (stft_common.hpp) for win = n_fft.
-template <int NC>
+template <int NC, int INF>
 __device__ __forceinline__ void load_raw_generic(const StftLaunch& a, float* region, int j,
                                                  int64_t start, int64_t n, uint64_t base, int C,
                                                  bool fold, float2 (&raw)[Geo2<NC>::P]) {
@@ -44,7 +47,7 @@ __device__ __forceinline__ void load_raw_generic(const StftLaunch& a, float* reg
             if (i < 0) i = -i;
             if (i > n - 1) i = 2 * (n - 1) - i;
             i = i < 0 ? 0 : (i > n - 1 ? n - 1 : i);
-            region[m] = read_sample<IN_F32>(a.in, base, i, C, fold);
+            region[m] = read_sample<INF>(a.in, base, i, C, fold);
         }
         wave_lds_sync();
         static_for<0, P>([&](auto ic) {
@@ -55,32 +58,53 @@ __device__ __forceinline__ void load_raw_generic(const StftLaunch& a, float* reg
     }
 }
 
-template <int C>
-struct Chunk;  // one point's worth of input per lane: C interleaved channels x 2 samples
+// One point's worth of input per lane (2 samples x C interleaved channels) and its downmix:
+// f32 as is, s16 as value / 2^15 (audio.rs:16-19, exact), channels summed (lib.rs:42).
+template <int C, int INF>
+struct Chunk;
 template <>
-struct Chunk<1> {
+struct Chunk<1, IN_F32> {
     using T = float2;
     __device__ static float2 mix(T x) { return x; }
 };
 template <>
-struct Chunk<2> {
+struct Chunk<2, IN_F32> {
     using T = float4;
-    __device__ static float2 mix(T x) { return make_float2(x.x + x.y, x.z + x.w); }  // lib.rs:42
+    __device__ static float2 mix(T x) { return make_float2(x.x + x.y, x.z + x.w); }
+};
+template <>
+struct Chunk<1, IN_S16> {
+    using T = short2;
+    __device__ static float2 mix(T x) { return make_float2((float)x.x / 32768.0f, (float)x.y / 32768.0f); }
+};
+template <>
+struct Chunk<2, IN_S16> {
+    using T = short4;
+    __device__ static float2 mix(T x) {
+        return make_float2((float)x.x / 32768.0f + (float)x.y / 32768.0f,
+                           (float)x.z / 32768.0f + (float)x.w / 32768.0f);
+    }
 };
 
-// OK: 0 complex, 1 linear kinds, 2 mel kinds. C: 1 mono, 2 stereo (f32, interleaved).
-template <int NC, int OK, int C>
+// OK: 0 complex, 1 linear kinds, 2 mel kinds. C: 1 mono, 2 stereo (interleaved); INF: f32 / s16.
+template <int NC, int OK, int C, int INF>
 __global__ void __launch_bounds__(kBlock, 2)
 stft3_kernel(StftLaunch a, uint64_t fps) {
     using G = Geo2<NC>;
     using G3 = Geo3<NC>;
-    using CT = typename Chunk<C>::T;
+    using CK = Chunk<C, INF>;
+    using CT = typename CK::T;
+    using ET = typename std::conditional<INF == IN_S16, int16_t, float>::type;
     constexpr int P = G::P, L = G::L, FPW = G::FPW, F = G::F, SH = G3::SH;
 
     extern __shared__ __attribute__((aligned(16))) float lds[];
     float* wtab = lds;
-    float* work = lds + G::WIN_FLOATS;
+    float2* twtab = reinterpret_cast<float2*>(lds + G::WIN_FLOATS);
+    float* work = lds + G::WIN_FLOATS + G3::TW_FLOATS;
+    // mel tables in LDS: weight rows, then the per-lane start bins, then the round table
     float4* mel_lds = reinterpret_cast<float4*>(lds + G3::BASE_FLOATS);
+    int* k0_lds = reinterpret_cast<int*>(mel_lds + (OK == 2 ? a.mel4_rows * L : 0));
+    int2* rd_lds = reinterpret_cast<int2*>(k0_lds + (OK == 2 ? a.mel4_rounds * L : 0));
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int slot = lane / L, j = lane % L;
     const int partner = slot * L + ((L - j) % L);
@@ -89,9 +113,10 @@ stft3_kernel(StftLaunch a, uint64_t fps) {
     if constexpr (OK == 2) {
         const int nw = a.mel4_rows * L;
         for (int i = threadIdx.x; i < nw; i += kBlock) mel_lds[i] = a.mel4_wt[i];
+        for (int i = threadIdx.x; i < a.mel4_rounds * L; i += kBlock) k0_lds[i] = a.mel4_k0[i];
+        for (int i = threadIdx.x; i < a.mel4_rounds; i += kBlock) rd_lds[i] = a.mel4_round[i];
     }
-    float2 twb[G::TB], twa[G::TA];
-    load_tw2<NC>(a, j, twb, twa);
+    for (int i = threadIdx.x; i < P * L; i += kBlock) twtab[i] = a.tw3[i];
     float2 ub[G::CPL];
 #pragma unroll
     for (int c = 0; c < G::CPL; ++c) ub[c] = a.sincos[j + c * L];
@@ -103,12 +128,15 @@ stft3_kernel(StftLaunch a, uint64_t fps) {
     const uint64_t g1 = g0 + fps < total ? g0 + fps : total;
     const int hop = a.hop;
     float* region = work + (wave * FPW + slot) * G::RS;
-    const float* in = static_cast<const float*>(a.in);
+    const ET* in = static_cast<const ET*>(a.in);
 
     float2 raw[P];
     CT pre[SH];
     bool pre_ok = false;
     int hint = -1;
+    // the stream's current track, cached across frames (looked up again only past its end)
+    uint64_t g_beg = 1, g_end = 0, base = 0;
+    int64_t n = 0;
     for (uint64_t it = 0; it < fps; ++it) {  // wave-uniform trip count
         const uint64_t g = g0 + it;
         const bool valid = g < g1;
@@ -119,15 +147,16 @@ stft3_kernel(StftLaunch a, uint64_t fps) {
         int wj = j;
         asm volatile("" : "+v"(wj));
         const float2* wrow = reinterpret_cast<const float2*>(wtab) + wj;
-        int64_t start = 0, n = 0;
-        uint64_t base = 0, g_end = 0;
+        int64_t start = 0;
         if (valid) {
-            hint = find_track(a.trk_frame0, a.n_tracks, g, hint);
-            const uint64_t t = g - a.trk_frame0[hint];
-            n = (int64_t)a.trk_len[hint];
-            base = a.trk_in_off[hint];
-            g_end = a.trk_frame0[hint + 1];
-            start = (int64_t)t * hop - NC;  // half_win = NC, pad_left = 0
+            if (g >= g_end || g < g_beg) {
+                hint = find_track(a.trk_frame0, a.n_tracks, g, hint);
+                g_beg = a.trk_frame0[hint];
+                g_end = a.trk_frame0[hint + 1];
+                n = (int64_t)a.trk_len[hint];
+                base = a.trk_in_off[hint];
+            }
+            start = (int64_t)(g - g_beg) * hop - NC;  // half_win = NC, pad_left = 0
         }
         // ---- the frame's raw samples ----
         if (pre_ok) {
@@ -135,19 +164,19 @@ stft3_kernel(StftLaunch a, uint64_t fps) {
 #pragma unroll
             for (int n1 = 0; n1 < P - SH; ++n1) raw[n1] = raw[n1 + SH];
 #pragma unroll
-            for (int q = 0; q < SH; ++q) raw[P - SH + q] = Chunk<C>::mix(pre[q]);
+            for (int q = 0; q < SH; ++q) raw[P - SH + q] = CK::mix(pre[q]);
         } else if (valid && start >= 0 && start + 2 * NC <= n && ((base + (uint64_t)start * C) % (2 * C)) == 0) {
             const CT* src = reinterpret_cast<const CT*>(in + base + (uint64_t)start * C) + j;
             static_for<0, P / 8>([&](auto gc) {  // 8 loads in flight per chunk
                 constexpr int g8 = decltype(gc)::value;
                 static_for<0, 8>([&](auto ic) {
                     constexpr int n1 = 8 * g8 + decltype(ic)::value;
-                    raw[n1] = Chunk<C>::mix(src[L * n1]);
+                    raw[n1] = CK::mix(src[L * n1]);
                 });
                 pin_range<8 * g8, 8 * g8 + 8>(raw);
             });
         } else if (valid) {
-            load_raw_generic<NC>(a, region, j, start, n, base, C, C > 1, raw);
+            load_raw_generic<NC, INF>(a, region, j, start, n, base, C, a.fold != 0, raw);
         } else {
 #pragma unroll
             for (int n1 = 0; n1 < P; ++n1) raw[n1] = make_float2(0.f, 0.f);
@@ -172,17 +201,17 @@ stft3_kernel(StftLaunch a, uint64_t fps) {
             const float2 w = wrow[L * n1];
             v[n1] = make_float2(raw[n1].x * w.x, raw[n1].y * w.y);
         }
-        fft2<NC>(v, region, j, twb, twa);
+        fft2<NC>(v, region, j, TwTable{twtab + wj, L});
         if constexpr (OK == 2) {
             untangle2<NC>(v, j, partner, ub, [&](int k, float xr, float xi) {
-                region[k] = __builtin_amdgcn_sqrtf(xr * xr + xi * xi);  // |X| (lib.rs:124)
+                region[k] = __builtin_amdgcn_sqrtf(__builtin_fmaf(xr, xr, xi * xi));  // |X| (lib.rs:124)
             });
             if (j == 0) {
 #pragma unroll
                 for (int k = F; k < G::F4; ++k) region[k] = 0.0f;
             }
             wave_lds_sync();
-            mel4<NC>(a, region, mel_lds, j, g, valid);
+            mel4<NC>(a, region, mel_lds, rd_lds, k0_lds, j, g, valid);
         } else if constexpr (OK == 0) {
             float2* crow = reinterpret_cast<float2*>(a.out) + g * F;
             untangle2<NC>(v, j, partner, ub, [&](int k, float xr, float xi) {
@@ -193,7 +222,7 @@ stft3_kernel(StftLaunch a, uint64_t fps) {
             const bool power = kind == OUT_POWER || kind == OUT_POWER_DB;
             const bool db = kind == OUT_AMP_DB || kind == OUT_POWER_DB;
             untangle2<NC>(v, j, partner, ub, [&](int k, float xr, float xi) {
-                const float p2 = xr * xr + xi * xi;
+                const float p2 = __builtin_fmaf(xr, xr, xi * xi);
                 region[k] = power ? p2 : __builtin_amdgcn_sqrtf(p2);
             });
             wave_lds_sync();
@@ -215,14 +244,15 @@ stft3_kernel(StftLaunch a, uint64_t fps) {
 // --------------------------------------------------------------------------------------
 template <int NC>
 static int lds3_bytes(const StftLaunch& a, bool mel) {
-    return (Geo3<NC>::BASE_FLOATS + (mel ? a.mel4_rows * Geo2<NC>::L * 4 : 0)) * 4;
+    return (Geo3<NC>::BASE_FLOATS +
+            (mel ? (a.mel4_rows * 4 + a.mel4_rounds) * Geo2<NC>::L + 2 * a.mel4_rounds : 0)) * 4;
 }
 
-template <int NC, int OK, int C>
+template <int NC, int OK, int C, int INF>
 static int launch3_k(const StftLaunch& a, hipStream_t stream) {
     const int lds = lds3_bytes<NC>(a, OK == 2);
     if (lds > 163840) return -2;
-    auto kern = stft3_kernel<NC, OK, C>;
+    auto kern = stft3_kernel<NC, OK, C, INF>;
     if (hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
                             hipFuncAttributeMaxDynamicSharedMemorySize, lds) != hipSuccess)
         return -1;
@@ -237,21 +267,24 @@ static int launch3_k(const StftLaunch& a, hipStream_t stream) {
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
-template <int NC, int C>
+template <int NC, int C, int INF>
 static int launch3_c(const StftLaunch& a, hipStream_t s) {
-    if (a.out_kind == OUT_COMPLEX) return launch3_k<NC, 0, C>(a, s);
-    if (a.out_kind == OUT_MEL || a.out_kind == OUT_MEL_AMP_DB) return launch3_k<NC, 2, C>(a, s);
-    return launch3_k<NC, 1, C>(a, s);
+    if (a.out_kind == OUT_COMPLEX) return launch3_k<NC, 0, C, INF>(a, s);
+    if (a.out_kind == OUT_MEL || a.out_kind == OUT_MEL_AMP_DB) return launch3_k<NC, 2, C, INF>(a, s);
+    return launch3_k<NC, 1, C, INF>(a, s);
 }
 
 template <int NC>
 static int launch3_nc(const StftLaunch& a, hipStream_t s) {
-    return a.channels == 2 ? launch3_c<NC, 2>(a, s) : launch3_c<NC, 1>(a, s);
+    if (a.in_format == IN_S16)
+        return a.channels == 2 ? launch3_c<NC, 2, IN_S16>(a, s) : launch3_c<NC, 1, IN_S16>(a, s);
+    return a.channels == 2 ? launch3_c<NC, 2, IN_F32>(a, s) : launch3_c<NC, 1, IN_F32>(a, s);
 }
 
 bool stft3_supports(int n_fft, int win, int hop, int in_format, int channels) {
     return (n_fft == 256 || n_fft == 512 || n_fft == 1024 || n_fft == 2048) && win == n_fft &&
-           hop * 4 == n_fft && in_format == IN_F32 && (channels == 1 || channels == 2);
+           hop * 4 == n_fft && (in_format == IN_F32 || in_format == IN_S16) &&
+           (channels == 1 || channels == 2);
 }
 
 int launch_stft3(const StftLaunch& a, hipStream_t s) {
