@@ -5,9 +5,10 @@ Workload ("C4 per-GPU shard", BASELINE.json configs[3]): every rank owns 1000 sy
 reference's in-memory format after open_audio_file, audio.rs:9-37), resident in HBM before
 timing. One step = one pass of the hot path over the rank's whole shard: channel-sum
 downmix (lib.rs:42) -> reflect framing + Hann/n_fft (lib.rs:367-440) -> real FFT
-(realfft.rs) -> |X| (lib.rs:124) -> 128-band mel projection (per-lane fma rounds) (lib.rs:131) -> amp dB
-(decibel.rs:79-88), n_fft 2048 / hop 512 / win 2048, one kernel launch. Files shard across
-ranks with no data-path collective ("weak" scaling: per-GPU work is fixed).
+(realfft.rs) -> |X| (lib.rs:124) -> 128-band mel projection (lib.rs:131) -> amp dB
+(decibel.rs:79-88), n_fft 2048 / hop 512 / win 2048, one launch of the streaming kernel
+(stft3_kernel). Files shard across ranks by LPT (thesia.shard) with no
+data-path collective ("weak" scaling: per-GPU work is fixed).
 
 Launch: python bench.py [--gpus N --steps K --warmup W]; for N > 1 under
 torch.distributed.run (one rank per GPU; gloo is used only for the timing barrier / max).
@@ -27,7 +28,7 @@ sys.path.insert(0, os.path.join(ROOT, "multi-spectrogram-viewer_amd"))
 import numpy as np  # noqa: E402
 
 import thesia  # noqa: E402  (loads libthesia before torch: one HIP runtime in the process)
-from thesia import engine  # noqa: E402
+from thesia import engine, shard  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s HBM3E (spec)
 
@@ -80,10 +81,12 @@ def max_over_ranks(pg, v: float) -> float:
     return float(t.item())
 
 
-def algorithmic_bytes(args, n_samples, total_frames, row_bins):
+def algorithmic_bytes(args, n_tracks, n_samples, total_frames, row_bins):
+    """Bytes one launch must move at least: the input once (hop-strided, not n_fft per frame)
+    plus the output rows (DESIGN.md §4 'Roofline and algorithmic bytes')."""
     in_el = 4 if args.input == "f32" else 2
     out_el = 8 if args.output == "complex" else 4
-    return args.tracks * n_samples * args.channels * in_el + total_frames * row_bins * out_el
+    return n_tracks * n_samples * args.channels * in_el + total_frames * row_bins * out_el
 
 
 def cpu_baseline(args, n_samples):
@@ -117,6 +120,15 @@ def cpu_baseline(args, n_samples):
                       f"({frames} frames, {dt:.2f} s wall) through the C oracle, {workers} threads"}
 
 
+def frames_all_ranks(pg, frames: int) -> int:
+    if pg is None:
+        return frames
+    import torch
+    t = torch.tensor([float(frames)], dtype=torch.float64)
+    pg.all_reduce(t, op=pg.ReduceOp.SUM)
+    return int(t.item())
+
+
 def traffic_from_profile(workload_key):
     path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     try:
@@ -131,7 +143,8 @@ def traffic_from_profile(workload_key):
 def main():
     args = parse()
     ws, rank, local, pg = dist_setup(args)
-    engine.set_device(local)
+    # one rank per GPU; on a box with fewer GPUs than ranks (a rehearsal) ranks share devices
+    engine.set_device(local % max(1, engine.device_count()))
     n_samples = int(round(args.seconds * args.sr))
     kind = {"mel_db": engine.OUT_MEL_AMP_DB, "amp_db": engine.OUT_AMP_DB,
             "power_db": engine.OUT_POWER_DB, "complex": engine.OUT_COMPLEX}[args.output]
@@ -140,11 +153,16 @@ def main():
                        n_mels=args.n_mels if kind == engine.OUT_MEL_AMP_DB else 0)
     el = 4 if fmt == engine.IN_F32 else 2
     per_track = n_samples * args.channels
-    din = engine.DeviceBuffer(args.tracks * per_track * el)
-    # distinct tracks per rank: the generator is seeded by the global track index
-    engine.synth_pcm_device(din, fmt, args.channels, args.tracks, n_samples, args.sr, seed=rank)
-    offs = np.arange(args.tracks, dtype=np.uint64) * per_track
-    lens = np.full(args.tracks, n_samples, np.uint64)
+    # the job's tracks (tracks-per-GPU x ranks) are partitioned per file by LPT
+    # (thesia.shard); every rank computes the same partition, no exchange
+    mine = shard.plan_shards([n_samples] * (args.tracks * ws), args.n_fft, args.hop, args.n_fft,
+                             args.n_mels if kind == engine.OUT_MEL_AMP_DB else 0, ws, rank)
+    n_local = len(mine)
+    din = engine.DeviceBuffer(n_local * per_track * el)
+    # distinct tracks per rank: the generator is seeded per rank and track
+    engine.synth_pcm_device(din, fmt, args.channels, n_local, n_samples, args.sr, seed=rank)
+    offs = np.arange(n_local, dtype=np.uint64) * per_track
+    lens = np.full(n_local, n_samples, np.uint64)
     frames = engine.Batch.frames_for(plan, lens)
     dout = engine.DeviceBuffer(frames * plan.row_bins * (8 if kind == engine.OUT_COMPLEX else 4))
     batch = engine.Batch(plan, din, offs, lens, dout, input_format=fmt, channels=args.channels)
@@ -179,10 +197,10 @@ def main():
     # kernel duration from HIP events on the launch stream (roofline numerator / denominator)
     kms = batch.run_timed(max(args.steps, 5)) / max(args.steps, 5)
     kms = max_over_ranks(pg, kms)
-    abytes = algorithmic_bytes(args, n_samples, frames, plan.row_bins)
+    abytes = algorithmic_bytes(args, n_local, n_samples, frames, plan.row_bins)
     achieved = abytes / (kms * 1e-3) / 1e9
 
-    total_frames_all = frames * ws
+    total_frames_all = frames_all_ranks(pg, frames)
     result = {
         "metric": "STFT frames/sec (n_fft=2048 hop=512) at 1/2/4/8 GPUs; % HBM roofline",
         "value": total_frames_all / dt,
@@ -201,7 +219,8 @@ def main():
                         f"{'stereo' if args.channels == 2 else str(args.channels) + '-ch'} tracks per GPU "
                         f"({args.input} interleaved), n_fft {args.n_fft} hop {args.hop} Hann, "
                         f"sum-downmix, {'mel-' + str(args.n_mels) + ' + amp dB' if kind == engine.OUT_MEL_AMP_DB else args.output}",
-            "tracks_per_gpu": args.tracks,
+            "tracks_per_gpu": n_local,
+            "tracks_total": args.tracks * ws,
             "frames_per_gpu": frames,
             "parallelism": f"file-sharded x{ws}, no collective",
         },

@@ -1,0 +1,95 @@
+"""Multi-GPU sharding of the spectrogram path.
+
+Files are independent through the whole spectrogram stage (lib.rs:112-136 runs per track), so
+they shard across ranks (one process per GPU) with no collective on the data path. The only
+cross-track coupling in the reference is the global dB range and the maximum sample rate that
+`update_spec_greys` reduces before any grey image is built (lib.rs:193-263): three scalars per
+rank, exchanged with one all_reduce between the spectrogram phase and the display phase.
+
+This module is host logic only (no device calls), so it is covered on CPU by world_size-2 gloo
+tests; on the GPU box the same calls run over RCCL ("nccl") or gloo.
+"""
+from __future__ import annotations
+
+import math
+from typing import List, Optional, Sequence, Tuple
+
+from .utils import stft_n_frames
+
+
+def track_cost(n_samples: int, win_length: int, hop_length: int, n_fft: int, n_mels: int = 0) -> float:
+    """Kernel cost model of one track: frames x (FFT work + per-bin work + mel work)."""
+    T = stft_n_frames(n_samples, win_length, hop_length)
+    F = n_fft // 2 + 1
+    return float(T) * (n_fft * math.log2(max(n_fft, 2)) + 2.0 * F + 2.0 * n_mels)
+
+
+def assign_tracks(costs: Sequence[float], world_size: int) -> List[List[int]]:
+    """Greedy LPT: tracks in decreasing cost (ties: lower index first) go to the least-loaded
+    rank (ties: lower rank). Deterministic, so every rank computes the same partition without
+    communicating. Returns, per rank, its track indices in increasing order."""
+    if world_size < 1:
+        raise ValueError("world_size must be >= 1")
+    order = sorted(range(len(costs)), key=lambda i: (-float(costs[i]), i))
+    load = [0.0] * world_size
+    shards: List[List[int]] = [[] for _ in range(world_size)]
+    for i in order:
+        r = min(range(world_size), key=lambda k: (load[k], k))
+        shards[r].append(i)
+        load[r] += float(costs[i])
+    return [sorted(s) for s in shards]
+
+
+def local_range(spec_max: Sequence[float], spec_min: Sequence[float]) -> Tuple[float, float]:
+    """Per-rank (max, min) over its tracks' dB spectrograms (lib.rs:194-207): -inf / +inf when the
+    rank holds no track (ndarray-stats' EmptyInput -> unwrap_or)."""
+    mx = max(spec_max, default=-math.inf)
+    mn = min(spec_min, default=math.inf)
+    return float(mx), float(mn)
+
+
+def global_db_range(local_max: float, local_min: float, local_max_sr: int, db_range: float = 120.0,
+                    group=None) -> Tuple[float, float, int]:
+    """The display path's one exchange: global (max_db, min_db, max_sr) as lib.rs:194-228
+    computes them over ALL tracks: max = min(max, 0), min = max(min, max - db_range).
+
+    With torch.distributed initialised, reduces over `group` (default world) with one
+    all_reduce(MAX) of (max, -min, max_sr); otherwise the local values are global."""
+    import numpy as np
+
+    mx, mn, sr = float(local_max), float(local_min), int(local_max_sr)
+    try:
+        import torch
+        import torch.distributed as dist
+        active = dist.is_available() and dist.is_initialized()
+    except ImportError:  # pragma: no cover - torch is in the image
+        active = False
+    if active:
+        backend = dist.get_backend(group)
+        dev = "cuda" if backend == "nccl" else "cpu"
+        t = torch.tensor([mx, -mn, float(sr)], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX, group=group)
+        mx, mn, sr = float(t[0]), -float(t[1]), int(t[2])
+    # lib.rs:208-209 in f32, as the reference stores them
+    gmax = float(np.float32(min(mx, 0.0)))
+    gmin = float(np.float32(max(mn, gmax - db_range)))
+    return gmax, gmin, sr
+
+
+def up_ratio(sr: int, max_sr: int, freq_scale_mel: bool) -> float:
+    """Per-track vertical ratio of the grey image (lib.rs:231-248), in f32 like the reference."""
+    import numpy as np
+    from .mel import hz_to_mel
+
+    if freq_scale_mel:
+        return float(np.float32(hz_to_mel(max_sr / 2.0)) / np.float32(hz_to_mel(sr / 2.0)))
+    return float(np.float32(max_sr) / np.float32(sr))
+
+
+def plan_shards(n_samples: Sequence[int], win_length: int, hop_length: int, n_fft: int,
+                n_mels: int, world_size: int, rank: Optional[int] = None):
+    """Convenience: LPT partition of tracks with the given lengths; returns all shards, or
+    rank's shard when `rank` is given."""
+    costs = [track_cost(n, win_length, hop_length, n_fft, n_mels) for n in n_samples]
+    shards = assign_tracks(costs, world_size)
+    return shards if rank is None else shards[rank]

@@ -1,0 +1,102 @@
+"""Multi-GPU sharding logic on CPU: the LPT partition and the one scalar
+exchange of the display path (lib.rs:193-263), including a world_size-2 gloo run."""
+import math
+import os
+import socket
+
+import numpy as np
+import pytest
+
+import oracle_ffi as O
+from thesia import shard
+
+
+def test_lpt_partition_is_disjoint_complete_and_balanced():
+    rng = np.random.default_rng(0)
+    lens = rng.integers(48000, 48000 * 60, size=257)
+    costs = [shard.track_cost(int(n), 2048, 512, 2048, 128) for n in lens]
+    for ws in (1, 2, 3, 8):
+        shards = shard.assign_tracks(costs, ws)
+        flat = sorted(i for s in shards for i in s)
+        assert flat == list(range(len(costs)))
+        loads = [sum(costs[i] for i in s) for s in shards]
+        # LPT bound: max load <= mean + max single cost
+        assert max(loads) <= sum(costs) / ws + max(costs) + 1e-6
+        assert shards == shard.assign_tracks(costs, ws)  # deterministic on every rank
+
+
+def test_equal_tracks_split_evenly():
+    costs = [shard.track_cost(1_440_000, 2048, 512, 2048, 128)] * 8000
+    shards = shard.assign_tracks(costs, 8)
+    assert [len(s) for s in shards] == [1000] * 8
+
+
+def test_empty_rank_range_and_single_process_exchange():
+    assert shard.local_range([], []) == (-math.inf, math.inf)
+    mx, mn, sr = shard.global_db_range(-3.0, -200.0, 48000)
+    assert (mx, mn, sr) == (-3.0, -123.0, 48000)
+    mx, mn, _ = shard.global_db_range(5.0, -20.0, 8000)  # lib.rs:208: max clamped to 0
+    assert (mx, mn) == (0.0, -20.0)
+
+
+def _tracks():
+    rng = np.random.default_rng(42)
+    out = []
+    for i, sr in enumerate([8000, 16000, 22050, 24000, 44100, 48000, 16000, 8000]):
+        n = int(sr * (0.1 + 0.05 * i))
+        amp = 10.0 ** (-i / 4)
+        out.append(((rng.standard_normal(n) * amp).astype(np.float32), sr))
+    return out
+
+
+def _spec_range(x, sr):
+    from thesia.utils import track_params
+    win, hop, n_fft = track_params(sr)
+    w = (O.hann(win) / np.float32(n_fft)).astype(np.float32)
+    db = O.amp_to_db_default(O.norm(O.perform_stft(x, win, hop, n_fft, window=w)))
+    return float(db.max()), float(db.min())
+
+
+def _worker(rank, world, port, q):
+    import torch.distributed as dist
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    tracks = _tracks()
+    mine = shard.plan_shards([len(x) for x, _ in tracks], 1024, 256, 1024, 0, world, rank)
+    ranges = [_spec_range(*tracks[i]) for i in mine]
+    lmx, lmn = shard.local_range([r[0] for r in ranges], [r[1] for r in ranges])
+    lsr = max((tracks[i][1] for i in mine), default=0)
+    q.put((rank, mine, shard.global_db_range(lmx, lmn, lsr)))
+    dist.destroy_process_group()
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def test_world_size_2_gloo_matches_single_process():
+    import torch.multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=120) for _ in procs]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    res.sort()
+    shards = [r[1] for r in res]
+    assert sorted(shards[0] + shards[1]) == list(range(8)) and not set(shards[0]) & set(shards[1])
+    # every rank ends with the same global range, equal to one process over all tracks
+    tracks = _tracks()
+    ranges = [_spec_range(x, sr) for x, sr in tracks]
+    ref = shard.global_db_range(max(r[0] for r in ranges), min(r[1] for r in ranges),
+                                max(sr for _, sr in tracks))
+    assert res[0][2] == res[1][2] == ref
