@@ -163,7 +163,7 @@ struct TwTable {
 
 // realfft untangle on bin pairs; calls epi(k, re, im) for every bin this lane produces
 // (k = j + c*L + P*t and NC - k for t < L/2; lane 0 also the self-paired bin NC/2).
-template <int NC, class Epi>
+template <int NC, bool BATCH = false, class Epi>
 __device__ __forceinline__ void untangle2(const float2 (&v)[Geo2<NC>::P], int j, int partner,
                                           const float2 (&ub)[Geo2<NC>::CPL], Epi&& epi) {
     using G = Geo2<NC>;
@@ -177,6 +177,20 @@ __device__ __forceinline__ void untangle2(const float2 (&v)[Geo2<NC>::P], int j,
         epi(k, ar + q, ai - p);
         if (both) epi(NC - k, ar - q, -ai - p);
     };
+    // BATCH: every partner value is requested before the first pair is formed (one LDS
+    // latency per frame instead of one per pair; costs CPL*L registers)
+    float2 recv[BATCH ? CPL * (L / 2) : 1];
+    if constexpr (BATCH) {
+        static_for<0, CPL>([&](auto cc) {
+            constexpr int c = decltype(cc)::value;
+            static_for<0, L / 2>([&](auto tc) {
+                constexpr int t = decltype(tc)::value;
+                constexpr int ps = (CPL - 1 - c) * L + ce_pos(L, L - 1 - t);
+                recv[c * (L / 2) + t].x = __shfl(v[ps].x, partner, 64);
+                recv[c * (L / 2) + t].y = __shfl(v[ps].y, partner, 64);
+            });
+        });
+    }
     static_for<0, CPL>([&](auto cc) {
         constexpr int c = decltype(cc)::value;
         static_for<0, L / 2>([&](auto tc) {
@@ -184,10 +198,14 @@ __device__ __forceinline__ void untangle2(const float2 (&v)[Geo2<NC>::P], int j,
             constexpr int pb = c * L + ce_pos(L, t);
             constexpr int ps = (CPL - 1 - c) * L + ce_pos(L, L - 1 - t);
             const float2 b = v[pb];
-            const float2 send = v[ps];
             float2 r;
-            r.x = __shfl(send.x, partner, 64);
-            r.y = __shfl(send.y, partner, 64);
+            if constexpr (BATCH) {
+                r = recv[c * (L / 2) + t];
+            } else {
+                const float2 send = v[ps];
+                r.x = __shfl(send.x, partner, 64);
+                r.y = __shfl(send.y, partner, 64);
+            }
             // lane 0 pairs inside its own registers: Z[(CPL-c) % CPL][c ? L-1-t : (L-t) % L]
             constexpr int c0 = (CPL - c) % CPL;
             constexpr int k20 = c == 0 ? (L - t) % L : L - 1 - t;
@@ -223,12 +241,11 @@ __device__ __forceinline__ void untangle2(const float2 (&v)[Geo2<NC>::P], int j,
 // lib.rs:131-132 on the |X| row in `region`: round r gives lane j mel r*L + j.
 // wt / rounds / k0: the float4 weight rows, the per-round {row, steps} and the per-lane start
 // bins (a.mel4_* in HBM, or their copies in LDS).
-template <int NC>
+template <int NC, int U = 4>
 __device__ __forceinline__ void mel4(const StftLaunch& a, const float* region, const float4* wt,
                                      const int2* rounds, const int* k0, int j, uint64_t g,
                                      bool valid) {
     constexpr int L = Geo2<NC>::L;
-    constexpr int U = 4;
     const int n_mels = a.n_mels;
     const bool db = a.out_kind == OUT_MEL_AMP_DB;
     float* out = static_cast<float*>(a.out) + g * (uint64_t)n_mels;

@@ -16,6 +16,7 @@
 // reflected). The mel weights are copied into LDS once per block.
 #include "stft2_core.hpp"
 
+#include <cstdlib>
 #include <type_traits>
 
 namespace thesia {
@@ -27,7 +28,11 @@ struct Geo3 {
     static constexpr int SH = P / 4;                      // points per lane a hop moves
     static constexpr int STREAMS = kWaves * FPW;          // streams (= frames in flight) per block
     static constexpr int TW_FLOATS = 2 * P * L;           // W_NC^{j*k1}, [P][L] float2
-    static constexpr int BASE_FLOATS = G2::WIN_FLOATS + TW_FLOATS + STREAMS * RS;
+    // window per lane: row j holds (w[2m], w[2m+1]) for m = L*n1 + j, n1 < P, read as float4;
+    // row stride 2P + 4 floats keeps 16 lanes of a ds_read_b128 group on distinct banks
+    static constexpr int WL_STRIDE = 2 * P + 4;
+    static constexpr int WL_FLOATS = L * WL_STRIDE;
+    static constexpr int BASE_FLOATS = WL_FLOATS + TW_FLOATS + STREAMS * RS;
     static_assert(P % 4 == 0, "hop = n_fft/4 must move whole points per lane");
 };
 
@@ -87,9 +92,14 @@ struct Chunk<2, IN_S16> {
 };
 
 // OK: 0 complex, 1 linear kinds, 2 mel kinds. C: 1 mono, 2 stereo (interleaved); INF: f32 / s16.
-template <int NC, int OK, int C, int INF>
+// VAR (experiments, THESIA_STFT_VARIANT): bit0 = per-pair partner exchange instead of the
+// batched one (measured 0.07 ms slower); ablations (outputs wrong, timing only): bit1 = no mel
+// projection, bit2 = no FFT (stages and transposes skipped), bit3 = no untangle / |X| / mel;
+// bit4 = mel with 4 float4 steps per LDS round trip instead of 8.
+template <int NC, int OK, int C, int INF, int VAR = 0>
 __global__ void __launch_bounds__(kBlock, 2)
 stft3_kernel(StftLaunch a, uint64_t fps) {
+    constexpr bool kBatch = (VAR & 1) == 0;
     using G = Geo2<NC>;
     using G3 = Geo3<NC>;
     using CK = Chunk<C, INF>;
@@ -98,9 +108,9 @@ stft3_kernel(StftLaunch a, uint64_t fps) {
     constexpr int P = G::P, L = G::L, FPW = G::FPW, F = G::F, SH = G3::SH;
 
     extern __shared__ __attribute__((aligned(16))) float lds[];
-    float* wtab = lds;
-    float2* twtab = reinterpret_cast<float2*>(lds + G::WIN_FLOATS);
-    float* work = lds + G::WIN_FLOATS + G3::TW_FLOATS;
+    float* wtl = lds;
+    float2* twtab = reinterpret_cast<float2*>(lds + G3::WL_FLOATS);
+    float* work = lds + G3::WL_FLOATS + G3::TW_FLOATS;
     // mel tables in LDS: weight rows, then the per-lane start bins, then the round table
     float4* mel_lds = reinterpret_cast<float4*>(lds + G3::BASE_FLOATS);
     int* k0_lds = reinterpret_cast<int*>(mel_lds + (OK == 2 ? a.mel4_rows * L : 0));
@@ -109,7 +119,10 @@ stft3_kernel(StftLaunch a, uint64_t fps) {
     const int slot = lane / L, j = lane % L;
     const int partner = slot * L + ((L - j) % L);
 
-    for (int i = threadIdx.x; i < 2 * NC; i += kBlock) wtab[i] = a.wpad[i] * 0.5f;  // exact
+    for (int i = threadIdx.x; i < 2 * NC; i += kBlock) {  // w/2 is exact (realfft's 1/2)
+        const int m = i >> 1, jj = m % L, n1 = m / L;
+        wtl[jj * G3::WL_STRIDE + 2 * n1 + (i & 1)] = a.wpad[i] * 0.5f;
+    }
     if constexpr (OK == 2) {
         const int nw = a.mel4_rows * L;
         for (int i = threadIdx.x; i < nw; i += kBlock) mel_lds[i] = a.mel4_wt[i];
@@ -146,7 +159,7 @@ stft3_kernel(StftLaunch a, uint64_t fps) {
         for (int c = 0; c < G::CPL; ++c) asm volatile("" : "+v"(ub[c].x), "+v"(ub[c].y));
         int wj = j;
         asm volatile("" : "+v"(wj));
-        const float2* wrow = reinterpret_cast<const float2*>(wtab) + wj;
+        const float4* wrow = reinterpret_cast<const float4*>(wtl + wj * G3::WL_STRIDE);
         int64_t start = 0;
         if (valid) {
             if (g >= g_end || g < g_beg) {
@@ -158,9 +171,10 @@ stft3_kernel(StftLaunch a, uint64_t fps) {
             }
             start = (int64_t)(g - g_beg) * hop - NC;  // half_win = NC, pad_left = 0
         }
-        // ---- the frame's raw samples ----
+        // ---- the frame's raw samples (a hop: shift by SH points + the prefetched new ones) ----
+        // (a rotating slot map instead of the shift was measured 1.05 ms slower: the switch
+        // over four slot maps keeps all P raw points live and spills in the hot loop)
         if (pre_ok) {
-            // shift by one hop, then the prefetched new points (same lane, SH further on)
 #pragma unroll
             for (int n1 = 0; n1 < P - SH; ++n1) raw[n1] = raw[n1 + SH];
 #pragma unroll
@@ -181,6 +195,14 @@ stft3_kernel(StftLaunch a, uint64_t fps) {
 #pragma unroll
             for (int n1 = 0; n1 < P; ++n1) raw[n1] = make_float2(0.f, 0.f);
         }
+        // window (lib.rs:379, with the 1/2 of realfft.rs:148-154 folded in)
+        float2 v[P];
+        static_for<0, P / 2>([&](auto qc) {
+            constexpr int q = decltype(qc)::value;
+            const float4 w = wrow[q];
+            v[2 * q] = make_float2(raw[2 * q].x * w.x, raw[2 * q].y * w.y);
+            v[2 * q + 1] = make_float2(raw[2 * q + 1].x * w.z, raw[2 * q + 1].y * w.w);
+        });
         // ---- prefetch the next frame's hop of new samples (its points P-SH .. P-1) ----
         {
             const int64_t nstart = start + hop;
@@ -194,16 +216,12 @@ stft3_kernel(StftLaunch a, uint64_t fps) {
             }
             pre_ok = nxt;
         }
-        // ---- window (lib.rs:379, the 1/2 of realfft.rs:148-154 folded in) and the FFT ----
-        float2 v[P];
-#pragma unroll
-        for (int n1 = 0; n1 < P; ++n1) {
-            const float2 w = wrow[L * n1];
-            v[n1] = make_float2(raw[n1].x * w.x, raw[n1].y * w.y);
-        }
-        fft2<NC>(v, region, j, TwTable{twtab + wj, L});
-        if constexpr (OK == 2) {
-            untangle2<NC>(v, j, partner, ub, [&](int k, float xr, float xi) {
+        if constexpr ((VAR & 4) == 0) fft2<NC>(v, region, j, TwTable{twtab + wj, L});
+        else pin(v);
+        if constexpr (OK == 2 && (VAR & 8) != 0) {  // ablation: no untangle / |X| / mel
+            pin(v);
+        } else if constexpr (OK == 2) {
+            untangle2<NC, kBatch>(v, j, partner, ub, [&](int k, float xr, float xi) {
                 region[k] = __builtin_amdgcn_sqrtf(__builtin_fmaf(xr, xr, xi * xi));  // |X| (lib.rs:124)
             });
             if (j == 0) {
@@ -211,17 +229,18 @@ stft3_kernel(StftLaunch a, uint64_t fps) {
                 for (int k = F; k < G::F4; ++k) region[k] = 0.0f;
             }
             wave_lds_sync();
-            mel4<NC>(a, region, mel_lds, rd_lds, k0_lds, j, g, valid);
+            // U = 8 float4 steps per LDS round trip (the FFT's registers are free by now)
+            if constexpr ((VAR & 2) == 0) mel4<NC, (VAR & 16) ? 4 : 8>(a, region, mel_lds, rd_lds, k0_lds, j, g, valid);
         } else if constexpr (OK == 0) {
             float2* crow = reinterpret_cast<float2*>(a.out) + g * F;
-            untangle2<NC>(v, j, partner, ub, [&](int k, float xr, float xi) {
+            untangle2<NC, kBatch>(v, j, partner, ub, [&](int k, float xr, float xi) {
                 if (valid) crow[k] = make_float2(xr, xi);
             });
         } else {
             const int kind = a.out_kind;
             const bool power = kind == OUT_POWER || kind == OUT_POWER_DB;
             const bool db = kind == OUT_AMP_DB || kind == OUT_POWER_DB;
-            untangle2<NC>(v, j, partner, ub, [&](int k, float xr, float xi) {
+            untangle2<NC, kBatch>(v, j, partner, ub, [&](int k, float xr, float xi) {
                 const float p2 = __builtin_fmaf(xr, xr, xi * xi);
                 region[k] = power ? p2 : __builtin_amdgcn_sqrtf(p2);
             });
@@ -248,11 +267,26 @@ static int lds3_bytes(const StftLaunch& a, bool mel) {
             (mel ? (a.mel4_rows * 4 + a.mel4_rounds) * Geo2<NC>::L + 2 * a.mel4_rounds : 0)) * 4;
 }
 
-template <int NC, int OK, int C, int INF>
+template <int NC, int OK, int C, int INF, int VAR = 0>
 static int launch3_k(const StftLaunch& a, hipStream_t stream) {
+#ifdef THESIA_EXPERIMENTS
+    if constexpr (VAR == 0 && NC == 1024 && OK == 2 && C == 2 && INF == IN_F32) {
+        const char* e = getenv("THESIA_STFT_VARIANT");
+        switch (e ? atoi(e) : 0) {
+            case 1: return launch3_k<NC, OK, C, INF, 1>(a, stream);
+            case 2: return launch3_k<NC, OK, C, INF, 2>(a, stream);
+            case 4: return launch3_k<NC, OK, C, INF, 4>(a, stream);
+            case 6: return launch3_k<NC, OK, C, INF, 6>(a, stream);
+            case 8: return launch3_k<NC, OK, C, INF, 8>(a, stream);
+            case 12: return launch3_k<NC, OK, C, INF, 12>(a, stream);
+            case 16: return launch3_k<NC, OK, C, INF, 16>(a, stream);
+            default: break;
+        }
+    }
+#endif
     const int lds = lds3_bytes<NC>(a, OK == 2);
     if (lds > 163840) return -2;
-    auto kern = stft3_kernel<NC, OK, C, INF>;
+    auto kern = stft3_kernel<NC, OK, C, INF, VAR>;
     if (hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
                             hipFuncAttributeMaxDynamicSharedMemorySize, lds) != hipSuccess)
         return -1;

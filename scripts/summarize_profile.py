@@ -18,7 +18,7 @@ import sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-def per_kernel(path, match="stft_kernel"):
+def per_kernel(path, match="stft"):
     vals = collections.defaultdict(list)
     meta = {}
     for r in csv.DictReader(open(path)):
