@@ -178,6 +178,19 @@ int thesia_grey_to_rgb(const float* grey, uint32_t width, uint32_t height, uint3
 int thesia_wav_to_image(const float* wav, size_t n, uint32_t nwidth, uint32_t nheight,
                         float amp_min, float amp_max, uint8_t* out, size_t cap);
 
+/* Device-resident display (HBM pointers on the current device; synchronous). Used by the
+ * batched render pipeline (thesia/pipeline.py) where spectrograms never leave HBM. */
+/* max / min of n f32 values (lib.rs:194-207 per track; NaN -> *has_nan, like the
+ * ndarray-stats error the reference maps to -inf / +inf). n == 0 gives -inf / +inf. */
+int thesia_minmax_device(const float* d_x, uint64_t n, float* max, float* min, int* has_nan);
+/* spec_to_grey on HBM buffers -- display.rs:44-54. d_grey holds H * T floats
+ * (thesia_spec_grey_height). */
+int thesia_spec_to_grey_device(const float* d_spec, size_t T, size_t bins, float up_ratio,
+                               float max, float min, float* d_grey);
+/* grey_to_rgb on HBM buffers -- display.rs:56-61. d_rgb holds nh * nw * 3 bytes. */
+int thesia_grey_to_rgb_device(const float* d_grey, uint32_t width, uint32_t height,
+                              uint32_t nwidth, uint32_t nheight, uint8_t* d_rgb);
+
 /* ---------------------------------------------------------------------------------- */
 /* MultiTrack -- lib.rs:72-365 (the viewer's stateful surface)                          */
 /* ---------------------------------------------------------------------------------- */

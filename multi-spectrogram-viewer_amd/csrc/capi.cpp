@@ -341,6 +341,40 @@ int thesia_grey_to_rgb(const float* grey, uint32_t w, uint32_t h, uint32_t nw, u
     GUARD_END
 }
 
+int thesia_minmax_device(const float* d_x, uint64_t n, float* max, float* min, int* has_nan) {
+    GUARD_BEGIN
+    if (!max || !min || (n && !d_x)) return set_error(THESIA_ERR_INVALID_ARG, "null pointer");
+    bool nan = false;
+    int rc = minmax_device(d_x, n, max, min, &nan, default_stream());
+    if (has_nan) *has_nan = nan ? 1 : 0;
+    return rc;
+    GUARD_END
+}
+
+int thesia_spec_to_grey_device(const float* d_spec, size_t T, size_t bins, float up_ratio,
+                               float max, float min, float* d_grey) {
+    GUARD_BEGIN
+    uint32_t H = 0;
+    thesia_spec_grey_height(bins, up_ratio, &H);
+    if (H < bins) return set_error(THESIA_ERR_INVALID_ARG, "up_ratio < 1 (display.rs:47 underflows)");
+    if (T == 0 || H == 0) return THESIA_OK;
+    if (!d_spec || !d_grey) return set_error(THESIA_ERR_INVALID_ARG, "null device pointer");
+    if (launch_spec_to_grey(d_spec, (uint32_t)T, (uint32_t)bins, H, max, min, d_grey, default_stream()))
+        return set_error(THESIA_ERR_DEVICE, "spec_to_grey launch failed");
+    THESIA_HIP(hipStreamSynchronize(default_stream()));
+    return THESIA_OK;
+    GUARD_END
+}
+
+int thesia_grey_to_rgb_device(const float* d_grey, uint32_t w, uint32_t h, uint32_t nw, uint32_t nh,
+                              uint8_t* d_rgb) {
+    GUARD_BEGIN
+    if ((size_t)nw * nh == 0) return THESIA_OK;
+    if (!d_grey || !d_rgb) return set_error(THESIA_ERR_INVALID_ARG, "null device pointer");
+    return grey_to_rgb_device(d_grey, w, h, nw, nh, d_rgb, default_stream());
+    GUARD_END
+}
+
 int thesia_wav_to_image(const float* wav, size_t n, uint32_t nwidth, uint32_t nheight,
                         float amp_min, float amp_max, uint8_t* out, size_t cap) {
     GUARD_BEGIN

@@ -6,6 +6,8 @@
 #include <cstdlib>
 #include <map>
 #include <mutex>
+#include <tuple>
+#include <memory>
 
 #include "host_tables.hpp"
 
@@ -438,31 +440,71 @@ static std::vector<uint8_t> colormap_bytes() {
     return c;
 }
 
+// Lanczos3 tap tables of one (size -> new size) resample, resident in HBM. Cached per
+// (device, size, new size): a batch of same-geometry images uploads them once.
+struct DevTaps {
+    DevBuf left, count, offset, weights;
+    int max_taps = 0;
+};
+
+static int dev_taps(uint32_t n, uint32_t nn, const DevTaps** out) {
+    static std::mutex mu;
+    // intentionally leaked: freeing HBM from a static destructor would race HIP's teardown
+    static auto& cache = *new std::map<std::tuple<int, uint32_t, uint32_t>, std::unique_ptr<DevTaps>>();
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    std::lock_guard<std::mutex> lk(mu);
+    auto key = std::make_tuple(dev, n, nn);
+    auto it = cache.find(key);
+    if (it == cache.end()) {
+        Taps t = lanczos3_taps(n, nn);
+        auto d = std::make_unique<DevTaps>();
+        int rc = d->left.upload(t.left.data(), t.left.size() * 4);
+        if (!rc) rc = d->count.upload(t.count.data(), t.count.size() * 4);
+        if (!rc) rc = d->offset.upload(t.offset.data(), t.offset.size() * 4);
+        if (!rc) rc = d->weights.upload(t.weights.data(), t.weights.size() * 4);
+        if (rc) return rc;
+        d->max_taps = t.max_taps;
+        it = cache.emplace(key, std::move(d)).first;
+    }
+    *out = it->second.get();
+    return THESIA_OK;
+}
+
 int grey_to_rgb_device(const float* d_grey, uint32_t w, uint32_t h, uint32_t nw, uint32_t nh,
                        uint8_t* d_rgb, hipStream_t s) {
     if (nw == 0 || nh == 0) return THESIA_OK;
     if (w == 0 || h == 0) return set_error(THESIA_ERR_INVALID_ARG, "empty grey image");
     // image 0.23.12 resize: vertical_sample (h -> nh) into f32, then horizontal (w -> nw)
-    Taps vt = lanczos3_taps(h, nh), ht = lanczos3_taps(w, nw);
-    DevBuf vl, vc, vo, vw, hl, hc, ho, hw, tmp, cmap;
-    std::vector<uint8_t> cm = colormap_bytes();
-    int rc = vl.upload(vt.left.data(), vt.left.size() * 4);
-    if (!rc) rc = vc.upload(vt.count.data(), vt.count.size() * 4);
-    if (!rc) rc = vo.upload(vt.offset.data(), vt.offset.size() * 4);
-    if (!rc) rc = vw.upload(vt.weights.data(), vt.weights.size() * 4);
-    if (!rc) rc = hl.upload(ht.left.data(), ht.left.size() * 4);
-    if (!rc) rc = hc.upload(ht.count.data(), ht.count.size() * 4);
-    if (!rc) rc = ho.upload(ht.offset.data(), ht.offset.size() * 4);
-    if (!rc) rc = hw.upload(ht.weights.data(), ht.weights.size() * 4);
-    if (!rc) rc = tmp.alloc((size_t)w * nh * sizeof(float));
-    if (!rc) rc = cmap.upload(cm.data(), cm.size());
+    const DevTaps *vt = nullptr, *ht = nullptr;
+    const uint8_t* cmap_ptr = nullptr;
+    int rc = dev_taps(h, nh, &vt);
+    if (!rc) rc = dev_taps(w, nw, &ht);
     if (rc) return rc;
-    if (launch_resize_v(d_grey, w, h, nh, vl.as<int32_t>(), vc.as<int32_t>(), vo.as<int32_t>(),
-                        vw.as<float>(), vt.max_taps, tmp.as<float>(), s))
+    {  // the colormap LUT, once per device
+        static std::mutex mu;
+        static auto& cmaps = *new std::map<int, DevBuf>();  // leaked, see dev_taps
+        int dev = 0;
+        (void)hipGetDevice(&dev);
+        std::lock_guard<std::mutex> lk(mu);
+        DevBuf& cm = cmaps[dev];
+        if (!cm.p) {
+            std::vector<uint8_t> bytes = colormap_bytes();
+            rc = cm.upload(bytes.data(), bytes.size());
+            if (rc) return rc;
+        }
+        cmap_ptr = cm.as<uint8_t>();
+    }
+    DevBuf tmp;
+    rc = tmp.alloc((size_t)w * nh * sizeof(float));
+    if (rc) return rc;
+    if (launch_resize_v(d_grey, w, h, nh, vt->left.as<int32_t>(), vt->count.as<int32_t>(),
+                        vt->offset.as<int32_t>(), vt->weights.as<float>(), vt->max_taps,
+                        tmp.as<float>(), s))
         return set_error(THESIA_ERR_DEVICE, "resize_v launch failed");
-    if (launch_resize_h_rgb(tmp.as<float>(), w, nh, nw, hl.as<int32_t>(), hc.as<int32_t>(),
-                            ho.as<int32_t>(), hw.as<float>(), ht.max_taps, cmap.as<uint8_t>(),
-                            d_rgb, s))
+    if (launch_resize_h_rgb(tmp.as<float>(), w, nh, nw, ht->left.as<int32_t>(),
+                            ht->count.as<int32_t>(), ht->offset.as<int32_t>(),
+                            ht->weights.as<float>(), ht->max_taps, cmap_ptr, d_rgb, s))
         return set_error(THESIA_ERR_DEVICE, "resize_h launch failed");
     THESIA_HIP(hipStreamSynchronize(s));
     return THESIA_OK;

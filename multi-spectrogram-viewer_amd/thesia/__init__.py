@@ -14,7 +14,7 @@ Everything numeric runs in HIP kernels on the GPU; there is no CPU fallback.
     engine.*          the batched device engine (plans / batches resident in HBM)
 """
 from ._lib import ThesiaError, EXPORTED, LIB_PATH  # noqa: F401  (import fails loudly if .so missing)
-from . import windows, mel, utils, display, engine, shard  # noqa: F401
+from . import windows, mel, utils, display, engine, shard, pipeline  # noqa: F401
 from .api import MultiTrack, FreqScale, perform_stft, get_colormap  # noqa: F401
 
 __all__ = ["MultiTrack", "FreqScale", "perform_stft", "get_colormap", "windows", "mel", "utils",

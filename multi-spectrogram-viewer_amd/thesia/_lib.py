@@ -80,6 +80,10 @@ _SIGS = {
     "thesia_spec_to_grey": (_i, [_fp, _sz, _sz, _f, _f, _f, _fp, _sz]),
     "thesia_grey_to_rgb": (_i, [_fp, _u32, _u32, _u32, _u32, _u8p, _sz]),
     "thesia_wav_to_image": (_i, [_fp, _sz, _u32, _u32, _f, _f, _u8p, _sz]),
+    "thesia_minmax_device": (_i, [C.c_void_p, C.c_uint64, C.POINTER(C.c_float), C.POINTER(C.c_float),
+                                  C.POINTER(C.c_int)]),
+    "thesia_spec_to_grey_device": (_i, [C.c_void_p, _sz, _sz, _f, _f, _f, C.c_void_p]),
+    "thesia_grey_to_rgb_device": (_i, [C.c_void_p, _u32, _u32, _u32, _u32, C.c_void_p]),
     "thesia_mt_create": (_i, [C.POINTER(_vp)]),
     "thesia_mt_destroy": (None, [_vp]),
     "thesia_mt_set_setting": (_i, [_vp, _f, _sz, _sz, _i, _f]),

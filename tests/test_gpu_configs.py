@@ -1,0 +1,94 @@
+"""GPU parity on the BASELINE.json configurations at sizes the
+oracle finishes in seconds, plus size-independent properties at full size.
+
+  C2  the reference's 6 sample rates (5 committed excerpts + the 48 kHz substitute),
+      n_fft 2048 / hop 512, power dB, one batch over all tracks (s16 input, audio.rs:16-19)
+  C3  48 kHz 10 s mono tracks, n_fft 2048 / hop 512, mel-128 + amp dB
+  C5  mixed rates x per-track n_fft in {256..2048}, amp dB -> global range -> grey ->
+      Lanczos3 -> colormap RGB (thesia.pipeline), bytes checked against the oracle display
+      path run on the device's own dB (bit-exact), dB against the oracle (tolerance)
+"""
+import os
+
+import numpy as np
+import pytest
+
+import oracle_ffi as O
+from thesia import engine, pipeline, shard
+from tolerances import DB_MAX, DB_P9999, db_clamped_err
+
+pytestmark = pytest.mark.gpu
+
+
+def _excerpts_s16(golden_dir):
+    z = np.load(os.path.join(golden_dir, "samples_excerpt.npz"))
+    out = [(z[f"pcm_{t}"], int(z[f"sr_{t}"])) for t in ["8k", "16k", "22k05", "24k", "44k1"]]
+    from scipy.signal import resample_poly  # the 48 kHz substitute
+    x48 = np.clip(np.round(resample_poly(z["pcm_24k"].astype(np.float64), 2, 1)), -32768, 32767)
+    out.append((x48.astype(np.int16), 48000))
+    return out
+
+
+def test_c2_six_sample_rates_power_db(golden_dir):
+    tracks = _excerpts_s16(golden_dir)
+    n_fft, hop = 2048, 512
+    plan = engine.Plan(n_fft, n_fft, hop, engine.OUT_POWER_DB)
+    flat = np.concatenate([t for t, _ in tracks])
+    offs = np.cumsum([0] + [len(t) for t, _ in tracks[:-1]])
+    lens = [len(t) for t, _ in tracks]
+    din = engine.DeviceBuffer.from_host(flat)
+    T = engine.Batch.frames_for(plan, lens)
+    dout = engine.DeviceBuffer(T * plan.row_bins * 4)
+    b = engine.Batch(plan, din, offs, lens, dout, input_format=engine.IN_S16, channels=1)
+    b.run()
+    engine.synchronize()
+    got = dout.to_host(np.float32, (T, plan.row_bins))
+    for k, (pcm, sr) in enumerate(tracks):
+        x = (0.0 + pcm.astype(np.float32) / np.float32(32768.0)).astype(np.float32)  # lib.rs:42 fold
+        ref = O.power_to_db_default(O.norm_sqr(O.perform_stft(x, n_fft, hop, n_fft)))
+        g = got[int(b.frame0[k]):int(b.frame0[k + 1])]
+        assert g.shape == ref.shape
+        mx, p = db_clamped_err(g, ref)
+        assert mx <= DB_MAX and p <= DB_P9999, (sr, mx, p)
+
+
+def test_c3_mel128_mono_10s():
+    n_tracks, n = 6, 480000
+    pcm = [engine.synth_pcm_host(1, i, n, 48000)[:, 0] for i in range(n_tracks)]
+    x = np.stack([p.astype(np.float32) / np.float32(32768.0) for p in pcm])
+    plan = engine.Plan(2048, 2048, 512, engine.OUT_MEL_AMP_DB, sr=48000, n_mels=128)
+    din = engine.DeviceBuffer.from_host(x)
+    T = engine.Batch.frames_for(plan, [n] * n_tracks)
+    assert T == 938 * n_tracks
+    dout = engine.DeviceBuffer(T * 128 * 4)
+    b = engine.Batch(plan, din, np.arange(n_tracks) * n, [n] * n_tracks, dout)
+    b.run()
+    engine.synchronize()
+    got = dout.to_host(np.float32, (T, 128))
+    fb = O.calc_mel_fb(48000, 2048, 128)
+    for k in (0, n_tracks - 1):
+        ref = O.amp_to_db_default(O.dot(O.norm(O.perform_stft(x[k], 2048, 512, 2048)), fb))
+        mx, p = db_clamped_err(got[938 * k:938 * (k + 1)], ref)
+        assert mx <= DB_MAX and p <= DB_P9999, (k, mx, p)
+    assert np.isfinite(got).all()
+
+
+def test_c5_mixed_rate_render_pipeline():
+    tracks = pipeline.c5_tracks(12, seconds=1.0)  # every (rate, n_fft) pair of the generator
+    out = pipeline.render_tracks(tracks, px_per_sec=100.0, nheight=120, keep_db=True)
+    # global range over all tracks (lib.rs:194-209) from the device's own dB
+    gmax, gmin, max_sr = shard.global_db_range(max(r.spec_max for r in out),
+                                               min(r.spec_min for r in out),
+                                               max(t.sr for t in tracks))
+    for t, r in zip(tracks, out):
+        x = (t.pcm.astype(np.float32) / np.float32(32768.0)).astype(np.float32)
+        x = (np.float32(0.0) + x).astype(np.float32)
+        ref_db = O.amp_to_db_default(O.norm(O.perform_stft(x, t.n_fft, t.n_fft // 4, t.n_fft)))
+        assert r.db.shape == ref_db.shape
+        mx, p = db_clamped_err(r.db, ref_db)
+        assert mx <= DB_MAX and p <= DB_P9999, (t.sr, t.n_fft, mx, p)
+        assert (r.spec_max, r.spec_min) == (float(r.db.max()), float(r.db.min()))
+        up = shard.up_ratio(t.sr, max_sr, freq_scale_mel=False)
+        grey = O.spec_to_grey(r.db, up, gmax, gmin)
+        img, _ = O.grey_to_rgb(grey, r.nwidth, 120)
+        assert r.rgb == img.tobytes(), (t.sr, t.n_fft)  # display path bit-exact
