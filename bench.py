@@ -36,12 +36,15 @@ HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s HBM3E (spec)
 def parse():
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--workload", choices=["c4", "c3", "c5"], default="c4",
+                   help="c4 (default, BASELINE.json metric): 48 kHz 30 s stereo, mel-128; "
+                        "c3: 48 kHz 10 s mono, mel-128; c5: mixed rates / n_fft, dB + RGB render")
     p.add_argument("--steps", type=int, default=20)
     p.add_argument("--warmup", type=int, default=3)
     p.add_argument("--tracks", type=int, default=1000, help="tracks per GPU")
-    p.add_argument("--seconds", type=float, default=30.0)
+    p.add_argument("--seconds", type=float, default=None, help="default 30 (c4) / 10 (c3, c5)")
     p.add_argument("--sr", type=int, default=48000)
-    p.add_argument("--channels", type=int, default=2)
+    p.add_argument("--channels", type=int, default=None, help="default 2 (c4) / 1 (c3, c5)")
     p.add_argument("--input", choices=["f32", "s16"], default="f32")
     p.add_argument("--n-fft", type=int, default=2048)
     p.add_argument("--hop", type=int, default=512)
@@ -51,7 +54,12 @@ def parse():
     p.add_argument("--cpu-workers", type=int, default=16)
     p.add_argument("--variants", default="", help="experiment: comma list of THESIA_STFT_VARIANT "
                    "values to A/B (interleaved rounds, one process); prints per-variant kernel ms")
-    return p.parse_args()
+    a = p.parse_args()
+    if a.seconds is None:
+        a.seconds = 30.0 if a.workload == "c4" else 10.0
+    if a.channels is None:
+        a.channels = 2 if a.workload == "c4" else 1
+    return a
 
 
 def dist_setup(args):
@@ -140,11 +148,82 @@ def traffic_from_profile(workload_key):
         return None
 
 
+def main_c5(args, ws, rank, pg):
+    """C5 (BASELINE.json configs[4]): mixed-rate tracks with per-track n_fft, amp dB, global
+    range exchange, grey + Lanczos3 + colormap RGB for every track (thesia.pipeline). One step =
+    spectrogram launches for every geometry group + the display path of every track, the RGB
+    images left in HBM (the copy to the host that get_spec_image implies, lib.rs:294-298, is
+    timed separately: PCIe-inclusive, never the reported value)."""
+    from thesia import pipeline
+
+    total = args.tracks * ws
+    gen = pipeline.c5_tracks(total, seconds=0.0)  # geometry only (empty PCM) for the partition
+    costs = [shard.track_cost(int(round(args.seconds * t.sr)), t.n_fft, t.n_fft // 4, t.n_fft)
+             for t in gen]
+    mine = shard.assign_tracks(costs, ws)[rank]
+    tracks = []
+    for i in mine:  # the generator is indexed by the global track id
+        tracks += pipeline.c5_tracks(1, seconds=args.seconds, first=i, channels=args.channels)
+    p = pipeline.RenderPipeline(tracks, px_per_sec=100.0, nheight=500)
+
+    def step(want_rgb=False):
+        # images stay in HBM in the timed step (inputs resident, outputs resident); the
+        # host-copy-inclusive rate is measured separately below (DESIGN.md §6)
+        p.run_spectrograms()
+        p.render(group=None, want_rgb=want_rgb)
+
+    for _ in range(args.warmup):
+        step()
+    engine.synchronize()
+    barrier(pg)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    engine.synchronize()
+    barrier(pg)
+    dt = max_over_ranks(pg, (time.perf_counter() - t0) / args.steps)
+    t0 = time.perf_counter()
+    step(want_rgb=True)
+    engine.synchronize()
+    dt_host = max_over_ranks(pg, time.perf_counter() - t0)
+    # spectrogram kernels alone (HIP events per group launch)
+    kms = sum(b.run_timed(3) / 3 for _, _, _, b in p.groups)
+    in_bytes = sum(t.pcm.nbytes for t in tracks)
+    out_bytes = sum(b.total_frames * pl.row_bins * 4 for pl, _, _, b in p.groups)
+    achieved = (in_bytes + out_bytes) / (kms * 1e-3) / 1e9
+    frames_all = frames_all_ranks(pg, p.total_frames)
+    if rank == 0:
+        print(json.dumps({
+            "metric": "STFT frames/sec (n_fft=2048 hop=512) at 1/2/4/8 GPUs; % HBM roofline",
+            "value": frames_all / dt, "unit": "frames/s", "n_gpus": ws, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": dt * 1e3, "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": "f32",
+            "data": "synthetic (int16 chirp + noise, seeded per track), resident in HBM",
+            "config": {"workload": f"C5: {total} mixed-rate tracks (8-48 kHz) x {args.seconds:g} s, "
+                                   f"n_fft 256-2048 per track, hop n_fft/4, amp dB + global range + "
+                                   f"grey + Lanczos3 + colormap RGB at 100 px/s x 500 px",
+                       "tracks_per_gpu": len(tracks), "images_per_s": total / dt,
+                       "geometry_groups": len(p.groups), "frames_per_gpu": p.total_frames,
+                       "ms_per_step_with_rgb_copied_to_host": dt_host * 1e3,
+                       "parallelism": f"file-sharded x{ws} (LPT), one all_reduce of 3 scalars"},
+            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+                         "kernel": "spectrogram launches of all geometry groups",
+                         "kernel_ms": kms, "algorithmic_bytes_per_launch": in_bytes + out_bytes},
+        }), flush=True)
+    p.close()
+
+
 def main():
     args = parse()
     ws, rank, local, pg = dist_setup(args)
     # one rank per GPU; on a box with fewer GPUs than ranks (a rehearsal) ranks share devices
     engine.set_device(local % max(1, engine.device_count()))
+    if args.workload == "c5":
+        main_c5(args, ws, rank, pg)
+        if pg is not None:
+            pg.destroy_process_group()
+        return
     n_samples = int(round(args.seconds * args.sr))
     kind = {"mel_db": engine.OUT_MEL_AMP_DB, "amp_db": engine.OUT_AMP_DB,
             "power_db": engine.OUT_POWER_DB, "complex": engine.OUT_COMPLEX}[args.output]
@@ -215,7 +294,7 @@ def main():
         "dtype": "f32",
         "data": "synthetic (int16-quantised chirp + noise, seeded per track), resident in HBM",
         "config": {
-            "workload": f"C4 per-GPU shard: {args.tracks} x {args.sr/1000:g} kHz {args.seconds:g} s "
+            "workload": f"{args.workload.upper()} per-GPU shard: {n_local} x {args.sr/1000:g} kHz {args.seconds:g} s "
                         f"{'stereo' if args.channels == 2 else str(args.channels) + '-ch'} tracks per GPU "
                         f"({args.input} interleaved), n_fft {args.n_fft} hop {args.hop} Hann, "
                         f"sum-downmix, {'mel-' + str(args.n_mels) + ' + amp dB' if kind == engine.OUT_MEL_AMP_DB else args.output}",
@@ -234,7 +313,7 @@ def main():
             "unit": "GB/s",
             "frac": achieved / HBM_PEAK_GBS,
             "traffic": traffic_from_profile(wkey),
-            "kernel": "thesia::stft_kernel (fused downmix+frame+window+rFFT+|X|+mel+dB)",
+            "kernel": "thesia::stft3_kernel (streaming: downmix+frame+window+rFFT+|X|+mel+dB, one launch)",
             "kernel_ms": kms,
             "algorithmic_bytes_per_launch": abytes,
         }

@@ -191,6 +191,18 @@ int thesia_spec_to_grey_device(const float* d_spec, size_t T, size_t bins, float
 int thesia_grey_to_rgb_device(const float* d_grey, uint32_t width, uint32_t height,
                               uint32_t nwidth, uint32_t nheight, uint8_t* d_rgb);
 
+/* Batched display for n tracks whose dB spectrograms are packed in one HBM buffer (rows
+ * [row0[i], row0[i+1]) of `bins` floats; row0 is a host array of n+1 entries) -- the
+ * per-track max/min of update_spec_greys (lib.rs:194-207) in one launch, and grey + Lanczos3
+ * + colormap for every track in one stream pass (lib.rs:249-260, 294-298): track i's RGB image
+ * [nheight, nwidth[i], 3] lands at d_rgb + rgb_off[i] (host arrays of n entries). */
+int thesia_minmax_segments_device(const float* d_spec, const uint64_t* row0, size_t bins,
+                                  size_t n, float* max, float* min, int* has_nan);
+int thesia_render_rgb_batch_device(const float* d_spec, const uint64_t* row0, size_t bins,
+                                   size_t n, const float* up_ratio, const uint32_t* nwidth,
+                                   uint32_t nheight, float max, float min, uint8_t* d_rgb,
+                                   const uint64_t* rgb_off);
+
 /* ---------------------------------------------------------------------------------- */
 /* MultiTrack -- lib.rs:72-365 (the viewer's stateful surface)                          */
 /* ---------------------------------------------------------------------------------- */

@@ -375,6 +375,27 @@ int thesia_grey_to_rgb_device(const float* d_grey, uint32_t w, uint32_t h, uint3
     GUARD_END
 }
 
+int thesia_minmax_segments_device(const float* d_spec, const uint64_t* row0, size_t bins,
+                                  size_t n, float* max, float* min, int* has_nan) {
+    GUARD_BEGIN
+    if (n && (!d_spec || !row0 || !max || !min || !has_nan))
+        return set_error(THESIA_ERR_INVALID_ARG, "null pointer");
+    return minmax_segments_device(d_spec, row0, bins, n, max, min, has_nan, default_stream());
+    GUARD_END
+}
+
+int thesia_render_rgb_batch_device(const float* d_spec, const uint64_t* row0, size_t bins,
+                                   size_t n, const float* up_ratio, const uint32_t* nwidth,
+                                   uint32_t nheight, float max, float min, uint8_t* d_rgb,
+                                   const uint64_t* rgb_off) {
+    GUARD_BEGIN
+    if (n && (!d_spec || !row0 || !up_ratio || !nwidth || !d_rgb || !rgb_off))
+        return set_error(THESIA_ERR_INVALID_ARG, "null pointer");
+    return render_rgb_batch_device(d_spec, row0, bins, n, up_ratio, nwidth, nheight, max, min,
+                                   d_rgb, rgb_off, default_stream());
+    GUARD_END
+}
+
 int thesia_wav_to_image(const float* wav, size_t n, uint32_t nwidth, uint32_t nheight,
                         float amp_min, float amp_max, uint8_t* out, size_t cap) {
     GUARD_BEGIN

@@ -103,6 +103,52 @@ int launch_minmax(const float* x, uint64_t n, float* partial, int* nan_flag, int
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
+// K3 over many tracks at once: segment s = elements [seg0[s], seg0[s+1]) of x; blockIdx.y is
+// the segment, blockIdx.x one of nper blocks striding through it.
+__global__ void minmax_seg_kernel(const float* x, const uint64_t* seg0, int nper, float* partial,
+                                  int* nan_flag) {
+    const int seg = blockIdx.y;
+    const uint64_t beg = seg0[seg], end = seg0[seg + 1];
+    float mx = -INFINITY, mn = INFINITY;
+    int nan = 0;
+    for (uint64_t i = beg + blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < end;
+         i += (uint64_t)nper * blockDim.x) {
+        const float v = x[i];
+        if (v != v) nan = 1;
+        mx = fmaxf(mx, v);
+        mn = fminf(mn, v);
+    }
+    __shared__ float smx[256], smn[256];
+    __shared__ int snan;
+    if (threadIdx.x == 0) snan = 0;
+    __syncthreads();
+    smx[threadIdx.x] = mx;
+    smn[threadIdx.x] = mn;
+    if (nan) snan = 1;
+    __syncthreads();
+    for (int st = 128; st > 0; st >>= 1) {
+        if ((int)threadIdx.x < st) {
+            smx[threadIdx.x] = fmaxf(smx[threadIdx.x], smx[threadIdx.x + st]);
+            smn[threadIdx.x] = fminf(smn[threadIdx.x], smn[threadIdx.x + st]);
+        }
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) {
+        const uint64_t o = ((uint64_t)seg * nper + blockIdx.x) * 2;
+        partial[o] = smx[0];
+        partial[o + 1] = smn[0];
+        if (snan) atomicOr(nan_flag + seg, 1);
+    }
+}
+
+int launch_minmax_seg(const float* x, const uint64_t* seg0, int n_seg, int nper, float* partial,
+                      int* nan_flag, hipStream_t s) {
+    if (n_seg == 0) return 0;
+    hipLaunchKernelGGL(minmax_seg_kernel, dim3(nper, n_seg), dim3(256), 0, s, x, seg0, nper,
+                       partial, nan_flag);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
 // ------------------------------------------------------------------------------------
 // K4 spec_to_grey (display.rs:44-54): grey[y][x], y < H, x < T
 // ------------------------------------------------------------------------------------

@@ -510,6 +510,96 @@ int grey_to_rgb_device(const float* d_grey, uint32_t w, uint32_t h, uint32_t nw,
     return THESIA_OK;
 }
 
+int minmax_segments_device(const float* d_x, const uint64_t* row0, size_t bins, size_t n,
+                           float* mx, float* mn, int* nan, hipStream_t s) {
+    if (n == 0) return THESIA_OK;
+    const int nper = 16;
+    std::vector<uint64_t> seg(n + 1);
+    for (size_t i = 0; i <= n; ++i) seg[i] = row0[i] * bins;
+    DevBuf dseg, part, flag;
+    int rc = dseg.upload(seg.data(), seg.size() * 8);
+    if (!rc) rc = part.alloc(n * nper * 2 * sizeof(float));
+    if (!rc) rc = flag.alloc(n * sizeof(int));
+    if (rc) return rc;
+    THESIA_HIP(hipMemsetAsync(flag.p, 0, n * sizeof(int), s));
+    if (launch_minmax_seg(d_x, dseg.as<uint64_t>(), (int)n, nper, part.as<float>(), flag.as<int>(), s))
+        return set_error(THESIA_ERR_DEVICE, "minmax_seg launch failed");
+    std::vector<float> h(n * nper * 2);
+    std::vector<int> hf(n);
+    THESIA_HIP(hipMemcpyAsync(h.data(), part.p, h.size() * sizeof(float), hipMemcpyDeviceToHost, s));
+    THESIA_HIP(hipMemcpyAsync(hf.data(), flag.p, n * sizeof(int), hipMemcpyDeviceToHost, s));
+    THESIA_HIP(hipStreamSynchronize(s));
+    for (size_t i = 0; i < n; ++i) {
+        float a = -INFINITY, b = INFINITY;  // empty track: ndarray-stats EmptyInput -> -inf / +inf
+        for (int k = 0; k < nper; ++k) {
+            a = fmaxf(a, h[(i * nper + k) * 2]);
+            b = fminf(b, h[(i * nper + k) * 2 + 1]);
+        }
+        mx[i] = a;
+        mn[i] = b;
+        nan[i] = hf[i];
+    }
+    return THESIA_OK;
+}
+
+int render_rgb_batch_device(const float* d_spec, const uint64_t* row0, size_t bins, size_t n,
+                            const float* up_ratio, const uint32_t* nwidth, uint32_t nheight,
+                            float max, float min, uint8_t* d_rgb, const uint64_t* rgb_off,
+                            hipStream_t s) {
+    if (n == 0 || nheight == 0) return THESIA_OK;
+    // workspaces sized for the largest track; launches are stream-ordered, so reusing them
+    // track after track is race-free
+    size_t grey_max = 1, tmp_max = 1;
+    std::vector<uint32_t> H(n);
+    for (size_t i = 0; i < n; ++i) {
+        const uint64_t T = row0[i + 1] - row0[i];
+        const float h = roundf((float)bins * up_ratio[i]);  // display.rs:46
+        H[i] = h > 0.f ? (uint32_t)h : 0u;
+        if (H[i] < bins) return set_error(THESIA_ERR_INVALID_ARG, "up_ratio < 1 (display.rs:47 underflows)");
+        grey_max = std::max<size_t>(grey_max, (size_t)H[i] * T);
+        tmp_max = std::max<size_t>(tmp_max, (size_t)T * nheight);
+    }
+    const uint8_t* cmap_ptr = nullptr;
+    {
+        static std::mutex mu;
+        static auto& cmaps = *new std::map<int, DevBuf>();  // leaked, see dev_taps
+        int dev = 0;
+        (void)hipGetDevice(&dev);
+        std::lock_guard<std::mutex> lk(mu);
+        DevBuf& cm = cmaps[dev];
+        if (!cm.p) {
+            std::vector<uint8_t> bytes = colormap_bytes();
+            int rc = cm.upload(bytes.data(), bytes.size());
+            if (rc) return rc;
+        }
+        cmap_ptr = cm.as<uint8_t>();
+    }
+    DevBuf grey, tmp;
+    int rc = grey.alloc(grey_max * sizeof(float));
+    if (!rc) rc = tmp.alloc(tmp_max * sizeof(float));
+    if (rc) return rc;
+    for (size_t i = 0; i < n; ++i) {
+        const uint32_t T = (uint32_t)(row0[i + 1] - row0[i]);
+        if (T == 0 || nwidth[i] == 0) continue;
+        const DevTaps *vt = nullptr, *ht = nullptr;
+        rc = dev_taps(H[i], nheight, &vt);
+        if (!rc) rc = dev_taps(T, nwidth[i], &ht);
+        if (rc) return rc;
+        if (launch_spec_to_grey(d_spec + row0[i] * bins, T, (uint32_t)bins, H[i], max, min,
+                                grey.as<float>(), s) ||
+            launch_resize_v(grey.as<float>(), T, H[i], nheight, vt->left.as<int32_t>(),
+                            vt->count.as<int32_t>(), vt->offset.as<int32_t>(),
+                            vt->weights.as<float>(), vt->max_taps, tmp.as<float>(), s) ||
+            launch_resize_h_rgb(tmp.as<float>(), T, nheight, nwidth[i], ht->left.as<int32_t>(),
+                                ht->count.as<int32_t>(), ht->offset.as<int32_t>(),
+                                ht->weights.as<float>(), ht->max_taps, cmap_ptr,
+                                d_rgb + rgb_off[i], s))
+            return set_error(THESIA_ERR_DEVICE, "render launch failed");
+    }
+    THESIA_HIP(hipStreamSynchronize(s));
+    return THESIA_OK;
+}
+
 int wav_to_image_device(const float* d_wav, uint64_t n, uint32_t nwidth, uint32_t nheight,
                         float amp_min, float amp_max, uint8_t* d_out, int* panicked,
                         hipStream_t s) {

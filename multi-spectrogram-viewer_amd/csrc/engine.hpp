@@ -92,6 +92,15 @@ int wav_to_image_device(const float* d_wav, uint64_t n, uint32_t nwidth, uint32_
                         float amp_min, float amp_max, uint8_t* d_out, int* panicked,
                         hipStream_t s);
 int minmax_device(const float* d_x, uint64_t n, float* mx, float* mn, bool* nan, hipStream_t s);
+// K3 for n tracks packed in one buffer: rows [row0[i], row0[i+1]) of `bins` floats each.
+int minmax_segments_device(const float* d_x, const uint64_t* row0, size_t bins, size_t n,
+                           float* mx, float* mn, int* nan, hipStream_t s);
+// K4-K6 for n tracks packed in one buffer, one stream, one sync: track i's [T_i, bins] dB rows
+// -> grey [H_i, T_i] (H_i = round(bins * up_ratio[i])) -> Lanczos3 -> RGB at rgb_off[i].
+int render_rgb_batch_device(const float* d_spec, const uint64_t* row0, size_t bins, size_t n,
+                            const float* up_ratio, const uint32_t* nwidth, uint32_t nheight,
+                            float max, float min, uint8_t* d_rgb, const uint64_t* rgb_off,
+                            hipStream_t s);
 
 // sine LUT for the synthetic generator (host copy + lazily uploaded device copy)
 const int16_t* synth_lut_host();

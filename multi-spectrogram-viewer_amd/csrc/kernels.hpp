@@ -85,6 +85,8 @@ int launch_downmix(const void* in, int in_format, int channels, uint64_t n, floa
                    hipStream_t s);
 int launch_minmax(const float* x, uint64_t n, float* partial /*[2*nblk]*/, int* nan_flag,
                   int nblk, hipStream_t s);
+int launch_minmax_seg(const float* x, const uint64_t* seg0, int n_seg, int nper, float* partial,
+                      int* nan_flag, hipStream_t s);
 int launch_spec_to_grey(const float* spec, uint32_t T, uint32_t bins, uint32_t H, float max,
                         float min, float* grey, hipStream_t s);
 int launch_resize_v(const float* in, uint32_t w, uint32_t h, uint32_t nh, const int32_t* left,

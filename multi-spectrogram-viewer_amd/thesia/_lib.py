@@ -84,6 +84,9 @@ _SIGS = {
                                   C.POINTER(C.c_int)]),
     "thesia_spec_to_grey_device": (_i, [C.c_void_p, _sz, _sz, _f, _f, _f, C.c_void_p]),
     "thesia_grey_to_rgb_device": (_i, [C.c_void_p, _u32, _u32, _u32, _u32, C.c_void_p]),
+    "thesia_minmax_segments_device": (_i, [C.c_void_p, _u64p, _sz, _sz, _fp, _fp, C.POINTER(C.c_int)]),
+    "thesia_render_rgb_batch_device": (_i, [C.c_void_p, _u64p, _sz, _sz, _fp, C.POINTER(C.c_uint32),
+                                            _u32, _f, _f, C.c_void_p, _u64p]),
     "thesia_mt_create": (_i, [C.POINTER(_vp)]),
     "thesia_mt_destroy": (None, [_vp]),
     "thesia_mt_set_setting": (_i, [_vp, _f, _sz, _sz, _i, _f]),

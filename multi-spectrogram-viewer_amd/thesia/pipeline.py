@@ -22,7 +22,7 @@ from typing import List, Optional, Sequence
 
 import numpy as np
 
-from ._lib import lib, check
+from ._lib import lib, check, _fp, _u64p
 from . import engine, shard
 
 
@@ -38,7 +38,8 @@ class Track:
 @dataclass
 class Rendered:
     db: Optional[np.ndarray]  # [T, n_fft/2+1] amp dB (only when keep_db)
-    rgb: bytes                # [nheight, nwidth, 3] (display.rs:56-61)
+    rgb: np.ndarray           # u8 [nheight * nwidth * 3] (display.rs:56-61; a view of the
+                              # group's one device-to-host copy)
     nwidth: int
     spec_max: float
     spec_min: float
@@ -52,65 +53,127 @@ def _geometry(t: Track):
     return (t.sr, t.n_fft, win, hop, ch, fmt)
 
 
+class RenderPipeline:
+    """The C5 pipeline with its inputs resident in HBM: `prepare` uploads the tracks and builds
+    one Plan + Batch per geometry group; `run_spectrograms` is one launch per group; `render`
+    runs the global-range exchange and the device display path for every track."""
+
+    def __init__(self, tracks: Sequence[Track], px_per_sec: float = 100.0, nheight: int = 500,
+                 db_range: float = 120.0):
+        self.tracks = list(tracks)
+        self.px_per_sec, self.nheight, self.db_range = px_per_sec, nheight, db_range
+        groups: "OrderedDict[tuple, List[int]]" = OrderedDict()
+        for i, t in enumerate(self.tracks):
+            groups.setdefault(_geometry(t), []).append(i)
+        self.groups = []
+        self.where = {}  # track -> (group index, row offset, T, bins)
+        for (sr, n_fft, win, hop, ch, fmt), idx in groups.items():
+            plan = engine.Plan(n_fft, win, hop, engine.OUT_AMP_DB, sr=sr)
+            flat = np.concatenate([np.ascontiguousarray(self.tracks[i].pcm).reshape(-1) for i in idx])
+            lens = [self.tracks[i].pcm.shape[0] for i in idx]
+            offs = np.cumsum([0] + [self.tracks[i].pcm.size for i in idx[:-1]]).astype(np.uint64)
+            din = engine.DeviceBuffer.from_host(flat)
+            T_all = engine.Batch.frames_for(plan, lens)
+            dout = engine.DeviceBuffer(T_all * plan.row_bins * 4)
+            b = engine.Batch(plan, din, offs, lens, dout, input_format=fmt, channels=ch)
+            g = len(self.groups)
+            self.groups.append((plan, din, dout, b))
+            for k, i in enumerate(idx):
+                f0, f1 = int(b.frame0[k]), int(b.frame0[k + 1])
+                self.where[i] = (g, f0 * plan.row_bins, f1 - f0, plan.row_bins)
+        self.total_frames = sum(grp[3].total_frames for grp in self.groups)
+        # display buffers, sized once
+        self._geo = []
+        max_rgb = 1
+        for i, t in enumerate(self.tracks):
+            _, _, T, bins = self.where[i]
+            nwidth = int(np.float32(px_per_sec) * np.float32(t.pcm.shape[0]) / np.float32(t.sr))
+            self._geo.append(nwidth)
+            max_rgb = max(max_rgb, nwidth * nheight * 3)
+        self._rgb = engine.DeviceBuffer(max_rgb)
+
+    def run_spectrograms(self) -> None:
+        """One kernel launch per geometry group (asynchronous)."""
+        for _, _, _, b in self.groups:
+            b.run()
+
+    def _spec_ptr(self, i):
+        g, row0, T, bins = self.where[i]
+        return C.c_void_p(self.groups[g][2].ptr.value + row0 * 4), T, bins
+
+    def ranges(self):
+        """Per-track (max, min) dB (lib.rs:194-207): one segmented reduction per group."""
+        out = [None] * len(self.tracks)
+        for g, (plan, _, dout, b) in enumerate(self.groups):
+            idx = [i for i in range(len(self.tracks)) if self.where[i][0] == g]
+            n = len(idx)
+            mx = np.empty(n, np.float32)
+            mn = np.empty(n, np.float32)
+            nan = np.empty(n, np.int32)
+            row0 = np.ascontiguousarray(b.frame0, np.uint64)
+            check(lib.thesia_minmax_segments_device(dout.ptr, row0.ctypes.data_as(_u64p), plan.row_bins,
+                                                    n, mx.ctypes.data_as(_fp), mn.ctypes.data_as(_fp),
+                                                    nan.ctypes.data_as(C.POINTER(C.c_int))))
+            for k, i in enumerate(idx):
+                # ndarray-stats max/min error on NaN -> unwrap_or(-inf / +inf) (lib.rs:198-199)
+                out[i] = (-np.inf, np.inf) if nan[k] else (float(mx[k]), float(mn[k]))
+        return out
+
+    def render(self, group=None, keep_db: bool = False, want_rgb: bool = True) -> List[Rendered]:
+        engine.synchronize()
+        ranges = self.ranges()
+        lmx, lmn = shard.local_range([r[0] for r in ranges], [r[1] for r in ranges])
+        lsr = max((t.sr for t in self.tracks), default=0)
+        gmax, gmin, max_sr = shard.global_db_range(lmx, lmn, lsr, db_range=self.db_range, group=group)
+        out: List[Optional[Rendered]] = [None] * len(self.tracks)
+        for g, (plan, _, dout, b) in enumerate(self.groups):
+            idx = [i for i in range(len(self.tracks)) if self.where[i][0] == g]
+            n = len(idx)
+            up = np.array([shard.up_ratio(self.tracks[i].sr, max_sr, freq_scale_mel=False) for i in idx],
+                          np.float32)
+            nw = np.array([self._geo[i] for i in idx], np.uint32)
+            sizes = nw.astype(np.uint64) * self.nheight * 3
+            off = np.concatenate([[0], np.cumsum(sizes)[:-1]]).astype(np.uint64)
+            total = int(sizes.sum())
+            if total > self._rgb.nbytes:
+                self._rgb.close()
+                self._rgb = engine.DeviceBuffer(total)
+            row0 = np.ascontiguousarray(b.frame0, np.uint64)
+            check(lib.thesia_render_rgb_batch_device(
+                dout.ptr, row0.ctypes.data_as(_u64p), plan.row_bins, n, up.ctypes.data_as(_fp),
+                nw.ctypes.data_as(C.POINTER(C.c_uint32)), self.nheight, gmax, gmin, self._rgb.ptr,
+                off.ctypes.data_as(_u64p)))
+            rgb_all = self._rgb.read(np.uint8, total) if want_rgb else None
+            for k, i in enumerate(idx):
+                img = rgb_all[int(off[k]):int(off[k]) + int(sizes[k])] if want_rgb else None
+                db = None
+                if keep_db:
+                    _, row_el, T, bins = self.where[i]
+                    db = dout.read(np.float32, T * bins, row_el).reshape(T, bins)
+                out[i] = Rendered(db, img, int(nw[k]), *ranges[i])
+        return out
+
+    def close(self):
+        for plan, din, dout, b in self.groups[::-1]:
+            b.close()
+            dout.close()
+            din.close()
+            plan.close()
+        self.groups = []
+        self._rgb.close()
+
+
 def render_tracks(tracks: Sequence[Track], px_per_sec: float = 100.0, nheight: int = 500,
                   db_range: float = 120.0, keep_db: bool = False, group=None) -> List[Rendered]:
     """Spectrogram (amp dB) + global range + grey + Lanczos3 + colormap for every track; one
     kernel launch per geometry group. `group`: torch.distributed group for the range exchange
     when tracks are sharded over ranks (None = default group if initialised)."""
-    groups: "OrderedDict[tuple, List[int]]" = OrderedDict()
-    for i, t in enumerate(tracks):
-        groups.setdefault(_geometry(t), []).append(i)
-
-    specs = {}   # track index -> (device buffer, row offset, T, bins) kept alive below
-    keep = []
-    ranges = {}
-    for (sr, n_fft, win, hop, ch, fmt), idx in groups.items():
-        plan = engine.Plan(n_fft, win, hop, engine.OUT_AMP_DB, sr=sr)
-        flat = np.concatenate([np.ascontiguousarray(tracks[i].pcm).reshape(-1) for i in idx])
-        lens = [tracks[i].pcm.shape[0] for i in idx]
-        offs = np.cumsum([0] + [tracks[i].pcm.size for i in idx[:-1]]).astype(np.uint64)
-        din = engine.DeviceBuffer.from_host(flat)
-        T_all = engine.Batch.frames_for(plan, lens)
-        dout = engine.DeviceBuffer(T_all * plan.row_bins * 4)
-        b = engine.Batch(plan, din, offs, lens, dout, input_format=fmt, channels=ch)
-        b.run()
-        engine.synchronize()
-        keep += [plan, din, dout, b]
-        for k, i in enumerate(idx):
-            f0, f1 = int(b.frame0[k]), int(b.frame0[k + 1])
-            specs[i] = (dout, f0 * plan.row_bins, f1 - f0, plan.row_bins)
-            ptr = C.c_void_p(dout.ptr.value + f0 * plan.row_bins * 4)
-            mx, mn, nan = C.c_float(), C.c_float(), C.c_int()
-            check(lib.thesia_minmax_device(ptr, (f1 - f0) * plan.row_bins, C.byref(mx), C.byref(mn),
-                                           C.byref(nan)))
-            # ndarray-stats max/min error on NaN -> unwrap_or(-inf / +inf) (lib.rs:198-199)
-            ranges[i] = (-np.inf, np.inf) if nan.value else (mx.value, mn.value)
-
-    lmx, lmn = shard.local_range([r[0] for r in ranges.values()], [r[1] for r in ranges.values()])
-    lsr = max((t.sr for t in tracks), default=0)
-    gmax, gmin, max_sr = shard.global_db_range(lmx, lmn, lsr, db_range=db_range, group=group)
-
-    out: List[Rendered] = []
-    for i, t in enumerate(tracks):
-        dbuf, row0, T, bins = specs[i]
-        up = shard.up_ratio(t.sr, max_sr, freq_scale_mel=False)
-        H = C.c_uint32()
-        check(lib.thesia_spec_grey_height(bins, up, C.byref(H)))
-        n = t.pcm.shape[0]
-        nwidth = int(np.float32(px_per_sec) * np.float32(n) / np.float32(t.sr))  # lib.rs:296
-        grey = engine.DeviceBuffer(max(1, H.value * T) * 4)
-        rgb = engine.DeviceBuffer(max(1, nwidth * nheight * 3))
-        check(lib.thesia_spec_to_grey_device(C.c_void_p(dbuf.ptr.value + row0 * 4), T, bins, up,
-                                             gmax, gmin, grey.ptr))
-        check(lib.thesia_grey_to_rgb_device(grey.ptr, T, H.value, nwidth, nheight, rgb.ptr))
-        img = rgb.to_host(np.uint8)[: nwidth * nheight * 3].tobytes()
-        db = dbuf.read(np.float32, T * bins, row0).reshape(T, bins) if keep_db else None
-        out.append(Rendered(db, img, nwidth, *ranges[i]))
-        grey.close()
-        rgb.close()
-    for k in keep[::-1]:
-        k.close()
-    return out
+    p = RenderPipeline(tracks, px_per_sec, nheight, db_range)
+    try:
+        p.run_spectrograms()
+        return p.render(group=group, keep_db=keep_db)
+    finally:
+        p.close()
 
 
 def c5_tracks(n_tracks: int, seconds: float = 10.0, seed: int = 0, channels: int = 1,

@@ -91,4 +91,4 @@ def test_c5_mixed_rate_render_pipeline():
         up = shard.up_ratio(t.sr, max_sr, freq_scale_mel=False)
         grey = O.spec_to_grey(r.db, up, gmax, gmin)
         img, _ = O.grey_to_rgb(grey, r.nwidth, 120)
-        assert r.rgb == img.tobytes(), (t.sr, t.n_fft)  # display path bit-exact
+        assert r.rgb.tobytes() == img.tobytes(), (t.sr, t.n_fft)  # display path bit-exact
