@@ -157,6 +157,10 @@ int thesia_batch_run_timed(thesia_batch* batch, void* stream, int iters, float* 
 int thesia_batch_kernel_info(const thesia_batch* batch, int* lds_bytes, int* tile_frames,
                              int* grid);
 
+/* Which fused kernel runs the batch: 1 stft_kernel (general), 2 stft2_kernel (4 waves/SIMD),
+ * 3 stft3_kernel (streaming; win = n_fft, hop = n_fft/4). */
+int thesia_batch_kernel(const thesia_batch* batch, int* kernel);
+
 /* Deterministic synthetic PCM (int16-quantised chirp + noise) written on the device, and
  * its bit-identical host twin. format: thesia_input_format. Layout [track][sample][ch]. */
 int thesia_synth_pcm_device(void* d_out, int format, uint32_t channels, uint64_t n_tracks,

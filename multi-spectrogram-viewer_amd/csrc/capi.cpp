@@ -272,6 +272,12 @@ int thesia_batch_kernel_info(const thesia_batch* batch, int* lds_bytes, int* til
     return THESIA_OK;
 }
 
+int thesia_batch_kernel(const thesia_batch* batch, int* kernel) {
+    if (!batch || !kernel) return set_error(THESIA_ERR_INVALID_ARG, "null pointer");
+    *kernel = reinterpret_cast<const Batch*>(batch)->kernel;
+    return THESIA_OK;
+}
+
 int thesia_synth_pcm_device(void* d_out, int format, uint32_t channels, uint64_t n_tracks,
                             uint64_t n_samples, uint32_t sr, uint64_t seed) {
     GUARD_BEGIN

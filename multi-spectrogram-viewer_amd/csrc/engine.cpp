@@ -367,6 +367,8 @@ int batch_create(Plan* plan, const thesia_batch_desc& d, Batch** out) {
     L.mel4_k0 = plan->mel4_k0.as<int>();
     L.mel4_wt = plan->mel4_wt.as<float4>();
     L.out = d.d_output;
+    // THESIA_GRID=n caps the launch at n blocks (tests: long frame streams on small batches)
+    if (const char* e = getenv("THESIA_GRID")) L.grid = std::max(0, atoi(e));
     // kernel choice: the streaming kernel for its geometry, else the 4-waves/SIMD kernel for
     // its sizes, else the general one. THESIA_STFT_KERNEL=1|2|3 forces one (experiments).
     b->kernel = plan->use_v2 ? 2 : 1;

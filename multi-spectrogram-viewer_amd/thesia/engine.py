@@ -155,6 +155,13 @@ class Batch:
         check(lib.thesia_batch_kernel_info(self.handle, C.byref(lds), C.byref(tile), C.byref(grid)))
         return {"lds_bytes": lds.value, "tile_frames": tile.value}
 
+    @property
+    def kernel(self) -> int:
+        """1 stft_kernel, 2 stft2_kernel, 3 stft3_kernel (streaming)."""
+        k = C.c_int()
+        check(lib.thesia_batch_kernel(self.handle, C.byref(k)))
+        return k.value
+
     def close(self):
         if self.handle and self.handle.value:
             lib.thesia_batch_destroy(self.handle)
