@@ -64,6 +64,9 @@ struct Plan {
     DevBuf mel4_round, mel4_k0, mel4_wt;  // stft2_kernel layout (float4 steps)
     int mel4_rounds = 0;
     size_t mel4_wt_rows = 0;
+    DevBuf tw4a, tw4b, mel5_round, mel5_meta, mel5_wt;  // stft4_kernel (n_fft 2048)
+    int mel5_rounds = 0;
+    size_t mel5_rows = 0;
     bool use_v2 = false;  // stft2_kernel runs this plan (n_fft 256..2048)
     size_t row_bins() const;
     size_t out_elem_bytes() const { return out_kind == OUT_COMPLEX ? 8 : 4; }
@@ -78,7 +81,7 @@ struct Batch {
     DevBuf d_in_off, d_len, d_frame0;
     uint64_t total_frames = 0;
     StftLaunch launch{};
-    int kernel = 1;  // 1 stft_kernel, 2 stft2_kernel, 3 stft3_kernel (streaming)
+    int kernel = 1;  // 1 stft_kernel, 2 stft2_kernel, 3 stft3_kernel, 4 stft4_kernel (streaming)
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     ~Batch();
 };

@@ -34,6 +34,34 @@ struct Geo2 {
     static_assert(2 * LDS_BYTES <= 163840, "two blocks per CU");
 };
 
+// One point's worth of input per lane (2 samples x C interleaved channels) and its downmix:
+// f32 as is, s16 as value / 2^15 (audio.rs:16-19, exact), channels summed (lib.rs:42).
+template <int C, int INF>
+struct Chunk;
+template <>
+struct Chunk<1, IN_F32> {
+    using T = float2;
+    __device__ static float2 mix(T x) { return x; }
+};
+template <>
+struct Chunk<2, IN_F32> {
+    using T = float4;
+    __device__ static float2 mix(T x) { return make_float2(x.x + x.y, x.z + x.w); }
+};
+template <>
+struct Chunk<1, IN_S16> {
+    using T = short2;
+    __device__ static float2 mix(T x) { return make_float2((float)x.x / 32768.0f, (float)x.y / 32768.0f); }
+};
+template <>
+struct Chunk<2, IN_S16> {
+    using T = short4;
+    __device__ static float2 mix(T x) {
+        return make_float2((float)x.x / 32768.0f + (float)x.y / 32768.0f,
+                           (float)x.z / 32768.0f + (float)x.w / 32768.0f);
+    }
+};
+
 // Interior frames of f32 mono / stereo input straight from HBM (8 / 16 B per lane); the
 // stereo sum is x[ch0] + x[ch1] (lib.rs:42; the fold's leading 0.0 + only differs for -0).
 template <int NC, int INF>

@@ -63,34 +63,6 @@ __device__ __forceinline__ void load_raw_generic(const StftLaunch& a, float* reg
     }
 }
 
-// One point's worth of input per lane (2 samples x C interleaved channels) and its downmix:
-// f32 as is, s16 as value / 2^15 (audio.rs:16-19, exact), channels summed (lib.rs:42).
-template <int C, int INF>
-struct Chunk;
-template <>
-struct Chunk<1, IN_F32> {
-    using T = float2;
-    __device__ static float2 mix(T x) { return x; }
-};
-template <>
-struct Chunk<2, IN_F32> {
-    using T = float4;
-    __device__ static float2 mix(T x) { return make_float2(x.x + x.y, x.z + x.w); }
-};
-template <>
-struct Chunk<1, IN_S16> {
-    using T = short2;
-    __device__ static float2 mix(T x) { return make_float2((float)x.x / 32768.0f, (float)x.y / 32768.0f); }
-};
-template <>
-struct Chunk<2, IN_S16> {
-    using T = short4;
-    __device__ static float2 mix(T x) {
-        return make_float2((float)x.x / 32768.0f + (float)x.y / 32768.0f,
-                           (float)x.z / 32768.0f + (float)x.w / 32768.0f);
-    }
-};
-
 // OK: 0 complex, 1 linear kinds, 2 mel kinds. C: 1 mono, 2 stereo (interleaved); INF: f32 / s16.
 // VAR (experiments, THESIA_STFT_VARIANT): bit0 = per-pair partner exchange instead of the
 // batched one (measured 0.07 ms slower); ablations (outputs wrong, timing only): bit1 = no mel
