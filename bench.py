@@ -51,6 +51,8 @@ def parse():
     p.add_argument("--n-mels", type=int, default=128)
     p.add_argument("--output", choices=["mel_db", "amp_db", "power_db", "complex"], default="mel_db")
     p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--no-rfft-roofline", action="store_true",
+                   help="skip the extra complex-output (window+rFFT kernel) roofline measurement")
     p.add_argument("--cpu-workers", type=int, default=16)
     p.add_argument("--variants", default="", help="experiment: comma list of THESIA_STFT_VARIANT "
                    "values to A/B (interleaved rounds, one process); prints per-variant kernel ms")
@@ -126,6 +128,28 @@ def cpu_baseline(args, n_samples):
     return {"value": frames / dt, "unit": "frames/s", "cores": workers, "kind": "port",
             "sample": f"{n_tracks} tracks x {args.seconds:g} s x {args.channels} ch @ {args.sr} Hz "
                       f"({frames} frames, {dt:.2f} s wall) through the C oracle, {workers} threads"}
+
+
+def rfft_roofline(args, din, offs, lens, fmt, n_local, n_samples):
+    """BASELINE.json north_star's "window+rFFT kernel" on the same resident input: the same
+    streaming kernel with complex-spectrum output ([T, F] complex64, perform_stft's result,
+    lib.rs:436-440), timed with HIP events on its launch stream; algorithmic bytes = input once
+    + F x 8 B per frame. Reported beside the headline roofline, never as `value`."""
+    plan = engine.Plan(args.n_fft, args.n_fft, args.hop, engine.OUT_COMPLEX, sr=args.sr)
+    frames = engine.Batch.frames_for(plan, lens)
+    dout = engine.DeviceBuffer(frames * plan.row_bins * 8)
+    b = engine.Batch(plan, din, offs, lens, dout, input_format=fmt, channels=args.channels)
+    b.run_timed(2)
+    kms = b.run_timed(5) / 5
+    in_el = 4 if args.input == "f32" else 2
+    abytes = n_local * n_samples * args.channels * in_el + frames * plan.row_bins * 8
+    achieved = abytes / (kms * 1e-3) / 1e9
+    b.close()
+    dout.close()
+    return {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": achieved / HBM_PEAK_GBS, "kernel_ms": kms, "algorithmic_bytes_per_launch": abytes,
+            "frames_per_s": frames / (kms * 1e-3),
+            "kernel": "thesia::stft3_kernel, complex output (downmix+frame+window+rFFT)"}
 
 
 def frames_all_ranks(pg, frames: int) -> int:
@@ -317,6 +341,8 @@ def main():
             "kernel_ms": kms,
             "algorithmic_bytes_per_launch": abytes,
         }
+        if kind != engine.OUT_COMPLEX and not args.no_rfft_roofline:
+            result["roofline_window_rfft"] = rfft_roofline(args, din, offs, lens, fmt, n_local, n_samples)
         if ws == 1 and not args.no_cpu_baseline:
             result["cpu_baseline"] = cpu_baseline(args, n_samples)
         print(json.dumps(result), flush=True)

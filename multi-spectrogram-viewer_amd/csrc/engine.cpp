@@ -159,6 +159,9 @@ static int build_mel4(Plan* p) {
                 len4 = std::max(len4, (h0 - lo[j] + 3) / 4);
             }
         }
+        // pad the round to whole 4-step batches (zero weights; mel4 issues a batch's LDS
+        // reads together), as long as the round still fits the F4-bin row
+        if ((len4 + 3) / 4 * 4 * 4 <= F4) len4 = (len4 + 3) / 4 * 4;
         rounds[r] = int2{(int)rows, (int)len4};
         wt.resize((rows + (size_t)len4) * L * 4, 0.0f);
         for (int j = 0; j < L; ++j) {

@@ -111,16 +111,28 @@ __device__ __forceinline__ bool load_direct2(const StftLaunch& a, int j, int64_t
 // On return v[c*L + ce_pos(L, k2)] = Z[k1 + P*k2] / 2 with k1 = j + c*L.
 // twf(k1c, x): applies the stage-1 twiddle W_NC^{j*k1} to x (k1c an integral_constant).
 template <int NC, class TwF>
-__device__ __forceinline__ void fft2(float2 (&v)[Geo2<NC>::P], float* region, int j, TwF&& twf) {
+__device__ __forceinline__ void fft2(float2 (&v)[Geo2<NC>::P], float* region, int j, const TwF& twf) {
     using G = Geo2<NC>;
     constexpr int L = G::L, P = G::P, S = G::S, CPL = G::CPL;
     pin(v);
     dif_fft<P, 1, 0, P>(v);
     pin(v);
-    static_for<1, P>([&](auto kc) {
-        constexpr int pk = ce_pos(P, decltype(kc)::value);
-        v[pk] = twf(kc, v[pk]);
-    });
+    if constexpr (TwF::kPairs) {
+        // two twiddles per ds_read_b128: all reads of the table issued before the products
+        float4 tw[P / 2];
+        static_for<0, P / 2>([&](auto qc) { tw[decltype(qc)::value] = twf.pair(decltype(qc)::value); });
+        static_for<1, P>([&](auto kc) {
+            constexpr int k1 = decltype(kc)::value;
+            constexpr int pk = ce_pos(P, k1);
+            const float4 t = tw[k1 / 2];
+            v[pk] = cmul(v[pk], (k1 & 1) ? make_float2(t.z, t.w) : make_float2(t.x, t.y));
+        });
+    } else {
+        static_for<1, P>([&](auto kc) {
+            constexpr int pk = ce_pos(P, decltype(kc)::value);
+            v[pk] = twf(kc, v[pk]);
+        });
+    }
 #pragma unroll
     for (int e = 0; e < 2; ++e) {
         wave_lds_sync();
@@ -167,6 +179,7 @@ __device__ __forceinline__ void load_tw2(const StftLaunch& a, int j, float2 (&tw
 // registers.
 template <int NC>
 struct TwBases {
+    static constexpr bool kPairs = false;
     float2 b[Geo2<NC>::TB], a[Geo2<NC>::TA];
     template <class K>
     __device__ __forceinline__ float2 operator()(K, float2 x) const {
@@ -181,12 +194,21 @@ struct TwBases {
 // Stage-1 twiddles as one product with W_NC^{j*k1} from a lane-major [P][L] table (LDS):
 // conflict-free ds_read_b64 (consecutive lanes, consecutive entries).
 struct TwTable {
+    static constexpr bool kPairs = false;
     const float2* row;  // table + j
     int L;
     template <class K>
     __device__ __forceinline__ float2 operator()(K, float2 x) const {
         return cmul(x, row[K::value * L]);
     }
+};
+// The same table with k1 pairs interleaved: [P/2][L] float4 {W^{j*2q}, W^{j*(2q+1)}}
+// (conflict-free ds_read_b128: consecutive lanes, consecutive 16-byte entries).
+struct TwTable4 {
+    static constexpr bool kPairs = true;
+    const float4* row;  // table + j
+    int L;
+    __device__ __forceinline__ float4 pair(int q) const { return row[q * L]; }
 };
 
 // realfft untangle on bin pairs; calls epi(k, re, im) for every bin this lane produces
@@ -283,19 +305,28 @@ __device__ __forceinline__ void mel4(const StftLaunch& a, const float* region, c
         const float4* wp = wt + (size_t)rd.x * L + j;
         float acc = 0.0f;
         int it = 0;
-        for (; it + U <= rd.y; it += U) {
-            float4 w[U], x[U];
+        // every LDS read of a batch is issued before its fma chain: one LDS round trip per
+        // batch (the host pads each round to a multiple of 4 steps with zero weights, so a
+        // round is U-batches plus at most one 4-batch; the 1-step loop is a safety net)
+        auto batch = [&](auto uc) {
+            constexpr int B = decltype(uc)::value;
+            float4 w[B], x[B];
 #pragma unroll
-            for (int u = 0; u < U; ++u) w[u] = wp[(it + u) * L];
+            for (int u = 0; u < B; ++u) w[u] = wp[(it + u) * L];
 #pragma unroll
-            for (int u = 0; u < U; ++u) x[u] = xp[it + u];
+            for (int u = 0; u < B; ++u) x[u] = xp[it + u];
 #pragma unroll
-            for (int u = 0; u < U; ++u) {
+            for (int u = 0; u < B; ++u) {
                 acc = __builtin_fmaf(x[u].x, w[u].x, acc);
                 acc = __builtin_fmaf(x[u].y, w[u].y, acc);
                 acc = __builtin_fmaf(x[u].z, w[u].z, acc);
                 acc = __builtin_fmaf(x[u].w, w[u].w, acc);
             }
+            it += B;
+        };
+        while (it + U <= rd.y) batch(std::integral_constant<int, U>{});
+        if constexpr (U > 4) {
+            if (it + 4 <= rd.y) batch(std::integral_constant<int, 4>{});
         }
         for (; it < rd.y; ++it) {
             const float4 w = wp[it * L], x = xp[it];
@@ -305,7 +336,7 @@ __device__ __forceinline__ void mel4(const StftLaunch& a, const float* region, c
             acc = __builtin_fmaf(x.w, w.w, acc);
         }
         const int m = r * L + j;
-        if (valid && m < n_mels) out[m] = db ? db_of(acc, a.log_amin, 1e-18f, 20.0f) : acc;
+        if (valid && m < n_mels) st_nt(out + m, db ? db_of(acc, a.log_amin, 1e-18f, 20.0f) : acc);
     }
 }
 

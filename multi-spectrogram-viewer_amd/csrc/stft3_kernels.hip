@@ -21,12 +21,15 @@
 
 namespace thesia {
 
-template <int NC>
+// WV waves per block, one block per CU: WV / 4 waves per SIMD (8: 2 waves/SIMD, 256 VGPRs;
+// 12: 3 waves/SIMD, 168 VGPRs).
+template <int NC, int WV = kWaves>
 struct Geo3 {
     using G2 = Geo2<NC>;
     static constexpr int L = G2::L, P = G2::P, FPW = G2::FPW, RS = G2::RS;
     static constexpr int SH = P / 4;                      // points per lane a hop moves
-    static constexpr int STREAMS = kWaves * FPW;          // streams (= frames in flight) per block
+    static constexpr int BLOCK = 64 * WV;
+    static constexpr int STREAMS = WV * FPW;              // streams (= frames in flight) per block
     static constexpr int TW_FLOATS = 2 * P * L;           // W_NC^{j*k1}, [P][L] float2
     // window per lane: row j holds (w[2m], w[2m+1]) for m = L*n1 + j, n1 < P, read as float4;
     // row stride 2P + 4 floats keeps 16 lanes of a ds_read_b128 group on distinct banks
@@ -68,12 +71,19 @@ __device__ __forceinline__ void load_raw_generic(const StftLaunch& a, float* reg
 // batched one (measured 0.07 ms slower); ablations (outputs wrong, timing only): bit1 = no mel
 // projection, bit2 = no FFT (stages and transposes skipped), bit3 = no untangle / |X| / mel;
 // bit4 = mel with 4 float4 steps per LDS round trip instead of 8.
-template <int NC, int OK, int C, int INF, int VAR = 0>
-__global__ void __launch_bounds__(kBlock, 2)
+#ifdef THESIA_MARKS
+#define MARK(x) asm volatile("; MARK " #x)
+#else
+#define MARK(x)
+#endif
+
+template <int NC, int OK, int C, int INF, int VAR = 0, int WV = kWaves>
+__global__ void __launch_bounds__(64 * WV, WV / 4)
 stft3_kernel(StftLaunch a, uint64_t fps) {
+    constexpr int kBlock = 64 * WV;
     constexpr bool kBatch = (VAR & 1) == 0;
     using G = Geo2<NC>;
-    using G3 = Geo3<NC>;
+    using G3 = Geo3<NC, WV>;
     using CK = Chunk<C, INF>;
     using CT = typename CK::T;
     using ET = typename std::conditional<INF == IN_S16, int16_t, float>::type;
@@ -101,14 +111,18 @@ stft3_kernel(StftLaunch a, uint64_t fps) {
         for (int i = threadIdx.x; i < a.mel4_rounds * L; i += kBlock) k0_lds[i] = a.mel4_k0[i];
         for (int i = threadIdx.x; i < a.mel4_rounds; i += kBlock) rd_lds[i] = a.mel4_round[i];
     }
-    for (int i = threadIdx.x; i < P * L; i += kBlock) twtab[i] = a.tw3[i];
+    // stage-1 twiddles with k1 pairs interleaved (TwTable4): [k1/2][j][k1&1]
+    for (int i = threadIdx.x; i < P * L; i += kBlock) {
+        const int k1 = i / L, jj = i % L;
+        twtab[((k1 >> 1) * L + jj) * 2 + (k1 & 1)] = a.tw3[i];
+    }
     float2 ub[G::CPL];
 #pragma unroll
     for (int c = 0; c < G::CPL; ++c) ub[c] = a.sincos[j + c * L];
     __syncthreads();
 
     const uint64_t total = a.total_frames;
-    const uint64_t stream = ((uint64_t)blockIdx.x * kWaves + wave) * FPW + slot;
+    const uint64_t stream = ((uint64_t)blockIdx.x * WV + wave) * FPW + slot;
     const uint64_t g0 = stream * fps;
     const uint64_t g1 = g0 + fps < total ? g0 + fps : total;
     const int hop = a.hop;
@@ -123,6 +137,7 @@ stft3_kernel(StftLaunch a, uint64_t fps) {
     uint64_t g_beg = 1, g_end = 0, base = 0;
     int64_t n = 0;
     for (uint64_t it = 0; it < fps; ++it) {  // wave-uniform trip count
+        MARK(top);
         const uint64_t g = g0 + it;
         const bool valid = g < g1;
         // opaque per frame: keeps the untangle rotations (from ub) and the window reads (from
@@ -167,6 +182,7 @@ stft3_kernel(StftLaunch a, uint64_t fps) {
 #pragma unroll
             for (int n1 = 0; n1 < P; ++n1) raw[n1] = make_float2(0.f, 0.f);
         }
+        MARK(loaded);
         // window (lib.rs:379, with the 1/2 of realfft.rs:148-154 folded in)
         float2 v[P];
         static_for<0, P / 2>([&](auto qc) {
@@ -188,8 +204,10 @@ stft3_kernel(StftLaunch a, uint64_t fps) {
             }
             pre_ok = nxt;
         }
-        if constexpr ((VAR & 4) == 0) fft2<NC>(v, region, j, TwTable{twtab + wj, L});
+        MARK(prefetched);
+        if constexpr ((VAR & 4) == 0) fft2<NC>(v, region, j, TwTable4{reinterpret_cast<const float4*>(twtab) + wj, L});
         else pin(v);
+        MARK(fft);
         if constexpr (OK == 2 && (VAR & 8) != 0) {  // ablation: no untangle / |X| / mel
             pin(v);
         } else if constexpr (OK == 2) {
@@ -201,12 +219,13 @@ stft3_kernel(StftLaunch a, uint64_t fps) {
                 for (int k = F; k < G::F4; ++k) region[k] = 0.0f;
             }
             wave_lds_sync();
+            MARK(untangled);
             // U = 8 float4 steps per LDS round trip (the FFT's registers are free by now)
             if constexpr ((VAR & 2) == 0) mel4<NC, (VAR & 16) ? 4 : 8>(a, region, mel_lds, rd_lds, k0_lds, j, g, valid);
         } else if constexpr (OK == 0) {
             float2* crow = reinterpret_cast<float2*>(a.out) + g * F;
             untangle2<NC, kBatch>(v, j, partner, ub, [&](int k, float xr, float xi) {
-                if (valid) crow[k] = make_float2(xr, xi);
+                if (valid) st_nt(crow + k, make_float2(xr, xi));
             });
         } else {
             const int kind = a.out_kind;
@@ -223,7 +242,7 @@ stft3_kernel(StftLaunch a, uint64_t fps) {
                     float val = region[k];
                     if (db) val = power ? db_of(val, a.log_amin, 1e-36f, 10.0f)
                                         : db_of(val, a.log_amin, 1e-18f, 20.0f);
-                    frow[k] = val;
+                    st_nt(frow + k, val);
                 }
             }
         }
@@ -233,16 +252,16 @@ stft3_kernel(StftLaunch a, uint64_t fps) {
 // --------------------------------------------------------------------------------------
 // host-side dispatch
 // --------------------------------------------------------------------------------------
-template <int NC>
+template <int NC, int WV = kWaves>
 static int lds3_bytes(const StftLaunch& a, bool mel) {
-    return (Geo3<NC>::BASE_FLOATS +
+    return (Geo3<NC, WV>::BASE_FLOATS +
             (mel ? (a.mel4_rows * 4 + a.mel4_rounds) * Geo2<NC>::L + 2 * a.mel4_rounds : 0)) * 4;
 }
 
-template <int NC, int OK, int C, int INF, int VAR = 0>
+template <int NC, int OK, int C, int INF, int VAR = 0, int WV = kWaves>
 static int launch3_k(const StftLaunch& a, hipStream_t stream) {
 #ifdef THESIA_EXPERIMENTS
-    if constexpr (VAR == 0 && NC == 1024 && OK == 2 && C == 2 && INF == IN_F32) {
+    if constexpr (VAR == 0 && WV == kWaves && NC == 1024 && OK == 2 && C == 2 && INF == IN_F32) {
         const char* e = getenv("THESIA_STFT_VARIANT");
         switch (e ? atoi(e) : 0) {
             case 1: return launch3_k<NC, OK, C, INF, 1>(a, stream);
@@ -252,18 +271,20 @@ static int launch3_k(const StftLaunch& a, hipStream_t stream) {
             case 8: return launch3_k<NC, OK, C, INF, 8>(a, stream);
             case 12: return launch3_k<NC, OK, C, INF, 12>(a, stream);
             case 16: return launch3_k<NC, OK, C, INF, 16>(a, stream);
+            case 1000: return launch3_k<NC, OK, C, INF, 0, 12>(a, stream);  // 3 waves/SIMD
             default: break;
         }
     }
 #endif
-    const int lds = lds3_bytes<NC>(a, OK == 2);
+    constexpr int kBlock = 64 * WV;
+    const int lds = lds3_bytes<NC, WV>(a, OK == 2);
     if (lds > 163840) return -2;
-    auto kern = stft3_kernel<NC, OK, C, INF, VAR>;
+    auto kern = stft3_kernel<NC, OK, C, INF, VAR, WV>;
     if (hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
                             hipFuncAttributeMaxDynamicSharedMemorySize, lds) != hipSuccess)
         return -1;
     if (a.total_frames == 0) return 0;
-    constexpr uint64_t per_block = Geo3<NC>::STREAMS;
+    constexpr uint64_t per_block = Geo3<NC, WV>::STREAMS;
     int grid = grid_for(reinterpret_cast<const void*>(kern), kBlock, lds,
                         (a.total_frames + per_block - 1) / per_block, a.grid);
     const uint64_t streams = (uint64_t)grid * per_block;

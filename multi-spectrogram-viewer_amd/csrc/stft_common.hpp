@@ -100,9 +100,19 @@ __device__ __forceinline__ int find_track(const uint64_t* f0, int n_tracks, uint
 }
 
 __device__ __forceinline__ float db_of(float x, float log_amin, float amin, float factor) {
-    // decibel.rs:49-55 with ref = 1 (log_ref = 0) then the separate *factor pass (:65/:75)
-    float l = x > amin ? log10f(x) : log_amin;
+    // decibel.rs:49-55 with ref = 1 (log_ref = 0) then the separate *factor pass (:65/:75).
+    // log10(x) = log2(x) * log10(2) with the hardware v_log_f32: x > amin >= 1e-36 is a
+    // normal float, so no denormal pre-scaling is needed; within a few ulp of glibc log10f
+    // (the reference's f32::log10), i.e. <= 1e-4 dB, far inside tests/tolerances.py.
+    float l = x > amin ? __builtin_amdgcn_logf(x) * 0.30102999566398119521f : log_amin;
     return factor * (l - 0.0f);
+}
+
+// Output rows are written once and never re-read by the kernel: non-temporal stores.
+__device__ __forceinline__ void st_nt(float* p, float v) { __builtin_nontemporal_store(v, p); }
+__device__ __forceinline__ void st_nt(float2* p, float2 v) {
+    typedef float v2 __attribute__((ext_vector_type(2)));
+    __builtin_nontemporal_store(v2{v.x, v.y}, reinterpret_cast<v2*>(p));
 }
 
 // |X| = hypot(re, im): v_sqrt_f32 of the f32 sum of squares (<= 1.5 ulp; the product kernel
