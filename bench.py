@@ -108,7 +108,7 @@ def cpu_baseline(args, n_samples):
     from concurrent.futures import ThreadPoolExecutor
 
     workers = max(1, min(args.cpu_workers, os.cpu_count() or 1))
-    n_tracks = 2 * workers
+    n_tracks = 3 * workers  # ~10-15 s of CPU work on 16 threads
     fb = O.calc_mel_fb(args.sr, args.n_fft, args.n_mels)
     pcm = [engine.synth_pcm_host(args.channels, i, n_samples, args.sr).astype(np.float32) / 32768.0
            for i in range(n_tracks)]

@@ -16,7 +16,7 @@ if [ "${SKIP_KT:-0}" != 1 ]; then
   timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof_kt" -o kt --output-format csv -- python3 "$REPO/bench.py" $BARGS > "$OUT/prof_kt.log" 2>&1
   rc=$?; echo "kt rc=$rc"; crash $rc && exit $rc
 fi
-PB=${PMC_BENCH_ARGS:---steps 3 --warmup 1 --no-cpu-baseline}
+PB=${PMC_BENCH_ARGS:---steps 3 --warmup 1 --no-cpu-baseline --no-rfft-roofline}
 SETS=${PMC_SETS:-"FETCH_SIZE;WRITE_SIZE;SQ_WAVES SQ_INSTS_VALU SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU"}
 IFS=';' read -ra sets <<< "$SETS"
 for c in "${sets[@]}"; do
