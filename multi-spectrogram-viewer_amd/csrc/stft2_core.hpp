@@ -336,7 +336,7 @@ __device__ __forceinline__ void mel4(const StftLaunch& a, const float* region, c
             acc = __builtin_fmaf(x.w, w.w, acc);
         }
         const int m = r * L + j;
-        if (valid && m < n_mels) st_nt(out + m, db ? db_of(acc, a.log_amin, 1e-18f, 20.0f) : acc);
+        if (valid && m < n_mels) st_out(out + m, db ? db_of(acc, a.log_amin, 1e-18f, 20.0f) : acc);
     }
 }
 

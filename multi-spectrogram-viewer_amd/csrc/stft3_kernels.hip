@@ -225,7 +225,7 @@ stft3_kernel(StftLaunch a, uint64_t fps) {
         } else if constexpr (OK == 0) {
             float2* crow = reinterpret_cast<float2*>(a.out) + g * F;
             untangle2<NC, kBatch>(v, j, partner, ub, [&](int k, float xr, float xi) {
-                if (valid) st_nt(crow + k, make_float2(xr, xi));
+                if (valid) st_out(crow + k, make_float2(xr, xi));
             });
         } else {
             const int kind = a.out_kind;
@@ -242,7 +242,7 @@ stft3_kernel(StftLaunch a, uint64_t fps) {
                     float val = region[k];
                     if (db) val = power ? db_of(val, a.log_amin, 1e-36f, 10.0f)
                                         : db_of(val, a.log_amin, 1e-18f, 20.0f);
-                    st_nt(frow + k, val);
+                    st_out(frow + k, val);
                 }
             }
         }

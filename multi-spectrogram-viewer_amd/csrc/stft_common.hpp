@@ -108,12 +108,18 @@ __device__ __forceinline__ float db_of(float x, float log_amin, float amin, floa
     return factor * (l - 0.0f);
 }
 
-// Output rows are written once and never re-read by the kernel: non-temporal stores.
-__device__ __forceinline__ void st_nt(float* p, float v) { __builtin_nontemporal_store(v, p); }
-__device__ __forceinline__ void st_nt(float2* p, float2 v) {
+// Output row stores. Plain stores: non-temporal ones (THESIA_NT_STORES, experiment) measured
+// slower and bimodal on the complex-output kernel (7.6 / 10.1 ms vs 6.24 ms).
+#ifdef THESIA_NT_STORES
+__device__ __forceinline__ void st_out(float* p, float v) { __builtin_nontemporal_store(v, p); }
+__device__ __forceinline__ void st_out(float2* p, float2 v) {
     typedef float v2 __attribute__((ext_vector_type(2)));
     __builtin_nontemporal_store(v2{v.x, v.y}, reinterpret_cast<v2*>(p));
 }
+#else
+__device__ __forceinline__ void st_out(float* p, float v) { *p = v; }
+__device__ __forceinline__ void st_out(float2* p, float2 v) { *p = v; }
+#endif
 
 // |X| = hypot(re, im): v_sqrt_f32 of the f32 sum of squares (<= 1.5 ulp; the product kernel
 // is parity-by-tolerance against glibc hypotf). VAR bit0 selects the correctly-rounded
