@@ -55,9 +55,10 @@ struct StftLaunch {
     const int2* mel_round = nullptr;  // [rounds] {first weight row, band length}
     const int* mel_k0 = nullptr;      // [rounds][L]
     const float* mel_wt = nullptr;    // [sum of band lengths][L]
-    // the same projection for stft2_kernel (4 bins per step): lane j runs float4 steps
-    // it < mel4_round[r].y from bin mel4_k0[r*L + j] (a multiple of 4), weights
-    // mel4_wt[(mel4_round[r].x + it) * L + j] (float4, zero outside the band)
+    // the same projection for stft2/stft3 (4 bins per step): lane j runs float4 steps
+    // it < mel4_round[r].y from bin k0 = mel4_k0[r*L + j] & 0xFFFF (a multiple of 4) for mel
+    // mel4_k0[r*L + j] >> 16 (0xFFFF: idle lane), weights mel4_wt[(mel4_round[r].x + it) * L + j]
+    // (float4, zero outside the band); engine.cpp build_mel4 places filters on lanes bank-aware
     int mel4_rounds = 0;
     int mel4_rows = 0;  // float4 rows of mel4_wt (x L lanes)
     const int2* mel4_round = nullptr;

@@ -110,10 +110,18 @@ __device__ __forceinline__ bool load_direct2(const StftLaunch& a, int j, int64_t
 // Stage-1 DFT_P + twiddles W_NC^{j k1}, LDS transpose (re then im), stage-2 DFT_L, in place.
 // On return v[c*L + ce_pos(L, k2)] = Z[k1 + P*k2] / 2 with k1 = j + c*L.
 // twf(k1c, x): applies the stage-1 twiddle W_NC^{j*k1} to x (k1c an integral_constant).
-template <int NC, class TwF>
+// WIDE: transpose rows of stride L + 4 floats read back as ds_read_b128 (4 LDS cycles per KiB,
+// conflict-free for L = 32: the 16-lane groups of a b128 read start on 16 distinct 4-bank
+// slots) instead of stride L + 2 read as float2 pairs, which the compiler merges into
+// ds_read2_b64 (8 cycles per KiB; MI355X_MICROARCH.md LDS table). Regions must then hold
+// P * (L + 4) floats and be 16-byte aligned.
+template <int NC>
+constexpr int fft2_stride(bool wide) { return Geo2<NC>::L + (wide ? 4 : 2); }
+
+template <int NC, class TwF, bool WIDE = false>
 __device__ __forceinline__ void fft2(float2 (&v)[Geo2<NC>::P], float* region, int j, const TwF& twf) {
     using G = Geo2<NC>;
-    constexpr int L = G::L, P = G::P, S = G::S, CPL = G::CPL;
+    constexpr int L = G::L, P = G::P, S = fft2_stride<NC>(WIDE), CPL = G::CPL;
     pin(v);
     dif_fft<P, 1, 0, P>(v);
     pin(v);
@@ -144,13 +152,29 @@ __device__ __forceinline__ void fft2(float2 (&v)[Geo2<NC>::P], float* region, in
         wave_lds_sync();
         static_for<0, CPL>([&](auto cc) {
             constexpr int c = decltype(cc)::value;
-            const float2* row = reinterpret_cast<const float2*>(region + (j + c * L) * S);
-            static_for<0, L / 2>([&](auto qc) {
-                constexpr int q = 2 * decltype(qc)::value;
-                const float2 t = row[q / 2];
-                if (e == 0) { v[c * L + q].x = t.x; v[c * L + q + 1].x = t.y; }
-                else        { v[c * L + q].y = t.x; v[c * L + q + 1].y = t.y; }
-            });
+            if constexpr (WIDE) {
+                const float4* row = static_cast<const float4*>(
+                    __builtin_assume_aligned(region + (j + c * L) * S, 16));
+                static_for<0, L / 4>([&](auto qc) {
+                    constexpr int q = 4 * decltype(qc)::value;
+                    const float4 t = row[q / 4];
+                    if (e == 0) {
+                        v[c * L + q].x = t.x; v[c * L + q + 1].x = t.y;
+                        v[c * L + q + 2].x = t.z; v[c * L + q + 3].x = t.w;
+                    } else {
+                        v[c * L + q].y = t.x; v[c * L + q + 1].y = t.y;
+                        v[c * L + q + 2].y = t.z; v[c * L + q + 3].y = t.w;
+                    }
+                });
+            } else {
+                const float2* row = reinterpret_cast<const float2*>(region + (j + c * L) * S);
+                static_for<0, L / 2>([&](auto qc) {
+                    constexpr int q = 2 * decltype(qc)::value;
+                    const float2 t = row[q / 2];
+                    if (e == 0) { v[c * L + q].x = t.x; v[c * L + q + 1].x = t.y; }
+                    else        { v[c * L + q].y = t.x; v[c * L + q + 1].y = t.y; }
+                });
+            }
         });
     }
     wave_lds_sync();
@@ -301,7 +325,8 @@ __device__ __forceinline__ void mel4(const StftLaunch& a, const float* region, c
     float* out = static_cast<float*>(a.out) + g * (uint64_t)n_mels;
     for (int r = 0; r < a.mel4_rounds; ++r) {
         const int2 rd = rounds[r];  // {first float4 row, float4 steps}: wave-uniform
-        const float4* xp = reinterpret_cast<const float4*>(region + k0[r * L + j]);
+        const int k0m = k0[r * L + j];  // start bin | mel index << 16 (engine.cpp build_mel4)
+        const float4* xp = reinterpret_cast<const float4*>(region + (k0m & 0xFFFF));
         const float4* wp = wt + (size_t)rd.x * L + j;
         float acc = 0.0f;
         int it = 0;
@@ -335,7 +360,7 @@ __device__ __forceinline__ void mel4(const StftLaunch& a, const float* region, c
             acc = __builtin_fmaf(x.z, w.z, acc);
             acc = __builtin_fmaf(x.w, w.w, acc);
         }
-        const int m = r * L + j;
+        const int m = (int)((unsigned)k0m >> 16);
         if (valid && m < n_mels) st_out(out + m, db ? db_of(acc, a.log_amin, 1e-18f, 20.0f) : acc);
     }
 }

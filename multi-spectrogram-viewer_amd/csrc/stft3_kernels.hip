@@ -26,7 +26,10 @@ namespace thesia {
 template <int NC, int WV = kWaves>
 struct Geo3 {
     using G2 = Geo2<NC>;
-    static constexpr int L = G2::L, P = G2::P, FPW = G2::FPW, RS = G2::RS;
+    static constexpr int L = G2::L, P = G2::P, FPW = G2::FPW;
+    // the wide (ds_read_b128) transpose for the headline size, L = 32 (fft2 WIDE)
+    static constexpr bool WIDE = L == 32;
+    static constexpr int RS = WIDE ? (P * fft2_stride<NC>(true) + 3) / 4 * 4 : G2::RS;
     static constexpr int SH = P / 4;                      // points per lane a hop moves
     static constexpr int BLOCK = 64 * WV;
     static constexpr int STREAMS = WV * FPW;              // streams (= frames in flight) per block
@@ -70,7 +73,8 @@ __device__ __forceinline__ void load_raw_generic(const StftLaunch& a, float* reg
 // VAR (experiments, THESIA_STFT_VARIANT): bit0 = per-pair partner exchange instead of the
 // batched one (measured 0.07 ms slower); ablations (outputs wrong, timing only): bit1 = no mel
 // projection, bit2 = no FFT (stages and transposes skipped), bit3 = no untangle / |X| / mel;
-// bit4 = mel with 4 float4 steps per LDS round trip instead of 8.
+// bit4 = mel with 4 float4 steps per LDS round trip instead of 8; bit5 = the narrow (stride
+// L + 2, ds_read2_b64) transpose instead of the wide one.
 #ifdef THESIA_MARKS
 #define MARK(x) asm volatile("; MARK " #x)
 #else
@@ -126,7 +130,7 @@ stft3_kernel(StftLaunch a, uint64_t fps) {
     const uint64_t g0 = stream * fps;
     const uint64_t g1 = g0 + fps < total ? g0 + fps : total;
     const int hop = a.hop;
-    float* region = work + (wave * FPW + slot) * G::RS;
+    float* region = work + (wave * FPW + slot) * G3::RS;
     const ET* in = static_cast<const ET*>(a.in);
 
     float2 raw[P];
@@ -205,7 +209,7 @@ stft3_kernel(StftLaunch a, uint64_t fps) {
             pre_ok = nxt;
         }
         MARK(prefetched);
-        if constexpr ((VAR & 4) == 0) fft2<NC>(v, region, j, TwTable4{reinterpret_cast<const float4*>(twtab) + wj, L});
+        if constexpr ((VAR & 4) == 0) fft2<NC, TwTable4, G3::WIDE && (VAR & 32) == 0>(v, region, j, TwTable4{reinterpret_cast<const float4*>(twtab) + wj, L});
         else pin(v);
         MARK(fft);
         if constexpr (OK == 2 && (VAR & 8) != 0) {  // ablation: no untangle / |X| / mel
@@ -271,6 +275,7 @@ static int launch3_k(const StftLaunch& a, hipStream_t stream) {
             case 8: return launch3_k<NC, OK, C, INF, 8>(a, stream);
             case 12: return launch3_k<NC, OK, C, INF, 12>(a, stream);
             case 16: return launch3_k<NC, OK, C, INF, 16>(a, stream);
+            case 32: return launch3_k<NC, OK, C, INF, 32>(a, stream);  // narrow transpose
             case 1000: return launch3_k<NC, OK, C, INF, 0, 12>(a, stream);  // 3 waves/SIMD
             default: break;
         }
