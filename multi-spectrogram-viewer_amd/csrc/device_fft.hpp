@@ -141,6 +141,11 @@ __device__ __forceinline__ void pin_rec(float2 (&v)[N]) {
 // move arithmetic across it. Used between FFT stages to bound live ranges.
 template <int N>
 __device__ __forceinline__ void pin(float2 (&v)[N]) { pin_rec<0, N>(v); }
+template <int N>
+__device__ __forceinline__ void pin_f(float (&v)[N]) {
+#pragma unroll
+    for (int i = 0; i < N; ++i) asm volatile("" : "+v"(v[i]));
+}
 template <int B, int E, int N>
 __device__ __forceinline__ void pin_range(float2 (&v)[N]) {
     if constexpr (B < E) {

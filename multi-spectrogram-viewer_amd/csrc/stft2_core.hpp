@@ -235,6 +235,17 @@ struct TwTable4 {
     __device__ __forceinline__ float4 pair(int q) const { return row[q * L]; }
 };
 
+// Calls epi(k, re, im, slot) when the epilogue takes the bin's compile-time slot (2i: bin
+// k = j + c*L + P*t with i = c*(L/2) + t, 2i + 1: bin NC - k, 2*CPL*(L/2): lane 0's NC/2),
+// else epi(k, re, im).
+template <int S, class Epi>
+__device__ __forceinline__ void call_epi(Epi& epi, int k, float re, float im) {
+    if constexpr (std::is_invocable_v<Epi&, int, float, float, std::integral_constant<int, S>>)
+        epi(k, re, im, std::integral_constant<int, S>{});
+    else
+        epi(k, re, im);
+}
+
 // realfft untangle on bin pairs; calls epi(k, re, im) for every bin this lane produces
 // (k = j + c*L + P*t and NC - k for t < L/2; lane 0 also the self-paired bin NC/2).
 template <int NC, bool BATCH = false, class Epi>
@@ -243,13 +254,15 @@ __device__ __forceinline__ void untangle2(const float2 (&v)[Geo2<NC>::P], int j,
     using G = Geo2<NC>;
     constexpr int L = G::L, P = G::P, CPL = G::CPL;
     const bool lane0 = j == 0;
-    auto pair = [&](float2 b, float2 r, float s, float co, int k, bool both) {
+    auto pair = [&](float2 b, float2 r, float s, float co, int k, auto slotc) {
+        constexpr int slot = decltype(slotc)::value;
+        constexpr bool both = slot < 2 * CPL * (L / 2);
         const float ar = b.x + r.x, ai = b.y - r.y;  // A = Z_k + conj Z_{NC-k}
         const float br = b.x - r.x, bi = b.y + r.y;  // B = Z_k - conj Z_{NC-k}
         const float p = __builtin_fmaf(co, br, s * bi);     // (p, q) = (co - i s) B
         const float q = __builtin_fmaf(co, bi, -(s * br));
-        epi(k, ar + q, ai - p);
-        if (both) epi(NC - k, ar - q, -ai - p);
+        call_epi<slot>(epi, k, ar + q, ai - p);
+        if constexpr (both) call_epi<slot + 1>(epi, NC - k, ar - q, -ai - p);
     };
     // BATCH: every partner value is requested before the first pair is formed (one LDS
     // latency per frame instead of one per pair; costs CPL*L registers)
@@ -264,6 +277,9 @@ __device__ __forceinline__ void untangle2(const float2 (&v)[Geo2<NC>::P], int j,
                 recv[c * (L / 2) + t].y = __shfl(v[ps].y, partner, 64);
             });
         });
+        // keep the batch a batch: without this the scheduler sinks each ds_bpermute next to
+        // its use and the untangle becomes CPL*L/4 dependent LDS round trips
+        pin(recv);
     }
     static_for<0, CPL>([&](auto cc) {
         constexpr int c = decltype(cc)::value;
@@ -298,7 +314,7 @@ __device__ __forceinline__ void untangle2(const float2 (&v)[Geo2<NC>::P], int j,
                 s = __builtin_fmaf(ub[c].x, cb, ub[c].y * sb);
                 co = __builtin_fmaf(ub[c].y, cb, -(ub[c].x * sb));
             }
-            pair(b, r, s, co, j + c * L + P * t, true);
+            pair(b, r, s, co, j + c * L + P * t, std::integral_constant<int, 2 * (c * (L / 2) + t)>{});
         });
     });
     if (lane0) {  // k = NC/2 pairs with itself: (sin, cos)(pi/2) from the base sin_cos[0]
@@ -308,15 +324,92 @@ __device__ __forceinline__ void untangle2(const float2 (&v)[Geo2<NC>::P], int j,
         constexpr float sb = -ce_tw_im(L / 2, 2 * L);
         const float s = __builtin_fmaf(ub[0].x, cb, ub[0].y * sb);
         const float co = __builtin_fmaf(ub[0].y, cb, -(ub[0].x * sb));
-        pair(b, b, s, co, NC / 2, false);
+        pair(b, b, s, co, NC / 2, std::integral_constant<int, 2 * CPL * (L / 2)>{});
     }
 }
 
 // lib.rs:131-132 on the |X| row in `region`: round r gives lane j mel r*L + j.
 // wt / rounds / k0: the float4 weight rows, the per-round {row, steps} and the per-lane start
 // bins (a.mel4_* in HBM, or their copies in LDS).
-template <int NC, int U = 4>
+template <int NC, int U = 4, int NACC = 1>
 __device__ __forceinline__ void mel4(const StftLaunch& a, const float* region, const float4* wt,
+                                     const int2* rounds, const int* k0, int j, uint64_t g,
+                                     bool valid) {
+    constexpr int L = Geo2<NC>::L;
+    constexpr int PR = 4;  // rounds whose {row, steps} and start bins are fetched up front
+    const int n_mels = a.n_mels;
+    const int R = a.mel4_rounds;
+    const bool db = a.out_kind == OUT_MEL_AMP_DB;
+    float* out = static_cast<float*>(a.out) + g * (uint64_t)n_mels;
+    auto round = [&](int2 rd, int k0m) {
+        // {first float4 row, float4 steps} are wave-uniform: scalar loop control
+        rd.x = __builtin_amdgcn_readfirstlane(rd.x);
+        rd.y = __builtin_amdgcn_readfirstlane(rd.y);
+        const float4* xp = reinterpret_cast<const float4*>(region + (k0m & 0xFFFF));
+        const float4* wp = wt + (size_t)rd.x * L + j;
+        // NACC = 4: one accumulator per float4 component (four independent fma chains, summed
+        // (a0 + a1) + (a2 + a3) at the end) instead of one k-ascending chain: a quarter of the
+        // dependent-fma latency; reassociation within fp32 rounding (tolerance parity)
+        float acc = 0.0f, a1 = 0.0f, a2 = 0.0f, a3 = 0.0f;
+        int it = 0;
+        // every LDS read of a batch is issued before its fma chain: one LDS round trip per
+        // batch (the host pads each round to a multiple of 4 steps with zero weights, so a
+        // round is U-batches plus at most one 4-batch; the 1-step loop is a safety net)
+        auto batch = [&](auto uc) {
+            constexpr int B = decltype(uc)::value;
+            float4 w[B], x[B];
+#pragma unroll
+            for (int u = 0; u < B; ++u) w[u] = wp[(it + u) * L];
+#pragma unroll
+            for (int u = 0; u < B; ++u) x[u] = xp[it + u];
+#pragma unroll
+            for (int u = 0; u < B; ++u) {
+                if constexpr (NACC == 4) {
+                    acc = __builtin_fmaf(x[u].x, w[u].x, acc);
+                    a1 = __builtin_fmaf(x[u].y, w[u].y, a1);
+                    a2 = __builtin_fmaf(x[u].z, w[u].z, a2);
+                    a3 = __builtin_fmaf(x[u].w, w[u].w, a3);
+                } else {
+                    acc = __builtin_fmaf(x[u].x, w[u].x, acc);
+                    acc = __builtin_fmaf(x[u].y, w[u].y, acc);
+                    acc = __builtin_fmaf(x[u].z, w[u].z, acc);
+                    acc = __builtin_fmaf(x[u].w, w[u].w, acc);
+                }
+            }
+            it += B;
+        };
+        while (it + U <= rd.y) batch(std::integral_constant<int, U>{});
+        if constexpr (U > 4) {
+            if (it + 4 <= rd.y) batch(std::integral_constant<int, 4>{});
+        }
+        for (; it < rd.y; ++it) {
+            const float4 w = wp[it * L], x = xp[it];
+            acc = __builtin_fmaf(x.x, w.x, acc);
+            acc = __builtin_fmaf(x.y, w.y, acc);
+            acc = __builtin_fmaf(x.z, w.z, acc);
+            acc = __builtin_fmaf(x.w, w.w, acc);
+        }
+        if constexpr (NACC == 4) acc = (acc + a1) + (a2 + a3);
+        const int m = (int)((unsigned)k0m >> 16);  // start bin | mel << 16 (build_mel4)
+        if (valid && m < n_mels) st_out(out + m, db ? db_of(acc, a.log_amin, 1e-18f, 20.0f) : acc);
+    };
+    // the first PR rounds' setup in one LDS round trip (not one dependent read per round)
+    int2 rdp[PR];
+    int k0p[PR];
+#pragma unroll
+    for (int r = 0; r < PR; ++r) {
+        rdp[r] = r < R ? rounds[r] : int2{0, 0};
+        k0p[r] = r < R ? k0[r * L + j] : 0;
+    }
+#pragma unroll
+    for (int r = 0; r < PR; ++r)
+        if (r < R) round(rdp[r], k0p[r]);
+    for (int r = PR; r < R; ++r) round(rounds[r], k0[r * L + j]);
+}
+
+// previous mel4 (per-round dependent setup reads), kept for in-process A/B (stft3 VAR bit6)
+template <int NC, int U = 4>
+__device__ __forceinline__ void mel4_v1(const StftLaunch& a, const float* region, const float4* wt,
                                      const int2* rounds, const int* k0, int j, uint64_t g,
                                      bool valid) {
     constexpr int L = Geo2<NC>::L;

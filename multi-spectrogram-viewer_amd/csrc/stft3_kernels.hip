@@ -74,7 +74,9 @@ __device__ __forceinline__ void load_raw_generic(const StftLaunch& a, float* reg
 // batched one (measured 0.07 ms slower); ablations (outputs wrong, timing only): bit1 = no mel
 // projection, bit2 = no FFT (stages and transposes skipped), bit3 = no untangle / |X| / mel;
 // bit4 = mel with 4 float4 steps per LDS round trip instead of 8; bit5 = the narrow (stride
-// L + 2, ds_read2_b64) transpose instead of the wide one.
+// L + 2, ds_read2_b64) transpose instead of the wide one; bit6 = the previous mel4 (per-round
+// setup reads); bit7 = four mel accumulators; bit8 = ablation: |X|^2 (no v_sqrt); bit9 = the
+// sqrts not batched.
 #ifdef THESIA_MARKS
 #define MARK(x) asm volatile("; MARK " #x)
 #else
@@ -215,9 +217,32 @@ stft3_kernel(StftLaunch a, uint64_t fps) {
         if constexpr (OK == 2 && (VAR & 8) != 0) {  // ablation: no untangle / |X| / mel
             pin(v);
         } else if constexpr (OK == 2) {
-            untangle2<NC, kBatch>(v, j, partner, ub, [&](int k, float xr, float xi) {
-                region[k] = __builtin_amdgcn_sqrtf(__builtin_fmaf(xr, xr, xi * xi));  // |X| (lib.rs:124)
+            // |X| (lib.rs:124) in three batches: every |X|^2 of the lane, then every v_sqrt (a
+            // transcendental whose result used right away stalls the wave: 0.34 ms per launch
+            // measured), then the LDS row writes
+            constexpr int NS = 2 * G::CPL * (L / 2) + 1;
+            float mag[NS];
+            mag[NS - 1] = 0.0f;
+            untangle2<NC, kBatch>(v, j, partner, ub, [&](int, float xr, float xi, auto sc) {
+                mag[decltype(sc)::value] = __builtin_fmaf(xr, xr, xi * xi);
             });
+            if constexpr ((VAR & 512) == 0) {
+                pin_f(mag);
+#pragma unroll
+                for (int i = 0; i < NS; ++i)
+                    if constexpr ((VAR & 256) == 0) mag[i] = __builtin_amdgcn_sqrtf(mag[i]);
+                pin_f(mag);
+            } else {
+#pragma unroll
+                for (int i = 0; i < NS; ++i) mag[i] = __builtin_amdgcn_sqrtf(mag[i]);
+            }
+            static_for<0, G::CPL * (L / 2)>([&](auto ic) {
+                constexpr int i = decltype(ic)::value, c = i / (L / 2), t = i % (L / 2);
+                const int k = j + c * L + P * t;
+                region[k] = mag[2 * i];
+                region[NC - k] = mag[2 * i + 1];
+            });
+            if (j == 0) region[NC / 2] = mag[NS - 1];
             if (j == 0) {
 #pragma unroll
                 for (int k = F; k < G::F4; ++k) region[k] = 0.0f;
@@ -225,7 +250,9 @@ stft3_kernel(StftLaunch a, uint64_t fps) {
             wave_lds_sync();
             MARK(untangled);
             // U = 8 float4 steps per LDS round trip (the FFT's registers are free by now)
-            if constexpr ((VAR & 2) == 0) mel4<NC, (VAR & 16) ? 4 : 8>(a, region, mel_lds, rd_lds, k0_lds, j, g, valid);
+            if constexpr ((VAR & 2) == 0 && (VAR & 64) == 0)
+                mel4<NC, (VAR & 16) ? 4 : 8, (VAR & 128) ? 4 : 1>(a, region, mel_lds, rd_lds, k0_lds, j, g, valid);
+            if constexpr ((VAR & 64) != 0) mel4_v1<NC, 8>(a, region, mel_lds, rd_lds, k0_lds, j, g, valid);
         } else if constexpr (OK == 0) {
             float2* crow = reinterpret_cast<float2*>(a.out) + g * F;
             untangle2<NC, kBatch>(v, j, partner, ub, [&](int k, float xr, float xi) {
@@ -276,6 +303,11 @@ static int launch3_k(const StftLaunch& a, hipStream_t stream) {
             case 12: return launch3_k<NC, OK, C, INF, 12>(a, stream);
             case 16: return launch3_k<NC, OK, C, INF, 16>(a, stream);
             case 32: return launch3_k<NC, OK, C, INF, 32>(a, stream);  // narrow transpose
+            case 64: return launch3_k<NC, OK, C, INF, 64>(a, stream);  // previous mel4
+            case 128: return launch3_k<NC, OK, C, INF, 128>(a, stream);  // 4 mel accumulators
+            case 256: return launch3_k<NC, OK, C, INF, 256>(a, stream);  // ablation: no sqrt
+            case 512: return launch3_k<NC, OK, C, INF, 512>(a, stream);  // unbatched sqrt
+            case 258: return launch3_k<NC, OK, C, INF, 258>(a, stream);  // ablation: no sqrt, no mel
             case 1000: return launch3_k<NC, OK, C, INF, 0, 12>(a, stream);  // 3 waves/SIMD
             default: break;
         }
