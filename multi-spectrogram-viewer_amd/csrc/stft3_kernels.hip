@@ -39,8 +39,44 @@ struct Geo3 {
     static constexpr int WL_STRIDE = 2 * P + 4;
     static constexpr int WL_FLOATS = L * WL_STRIDE;
     static constexpr int BASE_FLOATS = WL_FLOATS + TW_FLOATS + STREAMS * RS;
+    // linear / complex kinds stage the whole output row in the stream's region (plus up to 3
+    // floats of alignment shift) so it leaves as 16-byte aligned stores
+    static constexpr int ROW_FLOATS_OK(int ok) { return ok == 0 ? 2 * G2::F : G2::F; }
+    static constexpr int RS_OK(bool staged, int ok) {
+        return !staged ? RS : (RS > (ROW_FLOATS_OK(ok) + 3 + 3) / 4 * 4 ? RS : (ROW_FLOATS_OK(ok) + 3 + 3) / 4 * 4);
+    }
+    static constexpr int BASE_FLOATS_OK(bool staged, int ok) { return WL_FLOATS + TW_FLOATS + STREAMS * RS_OK(staged, ok); }
     static_assert(P % 4 == 0, "hop = n_fft/4 must move whole points per lane");
 };
+
+// Which kinds stage their output row (measured): linear kinds yes (power dB 6.25
+// vs 6.58 ms), complex no (7.50 vs 7.41 ms; HBM write traffic equals the algorithmic bytes
+// either way). VAR bit10 flips the choice.
+constexpr bool stage_rows(int ok, int var) {
+    return ok == 1 ? (var & 1024) == 0 : ok == 0 ? (var & 1024) != 0 : false;
+}
+
+// A row of nfl floats staged in LDS (row element e at stage[sh + e], sh = the row's global
+// float offset mod 4) written with 16-byte aligned stores: whole float4 chunks from the L lanes
+// of the frame, the row's partial first/last chunk float by float. Rows of 1025 floats
+// (linear kinds) or 1025 float2 (complex) are not 16-byte aligned, so lane-wise 4- or 8-byte
+// stores of them leave partial 64-byte segments that HBM writes back twice.
+template <int L>
+__device__ __forceinline__ void store_row_b128(float* row, int sh, const float* stage, int nfl, int j) {
+    float* ab = row - sh;  // 16-byte aligned
+    const int nch = (sh + nfl + 3) >> 2;
+    for (int i = j; i < nch; i += L) {
+        const int e0 = 4 * i;
+        if (e0 >= sh && e0 + 4 <= sh + nfl) {
+            const float4 v = *reinterpret_cast<const float4*>(__builtin_assume_aligned(stage + e0, 16));
+            *reinterpret_cast<float4*>(__builtin_assume_aligned(ab + e0, 16)) = v;
+        } else {
+#pragma unroll
+            for (int e = 0; e < 4; ++e)
+                if (e0 + e >= sh && e0 + e < sh + nfl) ab[e0 + e] = stage[e0 + e];
+        }
+    }
+}
 
 // Reflect-padded, downmixed samples of a frame (no window): the uniform rule of
 // load_frame_generic (stft_common.hpp) for win = n_fft.
@@ -76,7 +112,7 @@ __device__ __forceinline__ void load_raw_generic(const StftLaunch& a, float* reg
 // bit4 = mel with 4 float4 steps per LDS round trip instead of 8; bit5 = the narrow (stride
 // L + 2, ds_read2_b64) transpose instead of the wide one; bit6 = the previous mel4 (per-round
 // setup reads); bit7 = four mel accumulators; bit8 = ablation: |X|^2 (no v_sqrt); bit9 = the
-// sqrts not batched.
+// sqrts not batched; bit10 (linear / complex kinds) = the other row-store method (stage_rows).
 #ifdef THESIA_MARKS
 #define MARK(x) asm volatile("; MARK " #x)
 #else
@@ -132,7 +168,7 @@ stft3_kernel(StftLaunch a, uint64_t fps) {
     const uint64_t g0 = stream * fps;
     const uint64_t g1 = g0 + fps < total ? g0 + fps : total;
     const int hop = a.hop;
-    float* region = work + (wave * FPW + slot) * G3::RS;
+    float* region = work + (wave * FPW + slot) * G3::RS_OK(stage_rows(OK, VAR), OK);
     const ET* in = static_cast<const ET*>(a.in);
 
     float2 raw[P];
@@ -253,12 +289,37 @@ stft3_kernel(StftLaunch a, uint64_t fps) {
             if constexpr ((VAR & 2) == 0 && (VAR & 64) == 0)
                 mel4<NC, (VAR & 16) ? 4 : 8, (VAR & 128) ? 4 : 1>(a, region, mel_lds, rd_lds, k0_lds, j, g, valid);
             if constexpr ((VAR & 64) != 0) mel4_v1<NC, 8>(a, region, mel_lds, rd_lds, k0_lds, j, g, valid);
-        } else if constexpr (OK == 0) {
+        } else if constexpr (OK == 0 && !stage_rows(OK, VAR)) {  // lane-wise 8-byte stores
             float2* crow = reinterpret_cast<float2*>(a.out) + g * F;
             untangle2<NC, kBatch>(v, j, partner, ub, [&](int k, float xr, float xi) {
                 if (valid) st_out(crow + k, make_float2(xr, xi));
             });
-        } else {
+        } else if constexpr (OK == 0) {
+            float* crow = static_cast<float*>(a.out) + g * (2 * F);
+            const int sh = (int)((reinterpret_cast<uintptr_t>(crow) >> 2) & 3);  // 0 or 2
+            float2* st = reinterpret_cast<float2*>(region + sh);
+            untangle2<NC, kBatch>(v, j, partner, ub, [&](int k, float xr, float xi) {
+                st[k] = make_float2(xr, xi);
+            });
+            wave_lds_sync();
+            if (valid) store_row_b128<L>(crow, sh, region, 2 * F, j);
+        } else if constexpr (stage_rows(OK, VAR)) {
+            const int kind = a.out_kind;
+            const bool power = kind == OUT_POWER || kind == OUT_POWER_DB;
+            const bool db = kind == OUT_AMP_DB || kind == OUT_POWER_DB;
+            float* frow = static_cast<float*>(a.out) + g * F;
+            const int sh = (int)((reinterpret_cast<uintptr_t>(frow) >> 2) & 3);
+            float* st = region + sh;
+            untangle2<NC, kBatch>(v, j, partner, ub, [&](int k, float xr, float xi) {
+                const float p2 = __builtin_fmaf(xr, xr, xi * xi);
+                float val = power ? p2 : __builtin_amdgcn_sqrtf(p2);
+                if (db) val = power ? db_of(val, a.log_amin, 1e-36f, 10.0f)
+                                    : db_of(val, a.log_amin, 1e-18f, 20.0f);
+                st[k] = val;
+            });
+            wave_lds_sync();
+            if (valid) store_row_b128<L>(frow, sh, region, F, j);
+        } else {  // lane-wise 4-byte stores
             const int kind = a.out_kind;
             const bool power = kind == OUT_POWER || kind == OUT_POWER_DB;
             const bool db = kind == OUT_AMP_DB || kind == OUT_POWER_DB;
@@ -283,10 +344,10 @@ stft3_kernel(StftLaunch a, uint64_t fps) {
 // --------------------------------------------------------------------------------------
 // host-side dispatch
 // --------------------------------------------------------------------------------------
-template <int NC, int WV = kWaves>
-static int lds3_bytes(const StftLaunch& a, bool mel) {
-    return (Geo3<NC, WV>::BASE_FLOATS +
-            (mel ? (a.mel4_rows * 4 + a.mel4_rounds) * Geo2<NC>::L + 2 * a.mel4_rounds : 0)) * 4;
+template <int NC, int OK, int VAR, int WV = kWaves>
+static int lds3_bytes(const StftLaunch& a) {
+    return (Geo3<NC, WV>::BASE_FLOATS_OK(stage_rows(OK, VAR), OK) +
+            (OK == 2 ? (a.mel4_rows * 4 + a.mel4_rounds) * Geo2<NC>::L + 2 * a.mel4_rounds : 0)) * 4;
 }
 
 template <int NC, int OK, int C, int INF, int VAR = 0, int WV = kWaves>
@@ -312,9 +373,13 @@ static int launch3_k(const StftLaunch& a, hipStream_t stream) {
             default: break;
         }
     }
+    if constexpr (VAR == 0 && WV == kWaves && NC == 1024 && OK != 2 && C == 2 && INF == IN_F32) {
+        const char* e = getenv("THESIA_STFT_VARIANT");
+        if (e && atoi(e) == 1024) return launch3_k<NC, OK, C, INF, 1024>(a, stream);  // other row-store method
+    }
 #endif
     constexpr int kBlock = 64 * WV;
-    const int lds = lds3_bytes<NC, WV>(a, OK == 2);
+    const int lds = lds3_bytes<NC, OK, VAR, WV>(a);
     if (lds > 163840) return -2;
     auto kern = stft3_kernel<NC, OK, C, INF, VAR, WV>;
     if (hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
