@@ -10,7 +10,7 @@ import pytest
 
 import oracle_ffi as O
 from thesia import engine
-from tolerances import STFT_REL, stft_frame_err
+from tolerances import DB_MAX, DB_P9999, STFT_REL, db_clamped_err, stft_frame_err
 
 pytestmark = pytest.mark.gpu
 
@@ -69,3 +69,69 @@ def test_streams_across_tracks_edges_and_alignment(n_fft, kernel, channels, fmt,
         ref = O.perform_stft(_mono_fold(x.astype(np.float32)), n_fft, hop, n_fft)
         assert got.shape == ref.shape
         assert stft_frame_err(got, ref) <= STFT_REL, (len(t), stft_frame_err(got, ref))
+
+
+_LIN_KINDS = [engine.OUT_MAG, engine.OUT_POWER, engine.OUT_AMP_DB, engine.OUT_POWER_DB]
+
+
+@pytest.mark.parametrize("n_fft", [256, 2048])
+@pytest.mark.parametrize("kind", _LIN_KINDS + [engine.OUT_COMPLEX])
+@pytest.mark.parametrize("shift", [0, 1, 2, 3])
+@pytest.mark.parametrize("variant", ["0", "1024"])
+def test_row_stores_any_output_alignment(n_fft, kind, shift, variant, monkeypatch):
+    """Output rows of F floats / F float2 are not 16-byte aligned; the LDS-staged float4 row
+    stores (stft3 store_row_b128: linear kinds by default, complex with variant 1024) must write
+    exactly the row whatever the output pointer's alignment, and nothing outside the batch's
+    rows (guard floats on both sides stay untouched)."""
+    if kind == engine.OUT_COMPLEX and shift % 2:
+        pytest.skip("complex rows are float2: 8-byte aligned output")
+    if variant != "0" and n_fft != 2048:
+        pytest.skip("the store-method variant is compiled for n_fft 2048 stereo f32 only")
+    monkeypatch.setenv("THESIA_GRID", "3")
+    monkeypatch.setenv("THESIA_STFT_VARIANT", variant)
+    rng = np.random.default_rng(n_fft + 7 * kind + shift)
+    hop = n_fft // 4
+    lens = [n_fft - 1, 5 * n_fft + 3, 33 * hop + 1, 2 * n_fft]
+    tracks = [(rng.standard_normal((n, 2)) * 0.3).astype(np.float32) for n in lens]
+    plan = engine.Plan(n_fft, n_fft, hop, kind)
+    flat = np.concatenate([t.reshape(-1) for t in tracks])
+    offs = np.cumsum([0] + [t.size for t in tracks[:-1]])
+    din = engine.DeviceBuffer.from_host(flat)
+    T = engine.Batch.frames_for(plan, lens)
+    fl = plan.row_bins * (2 if kind == engine.OUT_COMPLEX else 1)
+    guard = 8
+    sentinel = np.float32(-12345.5)
+    host = np.full(T * fl + 2 * guard + 4, sentinel, np.float32)
+    dout = engine.DeviceBuffer.from_host(host)
+    ptr = dout.ptr.value + (guard + shift) * 4
+    b = engine.Batch(plan, din, offs, lens, ptr, input_format=engine.IN_F32, channels=2)
+    assert b.kernel == 3
+    b.run()
+    engine.synchronize()
+    res = dout.to_host(np.float32)
+    assert np.all(res[:guard + shift] == sentinel)
+    assert np.all(res[guard + shift + T * fl:] == sentinel)
+    got = res[guard + shift:guard + shift + T * fl]
+    for i, t in enumerate(tracks):
+        ref = O.perform_stft(_mono_fold(t), n_fft, hop, n_fft)
+        rows = got[int(b.frame0[i]) * fl:int(b.frame0[i + 1]) * fl]
+        if kind == engine.OUT_COMPLEX:
+            g = rows.view(np.complex64).reshape(ref.shape)
+            assert stft_frame_err(g, ref) <= STFT_REL
+            continue
+        g = rows.reshape(ref.shape)
+        if kind == engine.OUT_MAG:
+            r = O.norm(ref)
+        elif kind == engine.OUT_POWER:
+            r = O.norm_sqr(ref)
+        elif kind == engine.OUT_AMP_DB:
+            r = O.amp_to_db_default(O.norm(ref))
+        else:
+            r = O.power_to_db_default(O.norm_sqr(ref))
+        if kind in (engine.OUT_AMP_DB, engine.OUT_POWER_DB):
+            mx, p = db_clamped_err(g, r)
+            assert mx <= DB_MAX and p <= DB_P9999, (mx, p)
+        else:
+            scale = np.abs(r).max(axis=1, keepdims=True)
+            rel = 4e-6 if kind == engine.OUT_MAG else 8e-6
+            assert np.all(np.abs(g - r) <= rel * np.maximum(scale, 1e-30)), float(np.abs(g - r).max())
