@@ -375,7 +375,12 @@ static int launch3_k(const StftLaunch& a, hipStream_t stream) {
     }
     if constexpr (VAR == 0 && WV == kWaves && NC == 1024 && OK != 2 && C == 2 && INF == IN_F32) {
         const char* e = getenv("THESIA_STFT_VARIANT");
-        if (e && atoi(e) == 1024) return launch3_k<NC, OK, C, INF, 1024>(a, stream);  // other row-store method
+        switch (e ? atoi(e) : 0) {
+            case 1024: return launch3_k<NC, OK, C, INF, 1024>(a, stream);  // other row-store method
+            case 4: return launch3_k<NC, OK, C, INF, 4>(a, stream);  // ablation: no FFT
+            case 1028: return launch3_k<NC, OK, C, INF, 1028>(a, stream);
+            default: break;
+        }
     }
 #endif
     constexpr int kBlock = 64 * WV;
