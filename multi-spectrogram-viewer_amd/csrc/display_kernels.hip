@@ -14,6 +14,7 @@
 #include "kernels.hpp"
 
 #include <cmath>
+#include <cstdlib>
 #include <cstdint>
 
 namespace thesia {
@@ -152,11 +153,8 @@ int launch_minmax_seg(const float* x, const uint64_t* seg0, int n_seg, int nper,
 // ------------------------------------------------------------------------------------
 // K4 spec_to_grey (display.rs:44-54): grey[y][x], y < H, x < T
 // ------------------------------------------------------------------------------------
-__global__ void spec_to_grey_kernel(const float* spec, uint32_t T, uint32_t bins, uint32_t H,
-                                    float max, float min, float* grey) {
-    const uint32_t x = blockIdx.x * blockDim.x + threadIdx.x;
-    const uint32_t y = blockIdx.y;
-    if (x >= T || y >= H) return;
+__device__ __forceinline__ void grey_px(const float* spec, uint32_t T, uint32_t bins, uint32_t H,
+                                        float max, float min, float* grey, uint32_t x, uint32_t y) {
     float v = 0.0f;
     if (y >= H - bins) {
         const float db = spec[(uint64_t)x * bins + (H - 1 - y)];
@@ -165,6 +163,14 @@ __global__ void spec_to_grey_kernel(const float* spec, uint32_t T, uint32_t bins
         v = fminf(v, 1.0f);
     }
     grey[(uint64_t)y * T + x] = v;
+}
+
+__global__ void spec_to_grey_kernel(const float* spec, uint32_t T, uint32_t bins, uint32_t H,
+                                    float max, float min, float* grey) {
+    const uint32_t x = blockIdx.x * blockDim.x + threadIdx.x;
+    const uint32_t y = blockIdx.y;
+    if (x >= T || y >= H) return;
+    grey_px(spec, T, bins, H, max, min, grey, x, y);
 }
 
 int launch_spec_to_grey(const float* spec, uint32_t T, uint32_t bins, uint32_t H, float max,
@@ -178,17 +184,23 @@ int launch_spec_to_grey(const float* spec, uint32_t T, uint32_t bins, uint32_t H
 // ------------------------------------------------------------------------------------
 // K5 vertical Lanczos3 pass: out[oy][x] = sum_i in[left+i][x] * w[i] (sequential order)
 // ------------------------------------------------------------------------------------
+__device__ __forceinline__ void resize_v_px(const float* in, uint32_t w, const int32_t* left,
+                                            const int32_t* cnt, const int32_t* woff,
+                                            const float* wts, float* out, uint32_t x, uint32_t oy) {
+    const int32_t l = left[oy], n = cnt[oy];
+    const float* wr = wts + woff[oy];
+    float t = 0.0f;
+    for (int32_t i = 0; i < n; ++i) t += in[(uint64_t)(l + i) * w + x] * wr[i];
+    out[(uint64_t)oy * w + x] = t;
+}
+
 __global__ void resize_v_kernel(const float* in, uint32_t w, uint32_t nh, const int32_t* left,
                                 const int32_t* cnt, const int32_t* woff, const float* wts,
                                 float* out) {
     const uint32_t x = blockIdx.x * blockDim.x + threadIdx.x;
     const uint32_t oy = blockIdx.y;
     if (x >= w || oy >= nh) return;
-    const int32_t l = left[oy], n = cnt[oy];
-    const float* wr = wts + woff[oy];
-    float t = 0.0f;
-    for (int32_t i = 0; i < n; ++i) t += in[(uint64_t)(l + i) * w + x] * wr[i];
-    out[(uint64_t)oy * w + x] = t;
+    resize_v_px(in, w, left, cnt, woff, wts, out, x, oy);
 }
 
 int launch_resize_v(const float* in, uint32_t w, uint32_t h, uint32_t nh, const int32_t* left,
@@ -212,12 +224,11 @@ __device__ __forceinline__ uint8_t sat_u8(float v) {  // Rust `as u8`
     return (uint8_t)v;
 }
 
-__global__ void resize_h_rgb_kernel(const float* in, uint32_t w, uint32_t nh, uint32_t nw,
-                                    const int32_t* left, const int32_t* cnt, const int32_t* woff,
-                                    const float* wts, const uint8_t* cmap, uint8_t* out) {
-    const uint32_t ox = blockIdx.x * blockDim.x + threadIdx.x;
-    const uint32_t y = blockIdx.y;
-    if (ox >= nw || y >= nh) return;
+__device__ __forceinline__ void resize_h_rgb_px(const float* in, uint32_t w, uint32_t nw,
+                                                const int32_t* left, const int32_t* cnt,
+                                                const int32_t* woff, const float* wts,
+                                                const uint8_t* cmap, uint8_t* out, uint32_t ox,
+                                                uint32_t y) {
     const int32_t l = left[ox], n = cnt[ox];
     const float* wr = wts + woff[ox];
     const float* row = in + (uint64_t)y * w;
@@ -243,6 +254,182 @@ __global__ void resize_h_rgb_kernel(const float* in, uint32_t w, uint32_t nh, ui
         const float av = (float)cmap[index * 3 + c], bv = (float)cmap[(index + 1) * 3 + c];
         o[c] = sat_u8(roundf(ratio * bv + (1.0f - ratio) * av));
     }
+}
+
+__global__ void resize_h_rgb_kernel(const float* in, uint32_t w, uint32_t nh, uint32_t nw,
+                                    const int32_t* left, const int32_t* cnt, const int32_t* woff,
+                                    const float* wts, const uint8_t* cmap, uint8_t* out) {
+    const uint32_t ox = blockIdx.x * blockDim.x + threadIdx.x;
+    const uint32_t y = blockIdx.y;
+    if (ox >= nw || y >= nh) return;
+    resize_h_rgb_px(in, w, nw, left, cnt, woff, wts, cmap, out, ox, y);
+}
+
+// ------------------------------------------------------------------------------------
+// Batched render (render_rgb_batch_device): every track of a geometry group in ONE launch per
+// stage, blockIdx.z = track, per-track geometry, workspace offsets and Lanczos tap tables from a
+// descriptor array (RenderDesc). Same per-pixel bodies as the per-track kernels (bit-identical
+// bytes); replaces 3 launches per track (9-17 us each for one image, launch- and tail-bound).
+// ------------------------------------------------------------------------------------
+__global__ void spec_to_grey_batch_kernel(const float* spec, uint32_t bins, float max, float min,
+                                          const RenderDesc* d, float* grey) {
+    const RenderDesc r = d[blockIdx.z];
+    const uint32_t x = blockIdx.x * blockDim.x + threadIdx.x;
+    for (uint32_t y = blockIdx.y; y < r.H; y += gridDim.y)
+        if (x < r.T) grey_px(spec + r.spec_off, r.T, bins, r.H, max, min, grey + r.grey_off, x, y);
+}
+
+__global__ void resize_v_batch_kernel(uint32_t nh, const RenderDesc* d, const float* grey,
+                                      float* tmp) {
+    const RenderDesc r = d[blockIdx.z];
+    const uint32_t x = blockIdx.x * blockDim.x + threadIdx.x;
+    if (x >= r.T) return;
+    const float* in = grey + r.grey_off + x;
+    for (uint32_t oy = blockIdx.y; oy < nh; oy += gridDim.y) {
+        const int32_t l = r.vl[oy], n = r.vc[oy];  // row-uniform: scalar loads
+        if (n > 16) {
+            resize_v_px(grey + r.grey_off, r.T, r.vl, r.vc, r.vo, r.vw, tmp + r.tmp_off, x, oy);
+            continue;
+        }
+        const float* wr = r.vw + r.vo[oy];
+        const float* src = in + (uint64_t)l * r.T;
+        // all tap loads in flight together; the sum in resize_v_px's order
+        float v[16];
+#pragma unroll
+        for (int i = 0; i < 16; ++i) v[i] = i < n ? src[(uint64_t)i * r.T] : 0.0f;
+        float t = 0.0f;
+#pragma unroll
+        for (int i = 0; i < 16; ++i)
+            if (i < n) t += v[i] * wr[i];
+        tmp[r.tmp_off + (uint64_t)oy * r.T + x] = t;
+    }
+}
+
+// the colormap of one horizontal-pass value (display.rs:24-42), as resize_h_rgb_px
+__device__ __forceinline__ void colormap_px(float t, const uint8_t* cmap, uint8_t* o) {
+    float x = t;
+    if (!(x >= 0.0f)) x = 0.0f;
+    const float position = 10.0f * x;
+    const float fl = floorf(position);
+    if (fl >= 9.0f) {
+        o[0] = cmap[27];
+        o[1] = cmap[28];
+        o[2] = cmap[29];
+        return;
+    }
+    const int index = (int)fl;
+    const float ratio = position - (float)index;
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+        const float av = (float)cmap[index * 3 + c], bv = (float)cmap[(index + 1) * 3 + c];
+        o[c] = sat_u8(roundf(ratio * bv + (1.0f - ratio) * av));
+    }
+}
+
+// A block owns 256 output columns of one image and walks its rows (blockIdx.y-strided); a
+// thread's column taps (left, count, up to kHTaps weights) are loaded once into registers. The
+// sum runs in resize_h_rgb_px's order (t = 0; t += in * w, i ascending). The row segment's RGB
+// bytes are assembled in LDS and leave as aligned 32-bit words (3-byte pixels stored lane by
+// lane are byte stores at stride 3).
+constexpr int kHTaps = 16;
+constexpr int kHSpan = 2048;  // floats of a row segment staged in LDS
+__global__ void __launch_bounds__(256) resize_h_rgb_batch_kernel(uint32_t nh, const RenderDesc* d,
+                                                                 const float* tmp,
+                                                                 const uint8_t* cmap, uint8_t* rgb) {
+    __shared__ uint8_t seg[256 * 3];
+    __shared__ uint8_t cm[32];
+    const RenderDesc r = d[blockIdx.z];
+    const uint32_t ox0 = blockIdx.x * 256;
+    if (ox0 >= r.nw) return;  // block-uniform
+    if (threadIdx.x < 30) cm[threadIdx.x] = cmap[threadIdx.x];
+    const uint32_t ox = ox0 + threadIdx.x;
+    const bool act = ox < r.nw;
+    int32_t l = 0, n = 0;
+    float w[kHTaps];
+    const float* wr = r.hw;
+    if (act) {
+        l = r.hl[ox];
+        n = r.hc[ox];
+        wr = r.hw + r.ho[ox];
+    }
+#pragma unroll
+    for (int i = 0; i < kHTaps; ++i) w[i] = (i < n && n <= kHTaps) ? wr[i] : 0.0f;
+    const uint32_t npx = r.nw - ox0 < 256u ? r.nw - ox0 : 256u;
+    const uint32_t nb = 3 * npx;
+    // the block's input span [lb, lb + span) of each row is staged in LDS when it fits (the
+    // taps of 256 neighbouring columns overlap: one coalesced load per element instead of up
+    // to kHTaps partially-masked gathers per column)
+    // + kHTaps zeros after the span: the staged sum runs all kHTaps terms branch-free, the
+    // terms past a column's count being (+0 weight) x (finite value) = +-0, which leave the
+    // sum's bits unchanged (t is never -0: it starts at +0 and x + -x rounds to +0)
+    __shared__ float rin[kHSpan + kHTaps];
+    for (int k = threadIdx.x; k < kHSpan + kHTaps; k += 256) rin[k] = 0.0f;
+    const int32_t lb = r.hl[ox0];
+    const uint32_t last = ox0 + npx - 1;
+    int32_t span = r.hl[last] + r.hc[last] - lb;  // supports are monotone in ox
+    span = span < 0 ? 0 : (span > kHSpan ? kHSpan : span);
+    // a column whose taps leave [lb, lb + span) (none for resize's tables) sends the whole
+    // block down the direct path
+    const bool fits = !act || (l >= lb && l + n <= lb + span && n <= kHTaps);
+    const bool staged = __syncthreads_and(fits) != 0;
+    __syncthreads();
+    for (uint32_t y = blockIdx.y; y < nh; y += gridDim.y) {
+        if (staged) {
+            const float* src = tmp + r.tmp_off + (uint64_t)y * r.T + lb;
+            for (int32_t k = threadIdx.x; k < span; k += 256) rin[k] = src[k];
+            __syncthreads();
+        }
+        if (act) {
+            const float* row = tmp + r.tmp_off + (uint64_t)y * r.T + l;
+            float t = 0.0f;
+            if (staged) {
+                const int base = l - lb;
+#pragma unroll
+                for (int i = 0; i < kHTaps; ++i) t += rin[base + i] * w[i];
+            } else if (n <= kHTaps) {
+                float v[kHTaps];
+#pragma unroll
+                for (int i = 0; i < kHTaps; ++i) v[i] = i < n ? row[i] : 0.0f;
+#pragma unroll
+                for (int i = 0; i < kHTaps; ++i)
+                    if (i < n) t += v[i] * w[i];
+            } else {
+                for (int32_t i = 0; i < n; ++i) t += row[i] * wr[i];
+            }
+            colormap_px(t, cm, seg + 3 * threadIdx.x);
+        }
+        __syncthreads();
+        uint8_t* g = rgb + r.rgb_off + ((uint64_t)y * r.nw + ox0) * 3;
+        const uint32_t mis = (uint32_t)(reinterpret_cast<uintptr_t>(g) & 3);
+        const uint32_t head = mis ? (4 - mis < nb ? 4 - mis : nb) : 0;
+        if (threadIdx.x < head) g[threadIdx.x] = seg[threadIdx.x];
+        const uint32_t nwords = (nb - head) / 4;
+        uint32_t* gw = reinterpret_cast<uint32_t*>(g + head);
+        for (uint32_t k = threadIdx.x; k < nwords; k += 256) {
+            const uint32_t b = head + 4 * k;
+            gw[k] = (uint32_t)seg[b] | ((uint32_t)seg[b + 1] << 8) | ((uint32_t)seg[b + 2] << 16) |
+                    ((uint32_t)seg[b + 3] << 24);
+        }
+        for (uint32_t b = head + 4 * nwords + threadIdx.x; b < nb; b += 256) g[b] = seg[b];
+        __syncthreads();
+    }
+}
+
+int launch_render_batch(const float* spec, uint32_t bins, float max, float min,
+                        const RenderDesc* d_desc, uint32_t n, uint32_t T_max, uint32_t H_max,
+                        uint32_t nw_max, uint32_t nh, float* grey, float* tmp,
+                        const uint8_t* cmap, uint8_t* rgb, hipStream_t s) {
+    if (n == 0 || nh == 0) return 0;
+    if (n > 65535) return -2;
+    uint32_t ry = 64;  // grid.y: row blocks per image (strided row loop inside)
+    if (const char* e = getenv("THESIA_RENDER_RY")) ry = (uint32_t)atoi(e) > 0 ? (uint32_t)atoi(e) : 64;
+    dim3 g1((T_max + 255) / 256, H_max < ry ? (H_max ? H_max : 1) : ry, n);
+    hipLaunchKernelGGL(spec_to_grey_batch_kernel, g1, dim3(256), 0, s, spec, bins, max, min, d_desc, grey);
+    dim3 g2((T_max + 255) / 256, nh < ry ? nh : ry, n);
+    hipLaunchKernelGGL(resize_v_batch_kernel, g2, dim3(256), 0, s, nh, d_desc, grey, tmp);
+    dim3 g3((nw_max + 255) / 256, nh < ry ? nh : ry, n);
+    hipLaunchKernelGGL(resize_h_rgb_batch_kernel, g3, dim3(256), 0, s, nh, d_desc, tmp, cmap, rgb);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
 int launch_resize_h_rgb(const float* in, uint32_t w, uint32_t nh, uint32_t nw,

@@ -751,6 +751,72 @@ int render_rgb_batch_device(const float* d_spec, const uint64_t* row0, size_t bi
         }
         cmap_ptr = cm.as<uint8_t>();
     }
+    if (!getenv("THESIA_RENDER_PER_TRACK")) {
+        // every track in one launch per stage (launch_render_batch); workspaces for all tracks
+        std::vector<RenderDesc> desc;
+        desc.reserve(n);
+        uint64_t grey_tot = 0, tmp_tot = 0;
+        uint32_t T_max = 0, H_max = 0, nw_max = 0;
+        for (size_t i = 0; i < n; ++i) {
+            const uint32_t T = (uint32_t)(row0[i + 1] - row0[i]);
+            if (T == 0 || nwidth[i] == 0) continue;
+            const DevTaps *vt = nullptr, *ht = nullptr;
+            int rc = dev_taps(H[i], nheight, &vt);
+            if (!rc) rc = dev_taps(T, nwidth[i], &ht);
+            if (rc) return rc;
+            RenderDesc r{};
+            r.spec_off = row0[i] * bins;
+            r.grey_off = grey_tot;
+            r.tmp_off = tmp_tot;
+            r.rgb_off = rgb_off[i];
+            r.T = T;
+            r.H = H[i];
+            r.nw = nwidth[i];
+            r.vl = vt->left.as<int32_t>(); r.vc = vt->count.as<int32_t>();
+            r.vo = vt->offset.as<int32_t>(); r.vw = vt->weights.as<float>();
+            r.hl = ht->left.as<int32_t>(); r.hc = ht->count.as<int32_t>();
+            r.ho = ht->offset.as<int32_t>(); r.hw = ht->weights.as<float>();
+            grey_tot += (uint64_t)H[i] * T;
+            tmp_tot += (uint64_t)T * nheight;
+            T_max = std::max(T_max, T);
+            H_max = std::max(H_max, H[i]);
+            nw_max = std::max(nw_max, nwidth[i]);
+            desc.push_back(r);
+        }
+        if (desc.empty()) return THESIA_OK;
+        // grow-only workspaces per device, held for the call (hipMalloc / hipFree of a few
+        // hundred MB per call measured as multi-ms stalls in the C5 step)
+        struct Ws { DevBuf grey, tmp, desc; };
+        static std::mutex ws_mu;
+        static auto& ws_map = *new std::map<int, Ws>();  // leaked, see dev_taps
+        int dev = 0;
+        (void)hipGetDevice(&dev);
+        std::lock_guard<std::mutex> lk(ws_mu);
+        Ws& ws = ws_map[dev];
+        auto grow = [](DevBuf& b, size_t bytes) {
+            if (b.bytes >= bytes && b.p) return 0;
+            b.release();
+            return b.alloc(bytes + bytes / 8);
+        };
+        int rc = grow(ws.grey, grey_tot * sizeof(float));
+        if (!rc) rc = grow(ws.tmp, tmp_tot * sizeof(float));
+        if (!rc) rc = grow(ws.desc, desc.size() * sizeof(RenderDesc));
+        if (rc) return rc;
+        THESIA_HIP(hipMemcpyAsync(ws.desc.p, desc.data(), desc.size() * sizeof(RenderDesc),
+                                  hipMemcpyHostToDevice, s));
+        DevBuf& grey = ws.grey;
+        DevBuf& tmp = ws.tmp;
+        DevBuf& ddesc = ws.desc;
+        for (size_t b = 0; b < desc.size(); b += 65535) {  // grid.z limit
+            const uint32_t nb = (uint32_t)std::min<size_t>(65535, desc.size() - b);
+            if (launch_render_batch(d_spec, (uint32_t)bins, max, min, ddesc.as<RenderDesc>() + b, nb,
+                                    T_max, H_max, nw_max, nheight, grey.as<float>(), tmp.as<float>(),
+                                    cmap_ptr, d_rgb, s))
+                return set_error(THESIA_ERR_DEVICE, "render batch launch failed");
+        }
+        THESIA_HIP(hipStreamSynchronize(s));
+        return THESIA_OK;
+    }
     DevBuf grey, tmp;
     int rc = grey.alloc(grey_max * sizeof(float));
     if (!rc) rc = tmp.alloc(tmp_max * sizeof(float));

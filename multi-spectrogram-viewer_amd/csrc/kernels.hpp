@@ -104,6 +104,21 @@ int launch_minmax(const float* x, uint64_t n, float* partial /*[2*nblk]*/, int* 
                   int nblk, hipStream_t s);
 int launch_minmax_seg(const float* x, const uint64_t* seg0, int n_seg, int nper, float* partial,
                       int* nan_flag, hipStream_t s);
+// One track of a batched render (launch_render_batch): offsets in elements of the batch's
+// spectrogram / grey / tmp buffers and bytes of the RGB buffer; the vertical (H -> nheight) and
+// horizontal (T -> nw) Lanczos3 tap tables (device pointers, cached per geometry).
+struct RenderDesc {
+    uint64_t spec_off, grey_off, tmp_off, rgb_off;
+    uint32_t T, H, nw, pad;
+    const int32_t *vl, *vc, *vo;
+    const float* vw;
+    const int32_t *hl, *hc, *ho;
+    const float* hw;
+};
+int launch_render_batch(const float* spec, uint32_t bins, float max, float min,
+                        const RenderDesc* d_desc, uint32_t n, uint32_t T_max, uint32_t H_max,
+                        uint32_t nw_max, uint32_t nh, float* grey, float* tmp,
+                        const uint8_t* cmap, uint8_t* rgb, hipStream_t s);
 int launch_spec_to_grey(const float* spec, uint32_t T, uint32_t bins, uint32_t H, float max,
                         float min, float* grey, hipStream_t s);
 int launch_resize_v(const float* in, uint32_t w, uint32_t h, uint32_t nh, const int32_t* left,

@@ -92,3 +92,28 @@ def test_c5_mixed_rate_render_pipeline():
         grey = O.spec_to_grey(r.db, up, gmax, gmin)
         img, _ = O.grey_to_rgb(grey, r.nwidth, 120)
         assert r.rgb.tobytes() == img.tobytes(), (t.sr, t.n_fft)  # display path bit-exact
+
+
+@pytest.mark.parametrize("per_track", [False, True])
+@pytest.mark.parametrize("px_per_sec", [73.0, 9.0])  # 9 px/s: > 16 horizontal taps (direct path)
+def test_render_batch_ragged_groups(per_track, px_per_sec, monkeypatch):
+    """Several tracks of different lengths per geometry group: the batched render (one launch
+    per stage for the whole group, blockIdx.z = track) and the per-track launches produce the
+    oracle's bytes for every image (ragged T, nwidth and workspace offsets)."""
+    if per_track:
+        monkeypatch.setenv("THESIA_RENDER_PER_TRACK", "1")
+    base = pipeline.c5_tracks(12, seconds=0.6)
+    tracks = []
+    for k, t in enumerate(base[:4] * 3):  # 4 geometries x 3 lengths each
+        n = int(t.pcm.shape[0] * (0.5 + 0.35 * (k // 4))) + 3 * k
+        n = max(n, t.n_fft)
+        tracks.append(pipeline.Track(t.pcm[:n].copy(), t.sr, t.n_fft))
+    out = pipeline.render_tracks(tracks, px_per_sec=px_per_sec, nheight=90, keep_db=True)
+    gmax, gmin, max_sr = shard.global_db_range(max(r.spec_max for r in out),
+                                               min(r.spec_min for r in out),
+                                               max(t.sr for t in tracks))
+    for t, r in zip(tracks, out):
+        up = shard.up_ratio(t.sr, max_sr, freq_scale_mel=False)
+        grey = O.spec_to_grey(r.db, up, gmax, gmin)
+        img, _ = O.grey_to_rgb(grey, r.nwidth, 90)
+        assert r.rgb.tobytes() == img.tobytes(), (t.sr, t.n_fft, t.pcm.shape)
