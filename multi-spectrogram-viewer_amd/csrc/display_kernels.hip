@@ -326,23 +326,30 @@ __device__ __forceinline__ void colormap_px(float t, const uint8_t* cmap, uint8_
     }
 }
 
-// A block owns 256 output columns of one image and walks its rows (blockIdx.y-strided); a
-// thread's column taps (left, count, up to kHTaps weights) are loaded once into registers. The
+// A block owns 256 output columns of one image and walks its rows (blockIdx.y-strided). The
+// block's input span [lb, lb + span) of each row is staged in LDS (one coalesced load per
+// element; the taps of neighbouring columns overlap). Columns with <= kHTaps taps keep their
+// weights in registers and sum branch-free; columns with more (downsampling: up to ntap, the
+// group's maximum) read their weights from an LDS copy laid out tap-major (conflict-free). The
 // sum runs in resize_h_rgb_px's order (t = 0; t += in * w, i ascending). The row segment's RGB
 // bytes are assembled in LDS and leave as aligned 32-bit words (3-byte pixels stored lane by
-// lane are byte stores at stride 3).
+// lane are byte stores at stride 3). A block whose taps do not fit takes the direct path.
 constexpr int kHTaps = 16;
-constexpr int kHSpan = 2048;  // floats of a row segment staged in LDS
 __global__ void __launch_bounds__(256) resize_h_rgb_batch_kernel(uint32_t nh, const RenderDesc* d,
                                                                  const float* tmp,
-                                                                 const uint8_t* cmap, uint8_t* rgb) {
-    __shared__ uint8_t seg[256 * 3];
-    __shared__ uint8_t cm[32];
+                                                                 const uint8_t* cmap, uint8_t* rgb,
+                                                                 int ntap, int span_cap, int abl) {
+    extern __shared__ __attribute__((aligned(16))) float hsm[];
+    float* rin = hsm;                                       // span_cap + kHTaps floats
+    float* wl = hsm + span_cap + kHTaps;                    // ntap x 256 (when ntap > kHTaps)
+    uint8_t* seg = reinterpret_cast<uint8_t*>(wl + (ntap > kHTaps ? ntap * 256 : 0));
+    uint8_t* cm = seg + 256 * 3;
     const RenderDesc r = d[blockIdx.z];
     const uint32_t ox0 = blockIdx.x * 256;
     if (ox0 >= r.nw) return;  // block-uniform
-    if (threadIdx.x < 30) cm[threadIdx.x] = cmap[threadIdx.x];
-    const uint32_t ox = ox0 + threadIdx.x;
+    const int tid = threadIdx.x;
+    if (tid < 30) cm[tid] = cmap[tid];
+    const uint32_t ox = ox0 + tid;
     const bool act = ox < r.nw;
     int32_t l = 0, n = 0;
     float w[kHTaps];
@@ -354,71 +361,70 @@ __global__ void __launch_bounds__(256) resize_h_rgb_batch_kernel(uint32_t nh, co
     }
 #pragma unroll
     for (int i = 0; i < kHTaps; ++i) w[i] = (i < n && n <= kHTaps) ? wr[i] : 0.0f;
-    const uint32_t npx = r.nw - ox0 < 256u ? r.nw - ox0 : 256u;
-    const uint32_t nb = 3 * npx;
-    // the block's input span [lb, lb + span) of each row is staged in LDS when it fits (the
-    // taps of 256 neighbouring columns overlap: one coalesced load per element instead of up
-    // to kHTaps partially-masked gathers per column)
-    // + kHTaps zeros after the span: the staged sum runs all kHTaps terms branch-free, the
+    const bool wide = n > kHTaps && n <= ntap && ntap > kHTaps;
+    if (wide)
+        for (int i = 0; i < n; ++i) wl[i * 256 + tid] = wr[i];
+    // + kHTaps zeros after the span: the register sum runs all kHTaps terms branch-free, the
     // terms past a column's count being (+0 weight) x (finite value) = +-0, which leave the
     // sum's bits unchanged (t is never -0: it starts at +0 and x + -x rounds to +0)
-    __shared__ float rin[kHSpan + kHTaps];
-    for (int k = threadIdx.x; k < kHSpan + kHTaps; k += 256) rin[k] = 0.0f;
+    for (int k = tid; k < span_cap + kHTaps; k += 256) rin[k] = 0.0f;
+    const uint32_t npx = r.nw - ox0 < 256u ? r.nw - ox0 : 256u;
+    const uint32_t nb = 3 * npx;
     const int32_t lb = r.hl[ox0];
     const uint32_t last = ox0 + npx - 1;
     int32_t span = r.hl[last] + r.hc[last] - lb;  // supports are monotone in ox
-    span = span < 0 ? 0 : (span > kHSpan ? kHSpan : span);
-    // a column whose taps leave [lb, lb + span) (none for resize's tables) sends the whole
-    // block down the direct path
-    const bool fits = !act || (l >= lb && l + n <= lb + span && n <= kHTaps);
+    span = span < 0 ? 0 : (span > span_cap ? span_cap : span);
+    const bool fits = !act || (l >= lb && l + n <= lb + span && (n <= kHTaps || wide));
     const bool staged = __syncthreads_and(fits) != 0;
-    __syncthreads();
     for (uint32_t y = blockIdx.y; y < nh; y += gridDim.y) {
         if (staged) {
             const float* src = tmp + r.tmp_off + (uint64_t)y * r.T + lb;
-            for (int32_t k = threadIdx.x; k < span; k += 256) rin[k] = src[k];
+            if (!(abl & 4))  // ablation (timing only): no row loads
+                for (int32_t k = tid; k < span; k += 256) rin[k] = src[k];
             __syncthreads();
         }
         if (act) {
-            const float* row = tmp + r.tmp_off + (uint64_t)y * r.T + l;
             float t = 0.0f;
             if (staged) {
                 const int base = l - lb;
+                if (n <= kHTaps) {
 #pragma unroll
-                for (int i = 0; i < kHTaps; ++i) t += rin[base + i] * w[i];
-            } else if (n <= kHTaps) {
-                float v[kHTaps];
-#pragma unroll
-                for (int i = 0; i < kHTaps; ++i) v[i] = i < n ? row[i] : 0.0f;
-#pragma unroll
-                for (int i = 0; i < kHTaps; ++i)
-                    if (i < n) t += v[i] * w[i];
+                    for (int i = 0; i < kHTaps; ++i) t += rin[base + i] * w[i];
+                } else {
+                    for (int i = 0; i < n; ++i) t += rin[base + i] * wl[i * 256 + tid];
+                }
             } else {
+                const float* row = tmp + r.tmp_off + (uint64_t)y * r.T + l;
                 for (int32_t i = 0; i < n; ++i) t += row[i] * wr[i];
             }
-            colormap_px(t, cm, seg + 3 * threadIdx.x);
+            if (abl & 1) {  // ablation (timing only): no colormap
+                seg[3 * tid] = (uint8_t)t;
+            } else {
+                colormap_px(t, cm, seg + 3 * tid);
+            }
         }
         __syncthreads();
+        if (abl & 2) { __syncthreads(); continue; }  // ablation: no global stores
         uint8_t* g = rgb + r.rgb_off + ((uint64_t)y * r.nw + ox0) * 3;
         const uint32_t mis = (uint32_t)(reinterpret_cast<uintptr_t>(g) & 3);
         const uint32_t head = mis ? (4 - mis < nb ? 4 - mis : nb) : 0;
-        if (threadIdx.x < head) g[threadIdx.x] = seg[threadIdx.x];
+        if ((uint32_t)tid < head) g[tid] = seg[tid];
         const uint32_t nwords = (nb - head) / 4;
         uint32_t* gw = reinterpret_cast<uint32_t*>(g + head);
-        for (uint32_t k = threadIdx.x; k < nwords; k += 256) {
+        for (uint32_t k = tid; k < nwords; k += 256) {
             const uint32_t b = head + 4 * k;
             gw[k] = (uint32_t)seg[b] | ((uint32_t)seg[b + 1] << 8) | ((uint32_t)seg[b + 2] << 16) |
                     ((uint32_t)seg[b + 3] << 24);
         }
-        for (uint32_t b = head + 4 * nwords + threadIdx.x; b < nb; b += 256) g[b] = seg[b];
+        for (uint32_t b = head + 4 * nwords + tid; b < nb; b += 256) g[b] = seg[b];
         __syncthreads();
     }
 }
 
 int launch_render_batch(const float* spec, uint32_t bins, float max, float min,
                         const RenderDesc* d_desc, uint32_t n, uint32_t T_max, uint32_t H_max,
-                        uint32_t nw_max, uint32_t nh, float* grey, float* tmp,
-                        const uint8_t* cmap, uint8_t* rgb, hipStream_t s) {
+                        uint32_t nw_max, uint32_t nh, int h_taps, int h_span, float* grey,
+                        float* tmp, const uint8_t* cmap, uint8_t* rgb, hipStream_t s) {
     if (n == 0 || nh == 0) return 0;
     if (n > 65535) return -2;
     uint32_t ry = 64;  // grid.y: row blocks per image (strided row loop inside)
@@ -428,7 +434,17 @@ int launch_render_batch(const float* spec, uint32_t bins, float max, float min,
     dim3 g2((T_max + 255) / 256, nh < ry ? nh : ry, n);
     hipLaunchKernelGGL(resize_v_batch_kernel, g2, dim3(256), 0, s, nh, d_desc, grey, tmp);
     dim3 g3((nw_max + 255) / 256, nh < ry ? nh : ry, n);
-    hipLaunchKernelGGL(resize_h_rgb_batch_kernel, g3, dim3(256), 0, s, nh, d_desc, tmp, cmap, rgb);
+    // LDS: the staged span (+ kHTaps zeros), tap-major weights for > kHTaps taps, RGB segment,
+    // colormap; beyond 64 KiB the weights (then the span) stay in HBM (direct path)
+    int taps = h_taps > kHTaps ? h_taps : 0;
+    int span = h_span;
+    auto lds = [&]() { return (span + kHTaps + taps * 256) * 4 + 256 * 3 + 32; };
+    if (lds() > 65536) taps = 0;
+    if (lds() > 65536) span = 4096;
+    int abl = 0;
+    if (const char* e = getenv("THESIA_RENDER_ABL")) abl = atoi(e);
+    hipLaunchKernelGGL(resize_h_rgb_batch_kernel, g3, dim3(256), lds(), s, nh, d_desc, tmp, cmap, rgb,
+                       taps, span, abl);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 

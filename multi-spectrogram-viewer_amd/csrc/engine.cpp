@@ -757,6 +757,7 @@ int render_rgb_batch_device(const float* d_spec, const uint64_t* row0, size_t bi
         desc.reserve(n);
         uint64_t grey_tot = 0, tmp_tot = 0;
         uint32_t T_max = 0, H_max = 0, nw_max = 0;
+        int h_taps = 0, h_span = 0;  // horizontal pass: max taps, max input span of 256 columns
         for (size_t i = 0; i < n; ++i) {
             const uint32_t T = (uint32_t)(row0[i + 1] - row0[i]);
             if (T == 0 || nwidth[i] == 0) continue;
@@ -778,6 +779,8 @@ int render_rgb_batch_device(const float* d_spec, const uint64_t* row0, size_t bi
             r.ho = ht->offset.as<int32_t>(); r.hw = ht->weights.as<float>();
             grey_tot += (uint64_t)H[i] * T;
             tmp_tot += (uint64_t)T * nheight;
+            h_taps = std::max(h_taps, ht->max_taps);
+            h_span = std::max<int>(h_span, (int)((256.0 * T + nwidth[i] - 1) / nwidth[i]) + ht->max_taps + 8);
             T_max = std::max(T_max, T);
             H_max = std::max(H_max, H[i]);
             nw_max = std::max(nw_max, nwidth[i]);
@@ -810,7 +813,7 @@ int render_rgb_batch_device(const float* d_spec, const uint64_t* row0, size_t bi
         for (size_t b = 0; b < desc.size(); b += 65535) {  // grid.z limit
             const uint32_t nb = (uint32_t)std::min<size_t>(65535, desc.size() - b);
             if (launch_render_batch(d_spec, (uint32_t)bins, max, min, ddesc.as<RenderDesc>() + b, nb,
-                                    T_max, H_max, nw_max, nheight, grey.as<float>(), tmp.as<float>(),
+                                    T_max, H_max, nw_max, nheight, h_taps, h_span, grey.as<float>(), tmp.as<float>(),
                                     cmap_ptr, d_rgb, s))
                 return set_error(THESIA_ERR_DEVICE, "render batch launch failed");
         }

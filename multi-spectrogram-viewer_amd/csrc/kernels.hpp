@@ -117,8 +117,8 @@ struct RenderDesc {
 };
 int launch_render_batch(const float* spec, uint32_t bins, float max, float min,
                         const RenderDesc* d_desc, uint32_t n, uint32_t T_max, uint32_t H_max,
-                        uint32_t nw_max, uint32_t nh, float* grey, float* tmp,
-                        const uint8_t* cmap, uint8_t* rgb, hipStream_t s);
+                        uint32_t nw_max, uint32_t nh, int h_taps, int h_span, float* grey,
+                        float* tmp, const uint8_t* cmap, uint8_t* rgb, hipStream_t s);
 int launch_spec_to_grey(const float* spec, uint32_t T, uint32_t bins, uint32_t H, float max,
                         float min, float* grey, hipStream_t s);
 int launch_resize_v(const float* in, uint32_t w, uint32_t h, uint32_t nh, const int32_t* left,

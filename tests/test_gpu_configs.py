@@ -95,7 +95,7 @@ def test_c5_mixed_rate_render_pipeline():
 
 
 @pytest.mark.parametrize("per_track", [False, True])
-@pytest.mark.parametrize("px_per_sec", [73.0, 9.0])  # 9 px/s: > 16 horizontal taps (direct path)
+@pytest.mark.parametrize("px_per_sec", [73.0, 30.0, 9.0])  # 30: 17-64 taps (LDS weights); 9: > 64 (direct)
 def test_render_batch_ragged_groups(per_track, px_per_sec, monkeypatch):
     """Several tracks of different lengths per geometry group: the batched render (one launch
     per stage for the whole group, blockIdx.z = track) and the per-track launches produce the
