@@ -285,7 +285,12 @@ __global__ void resize_v_batch_kernel(uint32_t nh, const RenderDesc* d, const fl
     const uint32_t x = blockIdx.x * blockDim.x + threadIdx.x;
     if (x >= r.T) return;
     const float* in = grey + r.grey_off + x;
-    for (uint32_t oy = blockIdx.y; oy < nh; oy += gridDim.y) {
+    // a block walks a contiguous run of output rows: consecutive rows share most of their taps,
+    // so the grey rows they read are L1 hits after the first (a row-strided walk re-reads them
+    // from L2 once per tap: the pass was L2-bandwidth-bound)
+    const uint32_t rpb = (nh + gridDim.y - 1) / gridDim.y;
+    const uint32_t oy1 = (blockIdx.y + 1) * rpb < nh ? (blockIdx.y + 1) * rpb : nh;
+    for (uint32_t oy = blockIdx.y * rpb; oy < oy1; ++oy) {
         const int32_t l = r.vl[oy], n = r.vc[oy];  // row-uniform: scalar loads
         if (n > 16) {
             resize_v_px(grey + r.grey_off, r.T, r.vl, r.vc, r.vo, r.vw, tmp + r.tmp_off, x, oy);
