@@ -271,12 +271,37 @@ __global__ void resize_h_rgb_kernel(const float* in, uint32_t w, uint32_t nh, ui
 // descriptor array (RenderDesc). Same per-pixel bodies as the per-track kernels (bit-identical
 // bytes); replaces 3 launches per track (9-17 us each for one image, launch- and tail-bound).
 // ------------------------------------------------------------------------------------
-__global__ void spec_to_grey_batch_kernel(const float* spec, uint32_t bins, float max, float min,
-                                          const RenderDesc* d, float* grey) {
+// 64 x 64 tiles through LDS: the spectrogram is read along bins (coalesced) and the grey image
+// written along frames (coalesced); the per-pixel arithmetic is grey_px's.
+__global__ void __launch_bounds__(256) spec_to_grey_batch_kernel(const float* spec, uint32_t bins,
+                                                                 float max, float min,
+                                                                 const RenderDesc* d, float* grey) {
+    __shared__ float tile[64][65];
     const RenderDesc r = d[blockIdx.z];
-    const uint32_t x = blockIdx.x * blockDim.x + threadIdx.x;
-    for (uint32_t y = blockIdx.y; y < r.H; y += gridDim.y)
-        if (x < r.T) grey_px(spec + r.spec_off, r.T, bins, r.H, max, min, grey + r.grey_off, x, y);
+    const uint32_t x0 = blockIdx.x * 64, y0 = blockIdx.y * 64;
+    if (x0 >= r.T || y0 >= r.H) return;  // block-uniform
+    const uint32_t tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
+    const float* sp = spec + r.spec_off;
+    const uint32_t y = y0 + tx;
+#pragma unroll 4
+    for (uint32_t k = 0; k < 16; ++k) {
+        const uint32_t xi = ty + 4 * k, x = x0 + xi;
+        float v = 0.0f;
+        if (x < r.T && y < r.H && y >= r.H - bins) {
+            const float db = sp[(uint64_t)x * bins + (r.H - 1 - y)];
+            v = (db - min) / (max - min);
+            v = fmaxf(v, 0.0f);
+            v = fminf(v, 1.0f);
+        }
+        tile[tx][xi] = v;
+    }
+    __syncthreads();
+    float* g = grey + r.grey_off;
+#pragma unroll 4
+    for (uint32_t k = 0; k < 16; ++k) {
+        const uint32_t yi = ty + 4 * k, yy = y0 + yi, x = x0 + tx;
+        if (yy < r.H && x < r.T) g[(uint64_t)yy * r.T + x] = tile[yi][tx];
+    }
 }
 
 __global__ void resize_v_batch_kernel(uint32_t nh, const RenderDesc* d, const float* grey,
@@ -434,7 +459,7 @@ int launch_render_batch(const float* spec, uint32_t bins, float max, float min,
     if (n > 65535) return -2;
     uint32_t ry = 64;  // grid.y: row blocks per image (strided row loop inside)
     if (const char* e = getenv("THESIA_RENDER_RY")) ry = (uint32_t)atoi(e) > 0 ? (uint32_t)atoi(e) : 64;
-    dim3 g1((T_max + 255) / 256, H_max < ry ? (H_max ? H_max : 1) : ry, n);
+    dim3 g1((T_max + 63) / 64, (H_max + 63) / 64, n);
     hipLaunchKernelGGL(spec_to_grey_batch_kernel, g1, dim3(256), 0, s, spec, bins, max, min, d_desc, grey);
     dim3 g2((T_max + 255) / 256, nh < ry ? nh : ry, n);
     hipLaunchKernelGGL(resize_v_batch_kernel, g2, dim3(256), 0, s, nh, d_desc, grey, tmp);
