@@ -96,7 +96,8 @@ def test_c5_mixed_rate_render_pipeline():
 
 @pytest.mark.parametrize("per_track", [False, True])
 @pytest.mark.parametrize("px_per_sec", [73.0, 30.0, 9.0])  # 30: 17-64 taps (LDS weights); 9: > 64 (direct)
-def test_render_batch_ragged_groups(per_track, px_per_sec, monkeypatch):
+@pytest.mark.parametrize("nheight", [90, 400])  # 400: taller images (H->nheight downsampling ratio ~2.5)
+def test_render_batch_ragged_groups(per_track, px_per_sec, nheight, monkeypatch):
     """Several tracks of different lengths per geometry group: the batched render (one launch
     per stage for the whole group, blockIdx.z = track) and the per-track launches produce the
     oracle's bytes for every image (ragged T, nwidth and workspace offsets)."""
@@ -108,12 +109,12 @@ def test_render_batch_ragged_groups(per_track, px_per_sec, monkeypatch):
         n = int(t.pcm.shape[0] * (0.5 + 0.35 * (k // 4))) + 3 * k
         n = max(n, t.n_fft)
         tracks.append(pipeline.Track(t.pcm[:n].copy(), t.sr, t.n_fft))
-    out = pipeline.render_tracks(tracks, px_per_sec=px_per_sec, nheight=90, keep_db=True)
+    out = pipeline.render_tracks(tracks, px_per_sec=px_per_sec, nheight=nheight, keep_db=True)
     gmax, gmin, max_sr = shard.global_db_range(max(r.spec_max for r in out),
                                                min(r.spec_min for r in out),
                                                max(t.sr for t in tracks))
     for t, r in zip(tracks, out):
         up = shard.up_ratio(t.sr, max_sr, freq_scale_mel=False)
         grey = O.spec_to_grey(r.db, up, gmax, gmin)
-        img, _ = O.grey_to_rgb(grey, r.nwidth, 90)
+        img, _ = O.grey_to_rgb(grey, r.nwidth, nheight)
         assert r.rgb.tobytes() == img.tobytes(), (t.sr, t.n_fft, t.pcm.shape)
