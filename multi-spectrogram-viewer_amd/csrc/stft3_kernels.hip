@@ -112,7 +112,8 @@ __device__ __forceinline__ void load_raw_generic(const StftLaunch& a, float* reg
 // bit4 = mel with 4 float4 steps per LDS round trip instead of 8; bit5 = the narrow (stride
 // L + 2, ds_read2_b64) transpose instead of the wide one; bit6 = the previous mel4 (per-round
 // setup reads); bit7 = four mel accumulators; bit8 = ablation: |X|^2 (no v_sqrt); bit9 = the
-// sqrts not batched; bit10 (linear / complex kinds) = the other row-store method (stage_rows).
+// sqrts not batched; bit10 (linear / complex kinds) = the other row-store method (stage_rows);
+// bit12 = no wave-priority phases (s_setprio; previous).
 #ifdef THESIA_MARKS
 #define MARK(x) asm volatile("; MARK " #x)
 #else
@@ -180,6 +181,11 @@ stft3_kernel(StftLaunch a, uint64_t fps) {
     int64_t n = 0;
     for (uint64_t it = 0; it < fps; ++it) {  // wave-uniform trip count
         MARK(top);
+        // wave priority phases (measured): loads / window / FFT at priority 0,
+        // untangle / |X| / mel / stores at 2. With 2 waves per SIMD, the wave in the LDS-latency-
+        // bound chains (bpermute batch, |X| row, mel rounds) then issues first whenever it is
+        // ready and the other wave's FFT (high ILP) fills the gaps: mel-128 5.13 -> 4.67 ms.
+        if constexpr ((VAR & 4096) == 0) __builtin_amdgcn_s_setprio(0);
         const uint64_t g = g0 + it;
         const bool valid = g < g1;
         // opaque per frame: keeps the untangle rotations (from ub) and the window reads (from
@@ -250,6 +256,7 @@ stft3_kernel(StftLaunch a, uint64_t fps) {
         if constexpr ((VAR & 4) == 0) fft2<NC, TwTable4, G3::WIDE && (VAR & 32) == 0>(v, region, j, TwTable4{reinterpret_cast<const float4*>(twtab) + wj, L});
         else pin(v);
         MARK(fft);
+        if constexpr ((VAR & 4096) == 0) __builtin_amdgcn_s_setprio(2);
         if constexpr (OK == 2 && (VAR & 8) != 0) {  // ablation: no untangle / |X| / mel
             pin(v);
         } else if constexpr (OK == 2) {
@@ -370,6 +377,7 @@ static int launch3_k(const StftLaunch& a, hipStream_t stream) {
             case 512: return launch3_k<NC, OK, C, INF, 512>(a, stream);  // unbatched sqrt
             case 258: return launch3_k<NC, OK, C, INF, 258>(a, stream);  // ablation: no sqrt, no mel
             case 1000: return launch3_k<NC, OK, C, INF, 0, 12>(a, stream);  // 3 waves/SIMD
+            case 4096: return launch3_k<NC, OK, C, INF, 4096>(a, stream);  // no priority phases
             default: break;
         }
     }
@@ -379,6 +387,7 @@ static int launch3_k(const StftLaunch& a, hipStream_t stream) {
             case 1024: return launch3_k<NC, OK, C, INF, 1024>(a, stream);  // other row-store method
             case 4: return launch3_k<NC, OK, C, INF, 4>(a, stream);  // ablation: no FFT
             case 1028: return launch3_k<NC, OK, C, INF, 1028>(a, stream);
+            case 4096: return launch3_k<NC, OK, C, INF, 4096>(a, stream);  // no priority phases
             default: break;
         }
     }
