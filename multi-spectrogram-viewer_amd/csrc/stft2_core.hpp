@@ -118,13 +118,16 @@ __device__ __forceinline__ bool load_direct2(const StftLaunch& a, int j, int64_t
 template <int NC>
 constexpr int fft2_stride(bool wide) { return Geo2<NC>::L + (wide ? 4 : 2); }
 
-template <int NC, class TwF, bool WIDE = false>
+// TPRIO > 0: the twiddle reads and the LDS transpose run at wave priority TPRIO, the register
+// DFT stages at 0 (stft3 priority phases).
+template <int NC, class TwF, bool WIDE = false, int TPRIO = 0>
 __device__ __forceinline__ void fft2(float2 (&v)[Geo2<NC>::P], float* region, int j, const TwF& twf) {
     using G = Geo2<NC>;
     constexpr int L = G::L, P = G::P, S = fft2_stride<NC>(WIDE), CPL = G::CPL;
     pin(v);
     dif_fft<P, 1, 0, P>(v);
     pin(v);
+    if constexpr (TPRIO > 0) __builtin_amdgcn_s_setprio(TPRIO);
     if constexpr (TwF::kPairs) {
         // two twiddles per ds_read_b128: all reads of the table issued before the products
         float4 tw[P / 2];
@@ -179,6 +182,7 @@ __device__ __forceinline__ void fft2(float2 (&v)[Geo2<NC>::P], float* region, in
     }
     wave_lds_sync();
     pin(v);
+    if constexpr (TPRIO > 0) __builtin_amdgcn_s_setprio(0);
     static_for<0, CPL>([&](auto cc) {
         constexpr int c = decltype(cc)::value;
         dif_fft<L, 1, c * L, P>(v);

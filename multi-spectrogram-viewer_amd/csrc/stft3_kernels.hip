@@ -113,7 +113,8 @@ __device__ __forceinline__ void load_raw_generic(const StftLaunch& a, float* reg
 // L + 2, ds_read2_b64) transpose instead of the wide one; bit6 = the previous mel4 (per-round
 // setup reads); bit7 = four mel accumulators; bit8 = ablation: |X|^2 (no v_sqrt); bit9 = the
 // sqrts not batched; bit10 (linear / complex kinds) = the other row-store method (stage_rows);
-// bit12 = no wave-priority phases (s_setprio; previous).
+// bit12 = no wave-priority phases (s_setprio; previous); bit13 / bit14 = the FFT's twiddle reads
+// and transposes at priority 1 / 2.
 #ifdef THESIA_MARKS
 #define MARK(x) asm volatile("; MARK " #x)
 #else
@@ -253,7 +254,7 @@ stft3_kernel(StftLaunch a, uint64_t fps) {
             pre_ok = nxt;
         }
         MARK(prefetched);
-        if constexpr ((VAR & 4) == 0) fft2<NC, TwTable4, G3::WIDE && (VAR & 32) == 0>(v, region, j, TwTable4{reinterpret_cast<const float4*>(twtab) + wj, L});
+        if constexpr ((VAR & 4) == 0) fft2<NC, TwTable4, G3::WIDE && (VAR & 32) == 0, (VAR & 8192) ? 1 : (VAR & 16384) ? 2 : 0>(v, region, j, TwTable4{reinterpret_cast<const float4*>(twtab) + wj, L});
         else pin(v);
         MARK(fft);
         if constexpr ((VAR & 4096) == 0) __builtin_amdgcn_s_setprio(2);
@@ -378,6 +379,8 @@ static int launch3_k(const StftLaunch& a, hipStream_t stream) {
             case 258: return launch3_k<NC, OK, C, INF, 258>(a, stream);  // ablation: no sqrt, no mel
             case 1000: return launch3_k<NC, OK, C, INF, 0, 12>(a, stream);  // 3 waves/SIMD
             case 4096: return launch3_k<NC, OK, C, INF, 4096>(a, stream);  // no priority phases
+            case 8192: return launch3_k<NC, OK, C, INF, 8192>(a, stream);  // transposes at prio 1
+            case 16384: return launch3_k<NC, OK, C, INF, 16384>(a, stream);  // transposes at prio 2
             default: break;
         }
     }
