@@ -114,7 +114,7 @@ __device__ __forceinline__ void load_raw_generic(const StftLaunch& a, float* reg
 // setup reads); bit7 = four mel accumulators; bit8 = ablation: |X|^2 (no v_sqrt); bit9 = the
 // sqrts not batched; bit10 (linear / complex kinds) = the other row-store method (stage_rows);
 // bit12 = no wave-priority phases (s_setprio; previous); bit13 / bit14 = the FFT's twiddle reads
-// and transposes at priority 1 / 2.
+// and transposes at priority 1 / 2; bit15 = the mel rounds at priority 3.
 #ifdef THESIA_MARKS
 #define MARK(x) asm volatile("; MARK " #x)
 #else
@@ -293,6 +293,7 @@ stft3_kernel(StftLaunch a, uint64_t fps) {
             }
             wave_lds_sync();
             MARK(untangled);
+            if constexpr ((VAR & 32768) != 0) __builtin_amdgcn_s_setprio(3);  // experiment: mel at 3
             // U = 8 float4 steps per LDS round trip (the FFT's registers are free by now)
             if constexpr ((VAR & 2) == 0 && (VAR & 64) == 0)
                 mel4<NC, (VAR & 16) ? 4 : 8, (VAR & 128) ? 4 : 1>(a, region, mel_lds, rd_lds, k0_lds, j, g, valid);
@@ -381,6 +382,8 @@ static int launch3_k(const StftLaunch& a, hipStream_t stream) {
             case 4096: return launch3_k<NC, OK, C, INF, 4096>(a, stream);  // no priority phases
             case 8192: return launch3_k<NC, OK, C, INF, 8192>(a, stream);  // transposes at prio 1
             case 16384: return launch3_k<NC, OK, C, INF, 16384>(a, stream);  // transposes at prio 2
+            case 32768: return launch3_k<NC, OK, C, INF, 32768>(a, stream);  // mel rounds at prio 3
+            case 40960: return launch3_k<NC, OK, C, INF, 40960>(a, stream);  // + transposes at 1
             default: break;
         }
     }
