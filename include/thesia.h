@@ -49,6 +49,11 @@ int thesia_device_malloc(void** ptr, size_t bytes);
 int thesia_device_free(void* ptr);
 int thesia_memcpy_h2d(void* dst_device, const void* src_host, size_t bytes);
 int thesia_memcpy_d2h(void* dst_host, const void* src_device, size_t bytes);
+/* Page-lock (pin) a caller-owned host range so device-to-host copies into it run at DMA rate;
+ * for the RGB image readback that get_spec_image implies (lib.rs:294-298 hands the bytes to JS).
+ * The range stays the caller's; unregister it before freeing it. */
+int thesia_host_register(void* host, size_t bytes);
+int thesia_host_unregister(void* host);
 int thesia_memset_device(void* dst_device, int value, size_t bytes);
 int thesia_device_synchronize(void);
 /* Device name / CU count of the current device (for reports). */

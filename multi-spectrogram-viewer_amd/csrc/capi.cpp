@@ -74,6 +74,15 @@ int thesia_memcpy_d2h(void* dst, const void* src, size_t bytes) {
     THESIA_HIP(hipMemcpy(dst, src, bytes, hipMemcpyDeviceToHost));
     return THESIA_OK;
 }
+int thesia_host_register(void* host, size_t bytes) {
+    if (!host || !bytes) return set_error(THESIA_ERR_INVALID_ARG, "null / empty host range");
+    THESIA_HIP(hipHostRegister(host, bytes, hipHostRegisterDefault));
+    return THESIA_OK;
+}
+int thesia_host_unregister(void* host) {
+    THESIA_HIP(hipHostUnregister(host));
+    return THESIA_OK;
+}
 int thesia_memset_device(void* dst, int value, size_t bytes) {
     THESIA_HIP(hipMemset(dst, value, bytes));
     return THESIA_OK;

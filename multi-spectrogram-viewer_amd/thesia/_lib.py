@@ -51,6 +51,8 @@ _SIGS = {
     "thesia_device_free": (_i, [_vp]),
     "thesia_memcpy_h2d": (_i, [_vp, _vp, _sz]),
     "thesia_memcpy_d2h": (_i, [_vp, _vp, _sz]),
+    "thesia_host_register": (_i, [_vp, _sz]),
+    "thesia_host_unregister": (_i, [_vp]),
     "thesia_memset_device": (_i, [_vp, _i, _sz]),
     "thesia_device_synchronize": (_i, []),
     "thesia_device_info": (_i, [C.c_char_p, _sz, C.POINTER(_i)]),

@@ -59,8 +59,13 @@ class RenderPipeline:
     runs the global-range exchange and the device display path for every track."""
 
     def __init__(self, tracks: Sequence[Track], px_per_sec: float = 100.0, nheight: int = 500,
-                 db_range: float = 120.0):
+                 db_range: float = 120.0, pinned_output: bool = False):
+        """pinned_output: read the RGB images back into one page-locked host buffer per
+        geometry group (DMA-rate copies); the returned images are then views that the next
+        render() overwrites. Default: fresh pageable arrays per render()."""
         self.tracks = list(tracks)
+        self.pinned_output = pinned_output
+        self._pinned = {}  # group -> registered host array
         self.px_per_sec, self.nheight, self.db_range = px_per_sec, nheight, db_range
         groups: "OrderedDict[tuple, List[int]]" = OrderedDict()
         for i, t in enumerate(self.tracks):
@@ -143,7 +148,12 @@ class RenderPipeline:
                 dout.ptr, row0.ctypes.data_as(_u64p), plan.row_bins, n, up.ctypes.data_as(_fp),
                 nw.ctypes.data_as(C.POINTER(C.c_uint32)), self.nheight, gmax, gmin, self._rgb.ptr,
                 off.ctypes.data_as(_u64p)))
-            rgb_all = self._rgb.read(np.uint8, total) if want_rgb else None
+            if want_rgb and self.pinned_output:
+                rgb_all = self._pinned_host(g, total)
+                check(lib.thesia_memcpy_d2h(rgb_all.ctypes.data_as(C.c_void_p), self._rgb.ptr, total))
+                rgb_all = rgb_all[:total]
+            else:
+                rgb_all = self._rgb.read(np.uint8, total) if want_rgb else None
             for k, i in enumerate(idx):
                 img = rgb_all[int(off[k]):int(off[k]) + int(sizes[k])] if want_rgb else None
                 db = None
@@ -153,7 +163,20 @@ class RenderPipeline:
                 out[i] = Rendered(db, img, int(nw[k]), *ranges[i])
         return out
 
+    def _pinned_host(self, g: int, total: int) -> np.ndarray:
+        buf = self._pinned.get(g)
+        if buf is None or buf.nbytes < total:
+            if buf is not None:
+                check(lib.thesia_host_unregister(buf.ctypes.data_as(C.c_void_p)))
+            buf = np.empty(max(total, 1), np.uint8)
+            check(lib.thesia_host_register(buf.ctypes.data_as(C.c_void_p), buf.nbytes))
+            self._pinned[g] = buf
+        return buf
+
     def close(self):
+        for buf in self._pinned.values():
+            lib.thesia_host_unregister(buf.ctypes.data_as(C.c_void_p))
+        self._pinned = {}
         for plan, din, dout, b in self.groups[::-1]:
             b.close()
             dout.close()

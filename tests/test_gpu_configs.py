@@ -118,3 +118,18 @@ def test_render_batch_ragged_groups(per_track, px_per_sec, nheight, monkeypatch)
         grey = O.spec_to_grey(r.db, up, gmax, gmin)
         img, _ = O.grey_to_rgb(grey, r.nwidth, nheight)
         assert r.rgb.tobytes() == img.tobytes(), (t.sr, t.n_fft, t.pcm.shape)
+
+
+def test_render_pinned_readback_matches_pageable():
+    """RenderPipeline(pinned_output=True) reads the RGB bytes into page-locked host buffers
+    (thesia_host_register); the bytes equal the pageable readback's."""
+    tracks = pipeline.c5_tracks(6, seconds=0.5)
+    outs = []
+    for pinned in (False, True):
+        p = pipeline.RenderPipeline(tracks, px_per_sec=50.0, nheight=64, pinned_output=pinned)
+        try:
+            p.run_spectrograms()
+            outs.append([r.rgb.tobytes() for r in p.render()])
+        finally:
+            p.close()
+    assert outs[0] == outs[1]
