@@ -23,10 +23,14 @@
 // product, downmix and dB epilogue follow the reference's evaluation order.
 #include "stft2_core.hpp"
 
+#include <cstdlib>
+
 namespace thesia {
 
-// OK: 0 complex, 1 linear kinds (|X|, |X|^2, dB), 2 mel kinds.
-template <int NC, int OK, int INF>
+// OK: 0 complex, 1 linear kinds (|X|, |X|^2, dB), 2 mel kinds. PR: wave-priority phases as in
+// stft3 (loads / window / FFT at 0, untangle / |X| / mel / stores at 2); PR = 0 (experiment
+// variant 4096) without.
+template <int NC, int OK, int INF, int PR = 1>
 __global__ void __launch_bounds__(kBlock, 4)
 stft2_kernel(StftLaunch a, uint64_t tiles_per_block) {
     using G = Geo2<NC>;
@@ -58,6 +62,7 @@ stft2_kernel(StftLaunch a, uint64_t tiles_per_block) {
     for (uint64_t tile = t_begin; tile < t_end; ++tile) {
         const uint64_t g = tile * TILE + (uint64_t)(wave * FPW + slot);
         const bool valid = g < total;
+        if constexpr (PR != 0) __builtin_amdgcn_s_setprio(0);
         // opaque per pass: keeps the 2*(L/2)*CPL untangle rotations derived from ub inside the
         // loop instead of hoisted (and spilled) as loop invariants
 #pragma unroll
@@ -81,6 +86,7 @@ stft2_kernel(StftLaunch a, uint64_t tiles_per_block) {
             load_tw2<NC>(a, j, tw.b, tw.a);
             fft2<NC>(v, region, j, tw);
         }
+        if constexpr (PR != 0) __builtin_amdgcn_s_setprio(2);
         if constexpr (OK == 2) {
             untangle2<NC>(v, j, partner, ub, [&](int k, float xr, float xi) {
                 region[k] = __builtin_amdgcn_sqrtf(xr * xr + xi * xi);  // |X| (lib.rs:124)
@@ -125,10 +131,16 @@ stft2_kernel(StftLaunch a, uint64_t tiles_per_block) {
 // --------------------------------------------------------------------------------------
 // host-side dispatch
 // --------------------------------------------------------------------------------------
-template <int NC, int OK, int INF>
+template <int NC, int OK, int INF, int PR = 1>
 static int launch2_k(const StftLaunch& a, hipStream_t stream) {
+#ifdef THESIA_EXPERIMENTS
+    if constexpr (PR == 1) {
+        const char* e = getenv("THESIA_STFT_VARIANT");
+        if (e && atoi(e) == 4096) return launch2_k<NC, OK, INF, 0>(a, stream);
+    }
+#endif
     constexpr int lds = Geo2<NC>::LDS_BYTES;
-    auto kern = stft2_kernel<NC, OK, INF>;
+    auto kern = stft2_kernel<NC, OK, INF, PR>;
     static bool attr_set = false;
     if (!attr_set) {
         if (hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
