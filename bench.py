@@ -340,7 +340,11 @@ def main():
             "unit": "GB/s",
             "frac": achieved / HBM_PEAK_GBS,
             "traffic": traffic_from_profile(wkey),
-            "kernel": "thesia::stft3_kernel (streaming: downmix+frame+window+rFFT+|X|+mel+dB, one launch)",
+            "kernel": {1: "thesia::stft_kernel (general)", 2: "thesia::stft2_kernel (general, 4 waves/SIMD)",
+                       3: "thesia::stft3_kernel (streaming)"}.get(batch.kernel, "?")
+                      + ": downmix+frame+window+rFFT+" + {"mel_db": "|X|+mel+dB", "amp_db": "|X|+dB",
+                                                           "power_db": "|X|^2+dB", "complex": "complex out"}[args.output]
+                      + ", one launch",
             "kernel_ms": kms,
             "algorithmic_bytes_per_launch": abytes,
         }
