@@ -114,7 +114,8 @@ __device__ __forceinline__ void load_raw_generic(const StftLaunch& a, float* reg
 // setup reads); bit7 = four mel accumulators; bit8 = ablation: |X|^2 (no v_sqrt); bit9 = the
 // sqrts not batched; bit10 (linear / complex kinds) = the other row-store method (stage_rows);
 // bit12 = no wave-priority phases (s_setprio; previous); bit13 / bit14 = the FFT's twiddle reads
-// and transposes at priority 1 / 2; bit15 = the mel rounds at priority 3.
+// and transposes at priority 1 / 2; bit15 = the mel rounds at priority 3; bit16 = the prefetch
+// loads issued at priority 3.
 #ifdef THESIA_MARKS
 #define MARK(x) asm volatile("; MARK " #x)
 #else
@@ -246,12 +247,14 @@ stft3_kernel(StftLaunch a, uint64_t fps) {
             const bool nxt = valid && g + 1 < g1 && g + 1 < g_end && nstart + 2 * NC <= n &&
                              nstart + 2 * L * (P - SH) >= 0 &&
                              ((base + (uint64_t)(nstart + 2 * L * (P - SH)) * C) % (2 * C)) == 0;
+            if constexpr ((VAR & 65536) != 0) __builtin_amdgcn_s_setprio(3);  // experiment
             if (nxt) {
                 const CT* src = reinterpret_cast<const CT*>(in + base + (uint64_t)(nstart + 2 * L * (P - SH)) * C) + j;
 #pragma unroll
                 for (int q = 0; q < SH; ++q) pre[q] = src[L * q];
             }
             pre_ok = nxt;
+            if constexpr ((VAR & 65536) != 0) __builtin_amdgcn_s_setprio(0);
         }
         MARK(prefetched);
         if constexpr ((VAR & 4) == 0) fft2<NC, TwTable4, G3::WIDE && (VAR & 32) == 0, (VAR & 8192) ? 1 : (VAR & 16384) ? 2 : 0>(v, region, j, TwTable4{reinterpret_cast<const float4*>(twtab) + wj, L});
@@ -383,6 +386,7 @@ static int launch3_k(const StftLaunch& a, hipStream_t stream) {
             case 8192: return launch3_k<NC, OK, C, INF, 8192>(a, stream);  // transposes at prio 1
             case 16384: return launch3_k<NC, OK, C, INF, 16384>(a, stream);  // transposes at prio 2
             case 32768: return launch3_k<NC, OK, C, INF, 32768>(a, stream);  // mel rounds at prio 3
+            case 65536: return launch3_k<NC, OK, C, INF, 65536>(a, stream);  // prefetch issue at prio 3
             case 40960: return launch3_k<NC, OK, C, INF, 40960>(a, stream);  // + transposes at 1
             default: break;
         }
