@@ -166,6 +166,21 @@ int thesia_batch_kernel_info(const thesia_batch* batch, int* lds_bytes, int* til
  * 3 stft3_kernel (streaming; win = n_fft, hop = n_fft/4). */
 int thesia_batch_kernel(const thesia_batch* batch, int* kernel);
 
+/* Named alternatives of a batch (none changes what is computed, only how; all results stay
+ * within the parity contract). Not part of the reference surface. */
+typedef enum {
+    /* 0 = automatic (streaming kernel where its geometry allows), 1 / 2 / 3 = force that
+     * kernel (THESIA_ERR_UNSUPPORTED if it cannot run the geometry) */
+    THESIA_BATCH_OPT_KERNEL = 1,
+    /* at most this many workgroups per launch (0 = one full occupancy wave of the device);
+     * small values make every frame stream walk many frames */
+    THESIA_BATCH_OPT_MAX_BLOCKS = 2,
+    /* 1 = the other output-row store method of the streaming kernel (LDS-staged 16-byte stores
+     * for complex rows / lane-wise stores for linear rows; n_fft 2048 stereo f32 only) */
+    THESIA_BATCH_OPT_ROW_STORE = 3
+} thesia_batch_option;
+int thesia_batch_set_option(thesia_batch* batch, int option, int64_t value);
+
 /* Deterministic synthetic PCM (int16-quantised chirp + noise) written on the device, and
  * its bit-identical host twin. format: thesia_input_format. Layout [track][sample][ch]. */
 int thesia_synth_pcm_device(void* d_out, int format, uint32_t channels, uint64_t n_tracks,
@@ -207,6 +222,10 @@ int thesia_grey_to_rgb_device(const float* d_grey, uint32_t width, uint32_t heig
  * [nheight, nwidth[i], 3] lands at d_rgb + rgb_off[i] (host arrays of n entries). */
 int thesia_minmax_segments_device(const float* d_spec, const uint64_t* row0, size_t bins,
                                   size_t n, float* max, float* min, int* has_nan);
+/* Process-wide choice of the batched display path's launch structure: 0 = every track of a
+ * call in one launch per stage (default), 1 = per-track launches (the reference's one image
+ * at a time structure; a cross-check, byte-identical). */
+int thesia_set_render_path(int path);
 int thesia_render_rgb_batch_device(const float* d_spec, const uint64_t* row0, size_t bins,
                                    size_t n, const float* up_ratio, const uint32_t* nwidth,
                                    uint32_t nheight, float max, float min, uint8_t* d_rgb,

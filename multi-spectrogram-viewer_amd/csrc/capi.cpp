@@ -287,6 +287,15 @@ int thesia_batch_kernel(const thesia_batch* batch, int* kernel) {
     return THESIA_OK;
 }
 
+int thesia_batch_set_option(thesia_batch* batch, int option, int64_t value) {
+    GUARD_BEGIN
+    if (!batch) return set_error(THESIA_ERR_INVALID_ARG, "null batch");
+    return batch_set_option(reinterpret_cast<Batch*>(batch), option, value);
+    GUARD_END
+}
+
+int thesia_set_render_path(int path) { return set_render_path(path); }
+
 int thesia_synth_pcm_device(void* d_out, int format, uint32_t channels, uint64_t n_tracks,
                             uint64_t n_samples, uint32_t sr, uint64_t seed) {
     GUARD_BEGIN

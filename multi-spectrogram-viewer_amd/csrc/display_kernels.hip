@@ -458,14 +458,19 @@ int launch_render_batch(const float* spec, uint32_t bins, float max, float min,
     if (n == 0 || nh == 0) return 0;
     if (n > 65535) return -2;
     uint32_t ry = 64;  // grid.y: row blocks per image (strided row loop inside)
-    if (const char* e = getenv("THESIA_RENDER_RY")) ry = (uint32_t)atoi(e) > 0 ? (uint32_t)atoi(e) : 64;
+    bool ry_set = false;
+    int abl = 0;
+#ifdef THESIA_EXPERIMENTS
+    if (const char* e = getenv("THESIA_RENDER_RY")) { ry = (uint32_t)atoi(e) > 0 ? (uint32_t)atoi(e) : 64; ry_set = true; }
+    if (const char* e = getenv("THESIA_RENDER_ABL")) abl = atoi(e);  // ablations (timing only)
+#endif
     dim3 g1((T_max + 63) / 64, (H_max + 63) / 64, n);
     hipLaunchKernelGGL(spec_to_grey_batch_kernel, g1, dim3(256), 0, s, spec, bins, max, min, d_desc, grey);
     dim3 g2((T_max + 255) / 256, nh < ry ? nh : ry, n);
     hipLaunchKernelGGL(resize_v_batch_kernel, g2, dim3(256), 0, s, nh, d_desc, grey, tmp);
     // the horizontal pass prefers fewer, longer row walks (one LDS weight / tap setup per block
     // amortised over more rows): 16 row blocks per image measured 3.96 vs 4.46 ms at 64
-    const uint32_t ry_h = getenv("THESIA_RENDER_RY") ? ry : 16;
+    const uint32_t ry_h = ry_set ? ry : 16;
     dim3 g3((nw_max + 255) / 256, nh < ry_h ? nh : ry_h, n);
     // LDS: the staged span (+ kHTaps zeros), tap-major weights for > kHTaps taps, RGB segment,
     // colormap; beyond 64 KiB the weights (then the span) stay in HBM (direct path)
@@ -474,8 +479,6 @@ int launch_render_batch(const float* spec, uint32_t bins, float max, float min,
     auto lds = [&]() { return (span + kHTaps + taps * 256) * 4 + 256 * 3 + 32; };
     if (lds() > 65536) taps = 0;
     if (lds() > 65536) span = 4096;
-    int abl = 0;
-    if (const char* e = getenv("THESIA_RENDER_ABL")) abl = atoi(e);
     hipLaunchKernelGGL(resize_h_rgb_batch_kernel, g3, dim3(256), lds(), s, nh, d_desc, tmp, cmap, rgb,
                        taps, span, abl);
     return hipGetLastError() == hipSuccess ? 0 : -1;

@@ -236,90 +236,6 @@ static int build_mel4(Plan* p) {
     return rc;
 }
 
-// stft4_kernel's mel layout (stft4_kernels.hip mel5): filters are dealt, longest first, to
-// the least-loaded of 64 lanes, at most two per lane per round (longest paired with
-// shortest); a lane's filter A runs sA float4 steps from its band start rounded down to 4,
-// filter B the rest of the round (its start moved left so the round stays inside the row).
-// Positions are those of the kernel's skewed |X| row: bin k at k + 8 (k >> 8), the 8 floats
-// after every 256 bins carry weight 0.
-static long skew4(long k) { return k + ((k >> 8) << 3); }
-static int build_mel5(Plan* p) {
-    const long F = (long)p->NC + 1, F4 = (F + 3) / 4 * 4, XROW = skew4(F4 - 1) + 1;
-    const size_t M = p->n_mels;
-    std::vector<long> lo(M, 0), len(M, 0);
-    for (size_t m = 0; m < M; ++m) {
-        long l0 = -1, h0 = -1;
-        for (long k = 0; k < F; ++k)
-            if (p->mel_fb[(size_t)k * M + m] != 0.0f) {
-                if (l0 < 0) l0 = k;
-                h0 = k + 1;
-            }
-        if (l0 >= 0) {
-            lo[m] = skew4(l0 / 4 * 4);
-            len[m] = (skew4(h0 - 1) + 1 - lo[m] + 3) / 4;
-        }
-    }
-    auto weight = [&](long pos, long m) {  // the filter's weight at a skewed row position
-        const long blk = pos / 264, r = pos % 264;
-        const long k = 256 * blk + r;
-        return (r >= 256 || k >= F) ? 0.0f : p->mel_fb[(size_t)k * M + m];
-    };
-    std::vector<size_t> order(M);
-    for (size_t m = 0; m < M; ++m) order[m] = m;
-    std::stable_sort(order.begin(), order.end(), [&](size_t x, size_t y) { return len[x] > len[y]; });
-    const size_t U = (M + 127) / 128;
-    std::vector<int2> rounds(U);
-    std::vector<int> meta(U * 64 * 4, 0);
-    std::vector<float> wt;
-    size_t rows = 0;
-    for (size_t u = 0; u < U; ++u) {
-        std::vector<size_t> grp;  // round-robin over the sorted filters: similar rounds
-        for (size_t i = u; i < M; i += U) grp.push_back(order[i]);
-        std::vector<std::vector<size_t>> lanes(64);
-        std::vector<long> load(64, 0);
-        for (size_t m : grp) {
-            int best = -1;
-            for (int l = 0; l < 64; ++l)
-                if (lanes[l].size() < 2 && (best < 0 || load[l] < load[best])) best = l;
-            lanes[best].push_back(m);
-            load[best] += len[m];
-        }
-        long S = 1;
-        for (int l = 0; l < 64; ++l) S = std::max(S, load[l]);
-        if (4 * S > XROW) return set_error(THESIA_ERR_UNSUPPORTED, "mel filters too wide for one round");
-        rounds[u] = int2{(int)rows, (int)S};
-        wt.resize((rows + (size_t)S) * 64 * 4, 0.0f);
-        for (int l = 0; l < 64; ++l) {
-            // one filter: it is B (sA = 0); two: the longer first
-            const bool two = lanes[l].size() == 2;
-            const long mA = two ? (long)lanes[l][0] : -1;
-            const long mB = lanes[l].empty() ? -1 : (long)lanes[l][two ? 1 : 0];
-            const long sA = two ? len[mA] : 0;
-            const long kA = two ? lo[mA] : 0;
-            const long kB = std::min(mB >= 0 ? lo[mB] : XROW, (XROW - 4 * (S - sA)) / 4 * 4);
-            int* mt = &meta[(u * 64 + l) * 4];
-            mt[0] = (int)kA;
-            mt[1] = (int)(kB - 4 * sA);
-            mt[2] = (int)sA;
-            mt[3] = (int)((uint32_t)(mA >= 0 ? mA : 0xffff) | ((uint32_t)(mB >= 0 ? mB : 0xffff) << 16));
-            for (long s = 0; s < S; ++s) {
-                const long m = s < sA ? mA : mB;
-                if (m < 0) continue;
-                const long k0 = s < sA ? kA + 4 * s : kB + 4 * (s - sA);
-                for (int e = 0; e < 4; ++e) wt[((rows + (size_t)s) * 64 + l) * 4 + e] = weight(k0 + e, m);
-            }
-        }
-        rows += (size_t)S;
-    }
-    if (M >= 0xffff) return set_error(THESIA_ERR_UNSUPPORTED, "too many mel filters");
-    int rc = p->mel5_round.upload(rounds.data(), std::max<size_t>(U, 1) * sizeof(int2));
-    if (!rc) rc = p->mel5_meta.upload(meta.data(), std::max<size_t>(meta.size(), 4) * sizeof(int));
-    if (!rc) rc = p->mel5_wt.upload(wt.data(), std::max<size_t>(wt.size(), 4) * sizeof(float));
-    p->mel5_rounds = (int)U;
-    p->mel5_rows = rows;
-    return rc;
-}
-
 int plan_create(const thesia_plan_desc& d, Plan** out) {
     *out = nullptr;
     if (!is_pow2(d.n_fft) || d.n_fft < 2 || d.n_fft > 4096)
@@ -388,25 +304,6 @@ int plan_create(const thesia_plan_desc& d, Plan** out) {
         }
         if (tw3.empty()) tw3.assign(2, 0.0f);
     }
-    // stft4's stage-A twiddles [k1][lane] = W_1024^{lane*k1} and stage-B [la][kb] = W_64^{la*kb}
-    // (= W_1024^{16*la*kb}; rows padded to 17), the same f64-rounded values
-    std::vector<float> tw4a(2, 0.0f), tw4b(2, 0.0f);
-    if (p->NC == 1024) {
-        tw4a.assign(2 * 16 * 64, 0.0f);
-        for (size_t k1 = 0; k1 < 16; ++k1)
-            for (size_t l = 0; l < 64; ++l) {
-                const size_t e = (l * k1) % 1024;
-                tw4a[2 * (k1 * 64 + l)] = tw[2 * e];
-                tw4a[2 * (k1 * 64 + l) + 1] = tw[2 * e + 1];
-            }
-        tw4b.assign(2 * 4 * 17, 0.0f);
-        for (size_t la = 0; la < 4; ++la)
-            for (size_t kb = 0; kb < 16; ++kb) {
-                const size_t e = (16 * la * kb) % 1024;
-                tw4b[2 * (la * 17 + kb)] = tw[2 * e];
-                tw4b[2 * (la * 17 + kb) + 1] = tw[2 * e + 1];
-            }
-    }
     std::vector<float> sc = rfft_sin_cos(d.n_fft);
     const bool power = d.output == THESIA_OUT_POWER || d.output == THESIA_OUT_POWER_DB;
     p->log_amin = power ? log10f(1e-36f) : log10f(1e-18f);  // decibel.rs:7-8, :43
@@ -414,8 +311,6 @@ int plan_create(const thesia_plan_desc& d, Plan** out) {
     if (!rc) rc = p->tw.upload(tw.data(), tw.size() * sizeof(float));
     if (!rc) rc = p->tw2.upload(tw2.data(), tw2.size() * sizeof(float));
     if (!rc) rc = p->tw3.upload(tw3.data(), tw3.size() * sizeof(float));
-    if (!rc) rc = p->tw4a.upload(tw4a.data(), tw4a.size() * sizeof(float));
-    if (!rc) rc = p->tw4b.upload(tw4b.data(), tw4b.size() * sizeof(float));
     if (!rc) rc = p->sincos.upload(sc.data(), sc.size() * sizeof(float));
     if (!rc && (d.output == THESIA_OUT_MEL || d.output == THESIA_OUT_MEL_AMP_DB)) {
         const size_t F = p->NC + 1;
@@ -433,11 +328,9 @@ int plan_create(const thesia_plan_desc& d, Plan** out) {
         }
         if (!rc) rc = build_mel(p);
         if (!rc) rc = build_mel4(p);
-        if (!rc && p->NC == 1024) rc = build_mel5(p);
     }
     if (!rc) {
-        const char* v1 = getenv("THESIA_STFT_V1");  // experiment: force the general kernel
-        p->use_v2 = stft2_supports((int)d.n_fft) && !(v1 && atoi(v1) != 0);
+        p->use_v2 = stft2_supports((int)d.n_fft);
         if (p->use_v2) stft2_kernel_info((int)d.n_fft, &p->lds_bytes, &p->tile_frames, nullptr);
         else stft_kernel_info((int)d.n_fft, &p->lds_bytes, &p->tile_frames, nullptr);
     }
@@ -525,36 +418,13 @@ int batch_create(Plan* plan, const thesia_batch_desc& d, Batch** out) {
     L.mel4_round = plan->mel4_round.as<int2>();
     L.mel4_k0 = plan->mel4_k0.as<int>();
     L.mel4_wt = plan->mel4_wt.as<float4>();
-    if (plan->NC == 1024) {
-        L.tw4a = plan->tw4a.as<float2>();
-        L.tw4b = plan->tw4b.as<float2>();
-    }
-    L.mel5_rounds = plan->mel5_rounds;
-    L.mel5_rows = (int)plan->mel5_rows;
-    L.mel5_round = plan->mel5_round.as<int2>();
-    L.mel5_meta = plan->mel5_meta.as<int4>();
-    L.mel5_wt = plan->mel5_wt.as<float4>();
     L.out = d.d_output;
-    // THESIA_GRID=n caps the launch at n blocks (tests: long frame streams on small batches)
-    if (const char* e = getenv("THESIA_GRID")) L.grid = std::max(0, atoi(e));
     // kernel choice: the streaming kernel for its geometry, else the 4-waves/SIMD kernel for
-    // its sizes, else the general one. THESIA_STFT_KERNEL=1|2|3|4 forces one (experiments;
-    // 4 = the one-frame-per-wave streaming kernel for n_fft 2048, measured 15 % slower than
-    // stft3 on the C4 workload)
-    const bool mel = plan->out_kind == OUT_MEL || plan->out_kind == OUT_MEL_AMP_DB;
-    const bool k3 = plan->use_v2 && stft3_supports((int)plan->n_fft, (int)plan->win, (int)plan->hop,
-                                                   d.input_format, (int)d.channels);
-    const bool k4 = plan->use_v2 && stft4_supports((int)plan->n_fft, (int)plan->win, (int)plan->hop,
-                                                   d.input_format, (int)d.channels) &&
-                    (!mel || plan->mel5_rounds > 0);
-    b->kernel = plan->use_v2 ? 2 : 1;
-    if (k3) b->kernel = 3;
-    if (const char* e = getenv("THESIA_STFT_KERNEL")) {
-        const int k = atoi(e);
-        if (k == 1 || (k == 2 && stft2_supports((int)plan->n_fft))) b->kernel = k;
-        if (k == 3 && k3) b->kernel = 3;
-        if (k == 4 && k4 && stft4_lds_bytes(L, mel) <= 163840) b->kernel = 4;
-    }
+    // its sizes, else the general one (thesia_batch_set_option can force another one)
+    b->k3_ok = plan->use_v2 && stft3_supports((int)plan->n_fft, (int)plan->win, (int)plan->hop,
+                                              d.input_format, (int)d.channels) &&
+               stft3_lds_bytes(L) <= 163840;  // the mel weights must fit LDS (else stft2)
+    b->kernel = b->k3_ok ? 3 : plan->use_v2 ? 2 : 1;
     if (hipEventCreate(&b->ev0) != hipSuccess || hipEventCreate(&b->ev1) != hipSuccess) {
         delete b;
         return set_error(THESIA_ERR_DEVICE, "hipEventCreate failed");
@@ -563,11 +433,33 @@ int batch_create(Plan* plan, const thesia_batch_desc& d, Batch** out) {
     return THESIA_OK;
 }
 
+int batch_set_option(Batch* b, int option, int64_t value) {
+    switch (option) {
+        case THESIA_BATCH_OPT_KERNEL:
+            if (value == 0) b->kernel = b->k3_ok ? 3 : b->plan->use_v2 ? 2 : 1;
+            else if (value == 1) b->kernel = 1;
+            else if (value == 2 && stft2_supports((int)b->plan->n_fft)) b->kernel = 2;
+            else if (value == 3 && b->k3_ok) b->kernel = 3;
+            else return set_error(THESIA_ERR_UNSUPPORTED, "kernel " + std::to_string(value) +
+                                                             " does not run this batch's geometry");
+            return THESIA_OK;
+        case THESIA_BATCH_OPT_MAX_BLOCKS:
+            if (value < 0 || value > (1 << 30)) return set_error(THESIA_ERR_INVALID_ARG, "max_blocks out of range");
+            b->launch.grid = (int)value;
+            return THESIA_OK;
+        case THESIA_BATCH_OPT_ROW_STORE:
+            if (value < 0 || value > 1) return set_error(THESIA_ERR_INVALID_ARG, "row_store must be 0 or 1");
+            b->launch.row_alt = (int)value;
+            return THESIA_OK;
+        default:
+            return set_error(THESIA_ERR_INVALID_ARG, "unknown batch option");
+    }
+}
+
 int batch_run(Batch* b, hipStream_t s) {
     if (!s) s = default_stream();
     int rc = -2;
-    if (b->kernel == 4) rc = launch_stft4(b->launch, s);
-    if (rc == -2 && b->kernel >= 3) rc = launch_stft3(b->launch, s);
+    if (b->kernel >= 3) rc = launch_stft3(b->launch, s);
     if (rc == -2 && b->kernel >= 2) rc = launch_stft2(b->launch, s);
     if (rc == -2) rc = launch_stft(b->launch, s);
     if (rc == -2) return set_error(THESIA_ERR_UNSUPPORTED, "unsupported n_fft");
@@ -607,6 +499,14 @@ int minmax_device(const float* d_x, uint64_t n, float* mx, float* mn, bool* nan,
     *mx = a;
     *mn = b;
     *nan = hf != 0;
+    return THESIA_OK;
+}
+
+static int g_render_path = 0;  // thesia_set_render_path
+int render_path() { return __atomic_load_n(&g_render_path, __ATOMIC_RELAXED); }
+int set_render_path(int path) {
+    if (path != 0 && path != 1) return set_error(THESIA_ERR_INVALID_ARG, "render path must be 0 or 1");
+    __atomic_store_n(&g_render_path, path, __ATOMIC_RELAXED);
     return THESIA_OK;
 }
 
@@ -751,7 +651,7 @@ int render_rgb_batch_device(const float* d_spec, const uint64_t* row0, size_t bi
         }
         cmap_ptr = cm.as<uint8_t>();
     }
-    if (!getenv("THESIA_RENDER_PER_TRACK")) {
+    if (render_path() == 0) {
         // every track in one launch per stage (launch_render_batch); workspaces for all tracks
         std::vector<RenderDesc> desc;
         desc.reserve(n);

@@ -64,9 +64,6 @@ struct Plan {
     DevBuf mel4_round, mel4_k0, mel4_wt;  // stft2_kernel layout (float4 steps)
     int mel4_rounds = 0;
     size_t mel4_wt_rows = 0;
-    DevBuf tw4a, tw4b, mel5_round, mel5_meta, mel5_wt;  // stft4_kernel (n_fft 2048)
-    int mel5_rounds = 0;
-    size_t mel5_rows = 0;
     bool use_v2 = false;  // stft2_kernel runs this plan (n_fft 256..2048)
     size_t row_bins() const;
     size_t out_elem_bytes() const { return out_kind == OUT_COMPLEX ? 8 : 4; }
@@ -81,12 +78,18 @@ struct Batch {
     DevBuf d_in_off, d_len, d_frame0;
     uint64_t total_frames = 0;
     StftLaunch launch{};
-    int kernel = 1;  // 1 stft_kernel, 2 stft2_kernel, 3 stft3_kernel, 4 stft4_kernel (streaming)
+    int kernel = 1;  // 1 stft_kernel, 2 stft2_kernel, 3 stft3_kernel (streaming)
+    bool k3_ok = false;  // the streaming kernel supports this batch's geometry
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     ~Batch();
 };
 int batch_create(Plan* plan, const thesia_batch_desc& d, Batch** out);
 int batch_run(Batch* b, hipStream_t s);
+int batch_set_option(Batch* b, int option, int64_t value);  // thesia_batch_set_option
+
+// display path selection (thesia_set_render_path): 0 batched launches, 1 per-track launches
+int render_path();
+int set_render_path(int path);
 
 // ---- display helpers on device buffers (used by MultiTrack and the C ABI) ----
 int grey_to_rgb_device(const float* d_grey, uint32_t w, uint32_t h, uint32_t nw, uint32_t nh,

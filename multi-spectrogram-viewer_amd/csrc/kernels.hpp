@@ -44,8 +44,6 @@ struct StftLaunch {
     const float2* sincos = nullptr;  // [NC] realfft untangle table (sin, cos)
     const float2* tw2 = nullptr;     // stft2: [TB + TA][L] W_NC^{j*b}, W_NC^{j*TB*a} (lane-major)
     const float2* tw3 = nullptr;     // stft3: [P][L] W_NC^{j*k1} (lane-major)
-    const float2* tw4a = nullptr;    // stft4 (NC = 1024): [16][64] W_1024^{lane*k1}
-    const float2* tw4b = nullptr;    // stft4: [4][17] W_64^{la*kb} (row padded to 17)
     float log_amin = 0.f;            // log10f(amin), host-computed
     // mel (lib.rs:131): round r gives lane j of a frame mel r*L + j (L = lanes per frame);
     // the lane runs bins mel_k0[r*L + j] + it, it < mel_round[r].y, with weights
@@ -64,19 +62,11 @@ struct StftLaunch {
     const int2* mel4_round = nullptr;
     const int* mel4_k0 = nullptr;
     const float4* mel4_wt = nullptr;
-    // stft4_kernel (one frame per 64 lanes): round u, lane l runs filter A for sA float4 steps
-    // from bin kA, then filter B for the rest of the round's steps (stft4_kernels.hip mel5);
-    // mel5_meta[u*64 + l] = {kA, kB - 4*sA, sA, mA | mB << 16}, mel5_round[u] = {row, steps},
-    // weights mel5_wt[(row + s) * 64 + l]
-    int mel5_rounds = 0;
-    int mel5_rows = 0;
-    const int2* mel5_round = nullptr;
-    const int4* mel5_meta = nullptr;
-    const float4* mel5_wt = nullptr;
     // output
     void* out = nullptr;  // packed rows: frame g at out + g * row_elems
-    // scheduling
-    int grid = 0;  // 0 => computed from occupancy
+    // scheduling / named alternatives (thesia_batch_set_option)
+    int grid = 0;     // 0 => computed from occupancy, else at most this many blocks
+    int row_alt = 0;  // 1: the other row-store method (stft3 n_fft 2048 stereo f32)
 };
 
 // Returns 0 on success, -2 for an unsupported n_fft.
@@ -89,11 +79,7 @@ int stft2_kernel_info(int n_fft, int* lds_bytes, int* tile_frames, int* lanes_pe
 // the geometry is not its own (or the mel rows do not fit LDS).
 int launch_stft3(const StftLaunch& a, hipStream_t stream);
 bool stft3_supports(int n_fft, int win, int hop, int in_format, int channels);
-// stft4_kernel (streaming, one frame per wave; n_fft 2048, win = n_fft, hop = n_fft/4,
-// f32/s16 mono/stereo): 0 on success, -2 when the geometry is not its own.
-int launch_stft4(const StftLaunch& a, hipStream_t stream);
-bool stft4_supports(int n_fft, int win, int hop, int in_format, int channels);
-int stft4_lds_bytes(const StftLaunch& a, bool mel);
+int stft3_lds_bytes(const StftLaunch& a);  // dynamic LDS of the launch (> 163840: cannot run)
 // LDS bytes / frames per block pass / lanes per frame of the kernel for n_fft.
 int stft_kernel_info(int n_fft, int* lds_bytes, int* tile_frames, int* lanes_per_frame);
 

@@ -394,7 +394,6 @@ static int launch3_k(const StftLaunch& a, hipStream_t stream) {
     if constexpr (VAR == 0 && WV == kWaves && NC == 1024 && OK != 2 && C == 2 && INF == IN_F32) {
         const char* e = getenv("THESIA_STFT_VARIANT");
         switch (e ? atoi(e) : 0) {
-            case 1024: return launch3_k<NC, OK, C, INF, 1024>(a, stream);  // other row-store method
             case 4: return launch3_k<NC, OK, C, INF, 4>(a, stream);  // ablation: no FFT
             case 1028: return launch3_k<NC, OK, C, INF, 1028>(a, stream);
             case 4096: return launch3_k<NC, OK, C, INF, 4096>(a, stream);  // no priority phases
@@ -402,6 +401,11 @@ static int launch3_k(const StftLaunch& a, hipStream_t stream) {
         }
     }
 #endif
+    // the named alternative row-store method (thesia_batch_set_option ROW_STORE; measured,
+    // DESIGN.md §6), compiled for the headline geometry only
+    if constexpr (VAR == 0 && WV == kWaves && NC == 1024 && OK != 2 && C == 2 && INF == IN_F32) {
+        if (a.row_alt) return launch3_k<NC, OK, C, INF, 1024>(a, stream);
+    }
     constexpr int kBlock = 64 * WV;
     const int lds = lds3_bytes<NC, OK, VAR, WV>(a);
     if (lds > 163840) return -2;
@@ -432,6 +436,18 @@ static int launch3_nc(const StftLaunch& a, hipStream_t s) {
     if (a.in_format == IN_S16)
         return a.channels == 2 ? launch3_c<NC, 2, IN_S16>(a, s) : launch3_c<NC, 1, IN_S16>(a, s);
     return a.channels == 2 ? launch3_c<NC, 2, IN_F32>(a, s) : launch3_c<NC, 1, IN_F32>(a, s);
+}
+
+int stft3_lds_bytes(const StftLaunch& a) {
+    const bool mel = a.out_kind == OUT_MEL || a.out_kind == OUT_MEL_AMP_DB;
+    const int ok = a.out_kind == OUT_COMPLEX ? 0 : mel ? 2 : 1;
+    switch (a.n_fft / 2) {
+        case 128: return ok == 0 ? lds3_bytes<128, 0, 0>(a) : ok == 1 ? lds3_bytes<128, 1, 0>(a) : lds3_bytes<128, 2, 0>(a);
+        case 256: return ok == 0 ? lds3_bytes<256, 0, 0>(a) : ok == 1 ? lds3_bytes<256, 1, 0>(a) : lds3_bytes<256, 2, 0>(a);
+        case 512: return ok == 0 ? lds3_bytes<512, 0, 0>(a) : ok == 1 ? lds3_bytes<512, 1, 0>(a) : lds3_bytes<512, 2, 0>(a);
+        case 1024: return ok == 0 ? lds3_bytes<1024, 0, 0>(a) : ok == 1 ? lds3_bytes<1024, 1, 0>(a) : lds3_bytes<1024, 2, 0>(a);
+        default: return 1 << 30;
+    }
 }
 
 bool stft3_supports(int n_fft, int win, int hop, int in_format, int channels) {

@@ -83,6 +83,8 @@ _SIGS = {
     "thesia_grey_to_rgb": (_i, [_fp, _u32, _u32, _u32, _u32, _u8p, _sz]),
     "thesia_wav_to_image": (_i, [_fp, _sz, _u32, _u32, _f, _f, _u8p, _sz]),
     "thesia_batch_kernel": (_i, [_vp, C.POINTER(C.c_int)]),
+    "thesia_batch_set_option": (_i, [_vp, _i, C.c_int64]),
+    "thesia_set_render_path": (_i, [_i]),
     "thesia_minmax_device": (_i, [C.c_void_p, C.c_uint64, C.POINTER(C.c_float), C.POINTER(C.c_float),
                                   C.POINTER(C.c_int)]),
     "thesia_spec_to_grey_device": (_i, [C.c_void_p, _sz, _sz, _f, _f, _f, C.c_void_p]),

@@ -11,6 +11,7 @@ from ._lib import lib, check, PlanDesc, BatchDesc, _fp, _u64p
 
 OUT_COMPLEX, OUT_MAG, OUT_POWER, OUT_AMP_DB, OUT_POWER_DB, OUT_MEL, OUT_MEL_AMP_DB = range(7)
 IN_F32, IN_S16 = 0, 1
+OPT_KERNEL, OPT_MAX_BLOCKS, OPT_ROW_STORE = 1, 2, 3
 
 
 def device_count() -> int:
@@ -119,7 +120,9 @@ class Batch:
     track ([total_frames, row_bins])."""
 
     def __init__(self, plan: Plan, d_input: DeviceBuffer, track_offset, track_len, d_output,
-                 input_format: int = IN_F32, channels: int = 1, fold_mono: bool = False):
+                 input_format: int = IN_F32, channels: int = 1, fold_mono: bool = False,
+                 kernel: int = 0, max_blocks: int = 0, row_store: int = 0):
+        """kernel / max_blocks / row_store: thesia_batch_set_option (0 = defaults)."""
         self.plan = plan
         self._off = np.ascontiguousarray(track_offset, np.uint64)
         self._len = np.ascontiguousarray(track_len, np.uint64)
@@ -137,6 +140,12 @@ class Batch:
         check(lib.thesia_batch_frames(self.handle, C.byref(tot), f0.ctypes.data_as(_u64p)))
         self.total_frames = tot.value
         self.frame0 = f0
+        for opt, v in ((OPT_KERNEL, kernel), (OPT_MAX_BLOCKS, max_blocks), (OPT_ROW_STORE, row_store)):
+            if v:
+                self.set_option(opt, v)
+
+    def set_option(self, option: int, value: int) -> None:
+        check(lib.thesia_batch_set_option(self.handle, option, int(value)))
 
     @staticmethod
     def frames_for(plan: Plan, track_len) -> int:
@@ -172,6 +181,11 @@ class Batch:
             self.close()
         except Exception:
             pass
+
+
+def set_render_path(path: int) -> None:
+    """0: batched display launches (default); 1: per-track launches (cross-check)."""
+    check(lib.thesia_set_render_path(path))
 
 
 def synth_pcm_device(buf: DeviceBuffer, fmt: int, channels: int, n_tracks: int, n_samples: int,

@@ -48,3 +48,13 @@ def test_validation_errors_before_device_work():
     with pytest.raises(thesia.ThesiaError) as e:
         thesia.perform_stft([0.0, 1.0], 8, 2, 8)  # n < win - 1: lib.rs:413 panic
     assert e.value.code == _lib.ERR_TOO_SHORT
+
+
+def test_product_library_has_no_experiment_hooks():
+    """The shipped library reads no environment variable that changes a kernel: the ablation /
+    A-B variants (THESIA_STFT_VARIANT, some of which write wrong output by design) and the
+    launch-shape knobs exist only in lib/libthesia_exp.so (`make exp`, -DTHESIA_EXPERIMENTS)."""
+    blob = open(_lib.LIB_PATH, "rb").read()
+    for name in (b"THESIA_STFT_VARIANT", b"THESIA_GRID", b"THESIA_STFT_KERNEL", b"THESIA_STFT_V1",
+                 b"THESIA_RENDER_PER_TRACK", b"THESIA_RENDER_RY", b"THESIA_RENDER_ABL"):
+        assert name not in blob, name

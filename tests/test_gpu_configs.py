@@ -97,12 +97,18 @@ def test_c5_mixed_rate_render_pipeline():
 @pytest.mark.parametrize("per_track", [False, True])
 @pytest.mark.parametrize("px_per_sec", [73.0, 30.0, 9.0])  # 30: 17-64 taps (LDS weights); 9: > 64 (direct)
 @pytest.mark.parametrize("nheight", [90, 400])  # 400: taller images (H->nheight downsampling ratio ~2.5)
-def test_render_batch_ragged_groups(per_track, px_per_sec, nheight, monkeypatch):
+def test_render_batch_ragged_groups(per_track, px_per_sec, nheight):
     """Several tracks of different lengths per geometry group: the batched render (one launch
     per stage for the whole group, blockIdx.z = track) and the per-track launches produce the
     oracle's bytes for every image (ragged T, nwidth and workspace offsets)."""
-    if per_track:
-        monkeypatch.setenv("THESIA_RENDER_PER_TRACK", "1")
+    engine.set_render_path(1 if per_track else 0)
+    try:
+        _ragged(px_per_sec, nheight)
+    finally:
+        engine.set_render_path(0)
+
+
+def _ragged(px_per_sec, nheight):
     base = pipeline.c5_tracks(12, seconds=0.6)
     tracks = []
     for k, t in enumerate(base[:4] * 3):  # 4 geometries x 3 lengths each

@@ -1,4 +1,4 @@
-"""The streaming kernels (stft3_kernel; stft4_kernel at n_fft 2048) against the
+"""The streaming kernel (stft3_kernel) and the general kernels against the
 oracle on the cases their register ring makes special: streams that cross track ends, tracks that start at odd element
 offsets (no 8/16-byte alignment: per-frame reloads), the shortest legal tracks (n = win - 1,
 lib.rs:413), frames that reflect at both ends, mono / stereo, f32 / s16, and a grid small enough
@@ -22,7 +22,7 @@ def _mono_fold(t):  # lib.rs:42 channel sum, (0 + c0) + c1 ...
     return acc
 
 
-def _run(n_fft, tracks, channels, fmt, gap, kernel):
+def _run(n_fft, tracks, channels, fmt, gap, kernel, max_blocks=3):
     """tracks packed with `gap` elements between them (odd gaps break the alignment)."""
     hop = n_fft // 4
     parts, offs, off = [], [], 0
@@ -39,21 +39,21 @@ def _run(n_fft, tracks, channels, fmt, gap, kernel):
     din = engine.DeviceBuffer.from_host(flat)
     T = engine.Batch.frames_for(plan, lens)
     dout = engine.DeviceBuffer(T * plan.row_bins * 8)
-    b = engine.Batch(plan, din, offs, lens, dout, input_format=fmt, channels=channels)
-    assert b.kernel == kernel  # a streaming kernel runs these geometries
+    b = engine.Batch(plan, din, offs, lens, dout, input_format=fmt, channels=channels,
+                     kernel=kernel, max_blocks=max_blocks)
+    assert b.kernel == kernel
     b.run()
     engine.synchronize()
     out = dout.to_host(np.complex64, (T, plan.row_bins))
     return [out[int(b.frame0[i]):int(b.frame0[i + 1])] for i in range(len(tracks))]
 
 
-@pytest.mark.parametrize("n_fft,kernel", [(256, 3), (1024, 3), (2048, 3), (2048, 4)])
+@pytest.mark.parametrize("n_fft,kernel", [(256, 3), (1024, 3), (2048, 3), (2048, 2), (512, 1)])
 @pytest.mark.parametrize("channels,fmt", [(1, engine.IN_F32), (2, engine.IN_F32), (2, engine.IN_S16),
                                           (1, engine.IN_S16)])
 @pytest.mark.parametrize("gap", [0, 3])
-def test_streams_across_tracks_edges_and_alignment(n_fft, kernel, channels, fmt, gap, monkeypatch):
-    monkeypatch.setenv("THESIA_GRID", "3")  # 3 blocks: every stream walks many frames
-    monkeypatch.setenv("THESIA_STFT_KERNEL", str(kernel))
+def test_streams_across_tracks_edges_and_alignment(n_fft, kernel, channels, fmt, gap):
+    # at most 3 blocks: every stream of the streaming kernel walks many frames
     rng = np.random.default_rng(n_fft * 10 + channels * 3 + fmt + gap)
     hop = n_fft // 4
     lens = [n_fft - 1, n_fft, n_fft + 1, 3 * n_fft + 7, 37 * hop, 10 * n_fft + 3, 60 * hop + 5, 2 * n_fft]
@@ -77,18 +77,16 @@ _LIN_KINDS = [engine.OUT_MAG, engine.OUT_POWER, engine.OUT_AMP_DB, engine.OUT_PO
 @pytest.mark.parametrize("n_fft", [256, 2048])
 @pytest.mark.parametrize("kind", _LIN_KINDS + [engine.OUT_COMPLEX])
 @pytest.mark.parametrize("shift", [0, 1, 2, 3])
-@pytest.mark.parametrize("variant", ["0", "1024"])
-def test_row_stores_any_output_alignment(n_fft, kind, shift, variant, monkeypatch):
+@pytest.mark.parametrize("row_store", [0, 1])
+def test_row_stores_any_output_alignment(n_fft, kind, shift, row_store):
     """Output rows of F floats / F float2 are not 16-byte aligned; the LDS-staged float4 row
-    stores (stft3 store_row_b128: linear kinds by default, complex with variant 1024) must write
+    stores (stft3 store_row_b128: linear kinds by default, complex with the ROW_STORE option) must write
     exactly the row whatever the output pointer's alignment, and nothing outside the batch's
     rows (guard floats on both sides stay untouched)."""
     if kind == engine.OUT_COMPLEX and shift % 2:
         pytest.skip("complex rows are float2: 8-byte aligned output")
-    if variant != "0" and n_fft != 2048:
-        pytest.skip("the store-method variant is compiled for n_fft 2048 stereo f32 only")
-    monkeypatch.setenv("THESIA_GRID", "3")
-    monkeypatch.setenv("THESIA_STFT_VARIANT", variant)
+    if row_store and n_fft != 2048:
+        pytest.skip("the other store method is compiled for n_fft 2048 stereo f32 only")
     rng = np.random.default_rng(n_fft + 7 * kind + shift)
     hop = n_fft // 4
     lens = [n_fft - 1, 5 * n_fft + 3, 33 * hop + 1, 2 * n_fft]
@@ -104,7 +102,8 @@ def test_row_stores_any_output_alignment(n_fft, kind, shift, variant, monkeypatc
     host = np.full(T * fl + 2 * guard + 4, sentinel, np.float32)
     dout = engine.DeviceBuffer.from_host(host)
     ptr = dout.ptr.value + (guard + shift) * 4
-    b = engine.Batch(plan, din, offs, lens, ptr, input_format=engine.IN_F32, channels=2)
+    b = engine.Batch(plan, din, offs, lens, ptr, input_format=engine.IN_F32, channels=2,
+                     max_blocks=3, row_store=row_store)
     assert b.kernel == 3
     b.run()
     engine.synchronize()
