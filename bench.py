@@ -10,27 +10,27 @@ downmix (lib.rs:42) -> reflect framing + Hann/n_fft (lib.rs:367-440) -> real FFT
 (stft3_kernel). Files shard across ranks by LPT (thesia.shard) with no
 data-path collective ("weak" scaling: per-GPU work is fixed).
 
-Launch: python bench.py [--gpus N --steps K --warmup W]; for N > 1 under
-torch.distributed.run (one rank per GPU; gloo is used only for the timing barrier / max).
-Prints ONE JSON line on rank 0.
+Launch: `python bench.py [--gpus N --steps K --warmup W]`. With --gpus N > 1 and no
+WORLD_SIZE in the environment this process is only a launcher: it spawns N worker processes
+(RANK / LOCAL_RANK / WORLD_SIZE / MASTER_* set, one per GPU) before anything touches a GPU,
+relays rank 0's JSON line and exits with the workers' status. Under torch.distributed.run the
+process is a worker directly. gloo carries only the timing barrier / max and the per-rank
+report. Prints ONE JSON line on rank 0.
 """
 from __future__ import annotations
 
 import argparse
 import json
 import os
+import signal
+import socket
+import subprocess
 import sys
 import time
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
-sys.path.insert(0, os.path.join(ROOT, "multi-spectrogram-viewer_amd"))
-
-import numpy as np  # noqa: E402
-
-import thesia  # noqa: E402  (loads libthesia before torch: one HIP runtime in the process)
-from thesia import engine, shard  # noqa: E402
-
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s HBM3E (spec)
+METRIC = "STFT frames/sec (n_fft=2048 hop=512) at 1/2/4/8 GPUs; % HBM roofline"
 
 
 def parse():
@@ -53,9 +53,14 @@ def parse():
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-rfft-roofline", action="store_true",
                    help="skip the extra complex-output (window+rFFT kernel) roofline measurement")
-    p.add_argument("--cpu-workers", type=int, default=16)
-    p.add_argument("--variants", default="", help="experiment: comma list of THESIA_STFT_VARIANT "
-                   "values to A/B (interleaved rounds, one process); prints per-variant kernel ms")
+    p.add_argument("--no-c1", action="store_true", help="skip the C1 (48 kHz sample, 1024/256) line")
+    p.add_argument("--cpu-threads", type=int, default=0,
+                   help="CPU baseline threads (0: OMP_NUM_THREADS if set, else the affinity mask)")
+    p.add_argument("--variants", default="", help="experiment (needs THESIA_LIB=lib/libthesia_exp.so): "
+                   "comma list of THESIA_STFT_VARIANT values to A/B (interleaved rounds, one process)")
+    p.add_argument("--selftest", action="store_true",
+                   help="launcher / reduction plumbing only: no GPU, no thesia (CPU tests)")
+    p.add_argument("--selftest-fail-rank", type=int, default=-1, help=argparse.SUPPRESS)
     a = p.parse_args()
     if a.seconds is None:
         a.seconds = 30.0 if a.workload == "c4" else 10.0
@@ -64,7 +69,60 @@ def parse():
     return a
 
 
-def dist_setup(args):
+# ------------------------------------------------------------------------------------------
+# launcher (no GPU, no thesia / torch import: the workers own the devices)
+# ------------------------------------------------------------------------------------------
+def _free_port() -> int:
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch(n: int) -> int:
+    """Spawn n worker processes of this script (one per GPU, RANK = LOCAL_RANK = i), relay
+    rank 0's stdout, wait for all; a failing worker stops the others (their exact PIDs)."""
+    port = _free_port()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n),
+                   LOCAL_WORLD_SIZE=str(n), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:],
+                                      env=env, stdout=subprocess.PIPE if r == 0 else subprocess.DEVNULL))
+    import threading
+
+    def relay():
+        for line in procs[0].stdout:
+            sys.stdout.write(line.decode())
+            sys.stdout.flush()
+
+    reader = threading.Thread(target=relay, daemon=True)
+    reader.start()
+    rc = 0
+    try:
+        pending = list(procs)
+        while pending:
+            for p in list(pending):
+                code = p.poll()
+                if code is None:
+                    continue
+                pending.remove(p)
+                if code != 0 and rc == 0:
+                    rc = code
+                    for q in pending:  # stop the rest: their own PIDs only
+                        q.send_signal(signal.SIGTERM)
+            time.sleep(0.05)
+        reader.join(timeout=10)
+    finally:
+        for p in procs:
+            if p.poll() is None:
+                p.kill()
+    return rc if rc >= 0 else 128 - rc
+
+
+# ------------------------------------------------------------------------------------------
+# worker side
+# ------------------------------------------------------------------------------------------
+def dist_setup():
     ws = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -91,6 +149,131 @@ def max_over_ranks(pg, v: float) -> float:
     return float(t.item())
 
 
+def gather_reports(pg, rep: dict) -> list:
+    """Every rank's report (device, frames, ...) on every rank (gloo)."""
+    if pg is None:
+        return [rep]
+    out = [None] * pg.get_world_size()
+    pg.all_gather_object(out, rep)
+    return out
+
+
+def ranks_summary(reports: list, frames_key: str = "frames") -> dict:
+    devices = sorted({r["device"] for r in reports})
+    return {"n_devices": len(devices), "devices": devices,
+            "per_rank_frames": [int(r[frames_key]) for r in reports],
+            "total_frames": int(sum(r[frames_key] for r in reports))}
+
+
+def cpu_info() -> dict:
+    model = None
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    aff = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else None
+    return {"nproc": os.cpu_count(), "affinity_cpus": aff, "cpu_model": model,
+            "omp_num_threads": os.environ.get("OMP_NUM_THREADS")}
+
+
+def cpu_threads(args) -> int:
+    """The host share this run may use: --cpu-threads, else OMP_NUM_THREADS (the GPU box sets
+    it to its 16-CPU share per GPU; nproc there counts the whole machine), else the affinity."""
+    if args.cpu_threads > 0:
+        return args.cpu_threads
+    env = os.environ.get("OMP_NUM_THREADS")
+    if env and env.isdigit() and int(env) > 0:
+        return int(env)
+    return len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+
+
+def cpu_baseline(args, n_samples):
+    """The oracle (oracle/thesia_oracle.c, a C restatement of the reference path, test
+    infrastructure) timed on a bounded sample of the same workload with the reference's
+    execution structure: per-track parallel over a thread pool (rayon par_iter, lib.rs:161-166),
+    one FFT plan per track (lib.rs:459-467), dense mel dot, three-pass dB. One C call per
+    track (ctypes releases the GIL)."""
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import numpy as np
+    import oracle_ffi as O
+    from concurrent.futures import ThreadPoolExecutor
+    from thesia import engine
+
+    threads = cpu_threads(args)
+    n_tracks = 4 * threads  # ~0.19 s of CPU per C4 track: ~12 s of CPU work on 16 threads
+    kind = {"mel_db": O.TRACK_MEL_DB, "amp_db": O.TRACK_AMP_DB, "power_db": O.TRACK_POWER_DB,
+            "complex": O.TRACK_MAG}[args.output]
+    fb = O.calc_mel_fb(args.sr, args.n_fft, args.n_mels) if kind == O.TRACK_MEL_DB else None
+    pcm = [(engine.synth_pcm_host(args.channels, i, n_samples, args.sr).astype(np.float32) / np.float32(32768.0))
+           for i in range(n_tracks)]
+
+    def one(x):
+        return O.track_spec(x, args.n_fft, args.hop, args.n_fft, kind, fb).shape[0]
+
+    t0 = time.perf_counter()
+    with ThreadPoolExecutor(threads) as ex:
+        frames = sum(ex.map(one, pcm))
+    dt = time.perf_counter() - t0
+    return dict({"value": frames / dt, "unit": "frames/s", "cores": threads, "kind": "port",
+                 "sample": f"{n_tracks} tracks x {args.seconds:g} s x {args.channels} ch @ {args.sr} Hz "
+                           f"({frames} frames, {dt:.2f} s wall, {threads} threads) through the C oracle "
+                           f"(one FFT plan per track, dense mel dot)"}, **cpu_info())
+
+
+def c1_line(args):
+    """BASELINE.json configs[0] (C1): the 48 kHz sample (substitute: tests/fixtures.py
+    c1_substitute, 2 113 529 samples), n_fft 1024 / hop 256 / Hann, |X| (lib.rs:124).
+    GPU: one batch of that one track (stft3_kernel), HIP-event time. CPU: the reference's
+    single-track path -- frames built serially, then per-frame parallel with a fresh RealFFT
+    per frame (lib.rs:449-458) over the thread pool -- through the oracle."""
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import numpy as np
+    import fixtures
+    import oracle_ffi as O
+    from concurrent.futures import ThreadPoolExecutor
+    from thesia import engine
+
+    x = fixtures.s16_to_f32(fixtures.c1_substitute())
+    n = x.shape[0]
+    plan = engine.Plan(1024, 1024, 256, engine.OUT_MAG, sr=48000)
+    din = engine.DeviceBuffer.from_host(x)
+    T = engine.Batch.frames_for(plan, [n])
+    dout = engine.DeviceBuffer(T * plan.row_bins * 4)
+    b = engine.Batch(plan, din, [0], [n], dout)
+    b.run_timed(3)
+    kms = b.run_timed(20) / 20
+    gpu = {"frames": T, "kernel_ms": kms, "frames_per_s": T / (kms * 1e-3), "kernel": b.kernel}
+    b.close()
+    dout.close()
+    din.close()
+    plan.close()
+    out = {"workload": "C1: 48 kHz sample substitute (2 113 529 samples), n_fft 1024 hop 256 Hann, |X|",
+           "gpu": gpu}
+    if not args.no_cpu_baseline:
+        threads = cpu_threads(args)
+        reps = 8
+        t0 = time.perf_counter()
+        with ThreadPoolExecutor(threads) as ex:
+            for _ in range(reps):
+                fr = O.frames(x, 1024, 256, 1024)
+                mag = np.empty((fr.shape[0], 513), np.float32)
+                step = (fr.shape[0] + threads - 1) // threads
+                list(ex.map(lambda t: O.rfft_mag_rows(fr, t, min(t + step, fr.shape[0]), mag, True),
+                            range(0, fr.shape[0], step)))
+        dt = time.perf_counter() - t0
+        out["cpu_baseline_c1"] = dict({"value": reps * T / dt, "unit": "frames/s", "cores": threads,
+                                       "kind": "port",
+                                       "sample": f"{reps} passes over the whole C1 track ({reps * T} frames, "
+                                                 f"{dt:.2f} s wall): serial framing + per-frame parallel rfft "
+                                                 f"with a RealFFT::new per frame (lib.rs:449-458) + hypot"},
+                                      **cpu_info())
+    return out
+
+
 def algorithmic_bytes(args, n_tracks, n_samples, total_frames, row_bins):
     """Bytes one launch must move at least: the input once (hop-strided, not n_fft per frame)
     plus the output rows (DESIGN.md §4 'Roofline and algorithmic bytes')."""
@@ -99,42 +282,12 @@ def algorithmic_bytes(args, n_tracks, n_samples, total_frames, row_bins):
     return n_tracks * n_samples * args.channels * in_el + total_frames * row_bins * out_el
 
 
-def cpu_baseline(args, n_samples):
-    """The oracle (oracle/thesia_oracle.c, a C restatement of the reference path) on a
-    bounded sample of the same workload: per-track parallel with one plan per track, like
-    the reference's rayon path (lib.rs:161-166)."""
-    sys.path.insert(0, os.path.join(ROOT, "tests"))
-    import oracle_ffi as O
-    from concurrent.futures import ThreadPoolExecutor
-
-    workers = max(1, min(args.cpu_workers, os.cpu_count() or 1))
-    n_tracks = 3 * workers  # ~10-15 s of CPU work on 16 threads
-    fb = O.calc_mel_fb(args.sr, args.n_fft, args.n_mels)
-    pcm = [engine.synth_pcm_host(args.channels, i, n_samples, args.sr).astype(np.float32) / 32768.0
-           for i in range(n_tracks)]
-
-    def one(x):
-        mono = np.zeros(x.shape[0], np.float32)
-        for c in range(x.shape[1]):
-            mono = (mono + x[:, c]).astype(np.float32)
-        X = O.perform_stft(mono, args.n_fft, args.hop, args.n_fft)
-        db = O.amp_to_db_default(O.dot(O.norm(X), fb))
-        return db.shape[0]
-
-    t0 = time.perf_counter()
-    with ThreadPoolExecutor(workers) as ex:
-        frames = sum(ex.map(one, pcm))
-    dt = time.perf_counter() - t0
-    return {"value": frames / dt, "unit": "frames/s", "cores": workers, "kind": "port",
-            "sample": f"{n_tracks} tracks x {args.seconds:g} s x {args.channels} ch @ {args.sr} Hz "
-                      f"({frames} frames, {dt:.2f} s wall) through the C oracle, {workers} threads"}
-
-
 def rfft_roofline(args, din, offs, lens, fmt, n_local, n_samples):
     """BASELINE.json north_star's "window+rFFT kernel" on the same resident input: the same
     streaming kernel with complex-spectrum output ([T, F] complex64, perform_stft's result,
     lib.rs:436-440), timed with HIP events on its launch stream; algorithmic bytes = input once
     + F x 8 B per frame. Reported beside the headline roofline, never as `value`."""
+    from thesia import engine
     plan = engine.Plan(args.n_fft, args.n_fft, args.hop, engine.OUT_COMPLEX, sr=args.sr)
     frames = engine.Batch.frames_for(plan, lens)
     dout = engine.DeviceBuffer(frames * plan.row_bins * 8)
@@ -152,15 +305,6 @@ def rfft_roofline(args, din, offs, lens, fmt, n_local, n_samples):
             "kernel": "thesia::stft3_kernel, complex output (downmix+frame+window+rFFT)"}
 
 
-def frames_all_ranks(pg, frames: int) -> int:
-    if pg is None:
-        return frames
-    import torch
-    t = torch.tensor([float(frames)], dtype=torch.float64)
-    pg.all_reduce(t, op=pg.ReduceOp.SUM)
-    return int(t.item())
-
-
 def traffic_from_profile(workload_key):
     path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     try:
@@ -172,13 +316,31 @@ def traffic_from_profile(workload_key):
         return None
 
 
-def main_c5(args, ws, rank, pg):
+def main_selftest(args, ws, rank, pg):
+    """Launcher plumbing without a GPU: each rank 'processes' (rank + 1) x 1000 frames in a
+    short sleep; the reductions are the real ones (gloo barrier, max time, report gather)."""
+    if rank == args.selftest_fail_rank:
+        sys.exit(3)
+    barrier(pg)
+    t0 = time.perf_counter()
+    time.sleep(0.05 * (rank + 1))
+    barrier(pg)
+    dt = max_over_ranks(pg, time.perf_counter() - t0)
+    reps = gather_reports(pg, {"device": rank, "frames": 1000 * (rank + 1), "pid": os.getpid()})
+    if rank == 0:
+        s = ranks_summary(reps)
+        print(json.dumps({"selftest": True, "n_ranks": ws, "n_gpus": s["n_devices"], "value": s["total_frames"] / dt,
+                          "ms_per_step": dt * 1e3, "per_rank_frames": s["per_rank_frames"],
+                          "pids": [r["pid"] for r in reps]}), flush=True)
+
+
+def main_c5(args, ws, rank, pg, device):
     """C5 (BASELINE.json configs[4]): mixed-rate tracks with per-track n_fft, amp dB, global
     range exchange, grey + Lanczos3 + colormap RGB for every track (thesia.pipeline). One step =
     spectrogram launches for every geometry group + the display path of every track, the RGB
     images left in HBM (the copy to the host that get_spec_image implies, lib.rs:294-298, is
     timed separately: PCIe-inclusive, never the reported value)."""
-    from thesia import pipeline
+    from thesia import engine, pipeline, shard
 
     total = args.tracks * ws
     gen = pipeline.c5_tracks(total, seconds=0.0)  # geometry only (empty PCM) for the partition
@@ -215,20 +377,23 @@ def main_c5(args, ws, rank, pg):
     dt_host = max_over_ranks(pg, (time.perf_counter() - t0) / 3)
     # spectrogram kernels alone (HIP events per group launch)
     kms = sum(b.run_timed(3) / 3 for _, _, _, b in p.groups)
+    disp = p.display_timed(3)
     in_bytes = sum(t.pcm.nbytes for t in tracks)
     out_bytes = sum(b.total_frames * pl.row_bins * 4 for pl, _, _, b in p.groups)
     achieved = (in_bytes + out_bytes) / (kms * 1e-3) / 1e9
-    frames_all = frames_all_ranks(pg, p.total_frames)
+    reps = gather_reports(pg, {"device": device, "frames": p.total_frames, "tracks": len(tracks)})
+    summ = ranks_summary(reps)
     if rank == 0:
         print(json.dumps({
-            "metric": "STFT frames/sec (n_fft=2048 hop=512) at 1/2/4/8 GPUs; % HBM roofline",
-            "value": frames_all / dt, "unit": "frames/s", "n_gpus": ws, "steps": args.steps,
+            "metric": METRIC,
+            "value": summ["total_frames"] / dt, "unit": "frames/s", "n_gpus": summ["n_devices"], "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": dt * 1e3, "higher_is_better": True,
             "scaling": "weak", "vs_baseline": None, "dtype": "f32",
             "data": "synthetic (int16 chirp + noise, seeded per track), resident in HBM",
             "config": {"workload": f"C5: {total} mixed-rate tracks (8-48 kHz) x {args.seconds:g} s, "
                                    f"n_fft 256-2048 per track, hop n_fft/4, amp dB + global range + "
                                    f"grey + Lanczos3 + colormap RGB at 100 px/s x 500 px",
+                       "ranks": ws, "per_rank_frames": summ["per_rank_frames"],
                        "tracks_per_gpu": len(tracks), "images_per_s": total / dt,
                        "geometry_groups": len(p.groups), "frames_per_gpu": p.total_frames,
                        "ms_per_step_with_rgb_copied_to_host": dt_host * 1e3,
@@ -237,17 +402,27 @@ def main_c5(args, ws, rank, pg):
                          "frac": achieved / HBM_PEAK_GBS, "traffic": None,
                          "kernel": "spectrogram launches of all geometry groups",
                          "kernel_ms": kms, "algorithmic_bytes_per_launch": in_bytes + out_bytes},
+            "roofline_display": disp,
         }), flush=True)
     p.close()
 
 
-def main():
-    args = parse()
-    ws, rank, local, pg = dist_setup(args)
+def main_worker(args):
+    ws, rank, local, pg = dist_setup()
+    if args.selftest:
+        main_selftest(args, ws, rank, pg)
+        if pg is not None:
+            pg.destroy_process_group()
+        return
+    import numpy as np
+    sys.path.insert(0, os.path.join(ROOT, "multi-spectrogram-viewer_amd"))
+    from thesia import engine, shard
+
     # one rank per GPU; on a box with fewer GPUs than ranks (a rehearsal) ranks share devices
-    engine.set_device(local % max(1, engine.device_count()))
+    device = local % max(1, engine.device_count())
+    engine.set_device(device)
     if args.workload == "c5":
-        main_c5(args, ws, rank, pg)
+        main_c5(args, ws, rank, pg, device)
         if pg is not None:
             pg.destroy_process_group()
         return
@@ -306,12 +481,13 @@ def main():
     abytes = algorithmic_bytes(args, n_local, n_samples, frames, plan.row_bins)
     achieved = abytes / (kms * 1e-3) / 1e9
 
-    total_frames_all = frames_all_ranks(pg, frames)
+    reps = gather_reports(pg, {"device": device, "frames": frames, "tracks": n_local})
+    summ = ranks_summary(reps)
     result = {
-        "metric": "STFT frames/sec (n_fft=2048 hop=512) at 1/2/4/8 GPUs; % HBM roofline",
-        "value": total_frames_all / dt,
+        "metric": METRIC,
+        "value": summ["total_frames"] / dt,
         "unit": "frames/s",
-        "n_gpus": ws,
+        "n_gpus": summ["n_devices"],
         "steps": args.steps,
         "warmup": args.warmup,
         "ms_per_step": dt * 1e3,
@@ -328,6 +504,9 @@ def main():
             "tracks_per_gpu": n_local,
             "tracks_total": args.tracks * ws,
             "frames_per_gpu": frames,
+            "ranks": ws,
+            "devices": summ["devices"],
+            "per_rank_frames": summ["per_rank_frames"],
             "parallelism": f"file-sharded x{ws}, no collective",
         },
     }
@@ -352,10 +531,19 @@ def main():
             result["roofline_window_rfft"] = rfft_roofline(args, din, offs, lens, fmt, n_local, n_samples)
         if ws == 1 and not args.no_cpu_baseline:
             result["cpu_baseline"] = cpu_baseline(args, n_samples)
+        if ws == 1 and not args.no_c1:
+            result["c1"] = c1_line(args)
         print(json.dumps(result), flush=True)
     batch.close()
     if pg is not None:
         pg.destroy_process_group()
+
+
+def main():
+    args = parse()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(launch(args.gpus))
+    main_worker(args)
 
 
 if __name__ == "__main__":

@@ -58,6 +58,13 @@ int thesia_memset_device(void* dst_device, int value, size_t bytes);
 int thesia_device_synchronize(void);
 /* Device name / CU count of the current device (for reports). */
 int thesia_device_info(char* name, size_t cap, int* n_cu);
+/* HIP events for timing work on a stream (NULL stream => the library's stream of the current
+ * device, where every thesia_* call without a stream argument runs). elapsed synchronises on
+ * the second event. */
+int thesia_event_create(void** event);
+int thesia_event_destroy(void* event);
+int thesia_event_record(void* event, void* stream);
+int thesia_event_elapsed_ms(void* start, void* stop, float* ms);
 
 /* ---------------------------------------------------------------------------------- */
 /* host tables (bit-exact f32 restatements; computed with the same libm the reference  */

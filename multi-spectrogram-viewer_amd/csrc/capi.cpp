@@ -104,6 +104,30 @@ int thesia_device_info(char* name, size_t cap, int* n_cu) {
     return THESIA_OK;
 }
 
+int thesia_event_create(void** event) {
+    if (!event) return set_error(THESIA_ERR_INVALID_ARG, "null pointer");
+    hipEvent_t e = nullptr;
+    THESIA_HIP(hipEventCreate(&e));
+    *event = e;
+    return THESIA_OK;
+}
+int thesia_event_destroy(void* event) {
+    if (event) THESIA_HIP(hipEventDestroy(static_cast<hipEvent_t>(event)));
+    return THESIA_OK;
+}
+int thesia_event_record(void* event, void* stream) {
+    if (!event) return set_error(THESIA_ERR_INVALID_ARG, "null event");
+    hipStream_t s = stream ? static_cast<hipStream_t>(stream) : default_stream();
+    THESIA_HIP(hipEventRecord(static_cast<hipEvent_t>(event), s));
+    return THESIA_OK;
+}
+int thesia_event_elapsed_ms(void* start, void* stop, float* ms) {
+    if (!start || !stop || !ms) return set_error(THESIA_ERR_INVALID_ARG, "null argument");
+    THESIA_HIP(hipEventSynchronize(static_cast<hipEvent_t>(stop)));
+    THESIA_HIP(hipEventElapsedTime(ms, static_cast<hipEvent_t>(start), static_cast<hipEvent_t>(stop)));
+    return THESIA_OK;
+}
+
 // ---------------------------------------------------------------- tables
 int thesia_hann(size_t size, int symmetric, float* out) {
     GUARD_BEGIN

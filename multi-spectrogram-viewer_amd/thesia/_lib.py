@@ -56,6 +56,10 @@ _SIGS = {
     "thesia_memset_device": (_i, [_vp, _i, _sz]),
     "thesia_device_synchronize": (_i, []),
     "thesia_device_info": (_i, [C.c_char_p, _sz, C.POINTER(_i)]),
+    "thesia_event_create": (_i, [C.POINTER(_vp)]),
+    "thesia_event_destroy": (_i, [_vp]),
+    "thesia_event_record": (_i, [_vp, _vp]),
+    "thesia_event_elapsed_ms": (_i, [_vp, _vp, _fp]),
     "thesia_hann": (_i, [_sz, _i, _fp]),
     "thesia_calc_proper_n_fft": (_sz, [_sz]),
     "thesia_hz_to_mel": (_f, [_f]),

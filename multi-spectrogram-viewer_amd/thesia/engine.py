@@ -35,6 +35,40 @@ def device_info():
     return name.value.decode(), n.value
 
 
+class EventTimer:
+    """HIP events on the library stream: `with EventTimer() as t: ...; t.ms` (device time of the
+    work enqueued in between)."""
+
+    def __init__(self):
+        self._e0, self._e1 = C.c_void_p(), C.c_void_p()
+        check(lib.thesia_event_create(C.byref(self._e0)))
+        check(lib.thesia_event_create(C.byref(self._e1)))
+        self.ms = 0.0
+
+    def __enter__(self):
+        check(lib.thesia_event_record(self._e0, None))
+        return self
+
+    def __exit__(self, *exc):
+        check(lib.thesia_event_record(self._e1, None))
+        ms = C.c_float()
+        check(lib.thesia_event_elapsed_ms(self._e0, self._e1, C.byref(ms)))
+        self.ms = ms.value
+        return False
+
+    def close(self):
+        for e in (self._e0, self._e1):
+            if e and e.value:
+                lib.thesia_event_destroy(e)
+        self._e0 = self._e1 = C.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
 class DeviceBuffer:
     """An HBM allocation owned by Python (freed on close / GC)."""
 

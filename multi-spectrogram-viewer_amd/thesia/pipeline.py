@@ -163,6 +163,34 @@ class RenderPipeline:
                 out[i] = Rendered(db, img, int(nw[k]), *ranges[i])
         return out
 
+    def display_bytes(self) -> dict:
+        """Algorithmic HBM bytes of one display pass (DESIGN.md §4 'Display roofline'): the dB
+        spectrogram read once (the per-track range + grey/vertical pass), the vertical pass's
+        f32 intermediate [T, nheight] written and read once, the RGB bytes written once."""
+        spec = tmp = rgb = 0
+        for i, t in enumerate(self.tracks):
+            _, _, T, bins = self.where[i]
+            spec += T * bins * 4
+            tmp += T * self.nheight * 4
+            rgb += self._geo[i] * self.nheight * 3
+        return {"spec_read": spec, "tmp_write_read": 2 * tmp, "rgb_write": rgb,
+                "total": spec + 2 * tmp + rgb}
+
+    def display_timed(self, iters: int = 3) -> dict:
+        """Device time of the display path (range + grey + Lanczos3 + colormap, no host copy),
+        HIP events on the library stream, and its HBM-roofline fraction."""
+        engine.synchronize()
+        self.render(want_rgb=False)  # warm (workspaces, tap tables)
+        with engine.EventTimer() as tm:
+            for _ in range(iters):
+                self.render(want_rgb=False)
+        ms = tm.ms / iters
+        b = self.display_bytes()
+        ach = b["total"] / (ms * 1e-3) / 1e9
+        return {"bound": "hbm", "achieved": ach, "peak": 8000.0, "unit": "GB/s", "frac": ach / 8000.0,
+                "traffic": None, "display_ms": ms, "algorithmic_bytes": b,
+                "kernel": "per-track range + grey/vertical Lanczos3 + horizontal Lanczos3 + colormap"}
+
     def _pinned_host(self, g: int, total: int) -> np.ndarray:
         buf = self._pinned.get(g)
         if buf is None or buf.nbytes < total:

@@ -54,7 +54,10 @@ def global_db_range(local_max: float, local_min: float, local_max_sr: int, db_ra
     computes them over ALL tracks: max = min(max, 0), min = max(min, max - db_range).
 
     With torch.distributed initialised, reduces over `group` (default world) with one
-    all_reduce(MAX) of (max, -min, max_sr); otherwise the local values are global."""
+    all_reduce(MAX) of (max, -min, max_sr) on host tensors; otherwise the local values are
+    global. Three scalars are latency-bound on any transport, and the engine's buffers are not
+    torch tensors, so a non-gloo group (RCCL "nccl") is shadowed by a gloo group over the same
+    ranks (created once, collectively) instead of staging the scalars on a GPU."""
     import numpy as np
 
     mx, mn, sr = float(local_max), float(local_min), int(local_max_sr)
@@ -65,15 +68,28 @@ def global_db_range(local_max: float, local_min: float, local_max_sr: int, db_ra
     except ImportError:  # pragma: no cover - torch is in the image
         active = False
     if active:
-        backend = dist.get_backend(group)
-        dev = "cuda" if backend == "nccl" else "cpu"
-        t = torch.tensor([mx, -mn, float(sr)], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX, group=group)
+        g = _host_group(dist, group)
+        t = torch.tensor([mx, -mn, float(sr)], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX, group=g)
         mx, mn, sr = float(t[0]), -float(t[1]), int(t[2])
     # lib.rs:208-209 in f32, as the reference stores them
     gmax = float(np.float32(min(mx, 0.0)))
     gmin = float(np.float32(max(mn, gmax - db_range)))
     return gmax, gmin, sr
+
+
+_GLOO_SHADOW = {}
+
+
+def _host_group(dist, group):
+    """`group` itself when it is gloo, else a gloo group over the same ranks (cached)."""
+    if dist.get_backend(group) == "gloo":
+        return group
+    key = id(group)
+    if key not in _GLOO_SHADOW:
+        ranks = None if group is None else dist.get_process_group_ranks(group)
+        _GLOO_SHADOW[key] = dist.new_group(ranks=ranks, backend="gloo")
+    return _GLOO_SHADOW[key]
 
 
 def up_ratio(sr: int, max_sr: int, freq_scale_mel: bool) -> float:

@@ -82,6 +82,12 @@ int or_pad_reflect_f32(const float* x, size_t n, size_t left, size_t right, floa
 /* The exact rustfft butterfly op order is not reproducible here (no toolchain): parity */
 /* for the FFT is by tolerance.                                             */
 /* ------------------------------------------------------------------------------------ */
+/* The twiddles every butterfly uses come from a table built once per length (tw[i] =
+ * twiddle(i, len), i < len): the values are the ones the butterflies would compute inline, so
+ * planned and unplanned transforms are bit-identical. RealFFT::new (realfft.rs:80-101) builds
+ * the Radix4 plan (its twiddles) and the sin_cos table once; the reference reuses one plan per
+ * track on its multi-track path (lib.rs:459-467) and re-plans per frame only when a single
+ * track is added (lib.rs:449-458). */
 #define DEFINE_FFT(T, SUF)                                                                   \
     typedef struct { T re, im; } cx_##SUF;                                                   \
     static inline cx_##SUF cadd_##SUF(cx_##SUF a, cx_##SUF b) {                              \
@@ -103,12 +109,12 @@ int or_pad_reflect_f32(const float* x, size_t n, size_t left, size_t right, floa
         v3 = rot90_##SUF(v3);                                                                \
         bfly2_##SUF(&v0, &v1); bfly2_##SUF(&v2, &v3);                                        \
         buf[0] = v0; buf[1] = v2; buf[2] = v1; buf[3] = v3; }                                \
-    static void bfly8_##SUF(cx_##SUF* buf) {                                                 \
+    static void bfly8_##SUF(cx_##SUF* buf, cx_##SUF w1, cx_##SUF w3) {                       \
         cx_##SUF s[8] = {buf[0], buf[2], buf[4], buf[6], buf[1], buf[3], buf[5], buf[7]};    \
         bfly4_##SUF(s); bfly4_##SUF(s + 4);                                                  \
-        s[5] = cmul_##SUF(s[5], twiddle_##SUF(1, 8));                                        \
+        s[5] = cmul_##SUF(s[5], w1);                       /* twiddle(1, 8) */               \
         s[6] = rot90_##SUF(s[6]);                                                            \
-        s[7] = cmul_##SUF(s[7], twiddle_##SUF(3, 8));                                        \
+        s[7] = cmul_##SUF(s[7], w3);                       /* twiddle(3, 8) */               \
         for (int i = 0; i < 4; ++i) bfly2_##SUF(&s[i], &s[i + 4]);                           \
         for (int i = 0; i < 8; ++i) buf[i] = s[i]; }                                         \
     static void prepare_radix4_##SUF(size_t size, const cx_##SUF* sig, cx_##SUF* spec,       \
@@ -124,7 +130,9 @@ int or_pad_reflect_f32(const float* x, size_t n, size_t left, size_t right, floa
                                      stride * 4);                                            \
         }                                                                                    \
     }                                                                                        \
-    static void cfft_##SUF(const cx_##SUF* in, size_t len, cx_##SUF* out) {                  \
+    /* tw: [len] twiddle(i, len); w8: {twiddle(1, 8), twiddle(3, 8)} */                      \
+    static void cfft_tab_##SUF(const cx_##SUF* in, size_t len, cx_##SUF* out,                \
+                               const cx_##SUF* tw, const cx_##SUF* w8) {                     \
         if (len == 1) { out[0] = in[0]; return; }                                            \
         if (len == 2) { out[0] = in[0]; out[1] = in[1]; bfly2_##SUF(&out[0], &out[1]); return; } \
         if (len == 4) { memcpy(out, in, 4 * sizeof(cx_##SUF)); bfly4_##SUF(out); return; }   \
@@ -132,15 +140,15 @@ int or_pad_reflect_f32(const float* x, size_t n, size_t left, size_t right, floa
         unsigned bits = 0; while (((size_t)1 << bits) < len) ++bits;                         \
         size_t cur;                                                                          \
         if (bits % 2 == 0) { for (size_t c = 0; c < len; c += 4) bfly4_##SUF(out + c); cur = 16; } \
-        else { for (size_t c = 0; c < len; c += 8) bfly8_##SUF(out + c); cur = 32; }         \
+        else { for (size_t c = 0; c < len; c += 8) bfly8_##SUF(out + c, w8[0], w8[1]); cur = 32; } \
         for (; cur <= len; cur *= 4) {                                                       \
             size_t q = cur / 4, tstride = len / cur;                                         \
             for (size_t row = 0; row < len / cur; ++row) {                                   \
                 cx_##SUF* d = out + row * cur;                                               \
                 for (size_t j = 0; j < q; ++j) { /* rustfft butterfly_4, forward */          \
-                    cx_##SUF s0 = cmul_##SUF(d[j + q], twiddle_##SUF(j * 1 * tstride, len)); \
-                    cx_##SUF s1 = cmul_##SUF(d[j + 2 * q], twiddle_##SUF(j * 2 * tstride, len)); \
-                    cx_##SUF s2 = cmul_##SUF(d[j + 3 * q], twiddle_##SUF(j * 3 * tstride, len)); \
+                    cx_##SUF s0 = cmul_##SUF(d[j + q], tw[j * 1 * tstride]);                 \
+                    cx_##SUF s1 = cmul_##SUF(d[j + 2 * q], tw[j * 2 * tstride]);             \
+                    cx_##SUF s2 = cmul_##SUF(d[j + 3 * q], tw[j * 3 * tstride]);             \
                     cx_##SUF s5 = csub_##SUF(d[j], s1);                                      \
                     d[j] = cadd_##SUF(d[j], s1);                                             \
                     cx_##SUF s3 = cadd_##SUF(s0, s2);                                        \
@@ -153,32 +161,61 @@ int or_pad_reflect_f32(const float* x, size_t n, size_t left, size_t right, floa
             }                                                                                \
         }                                                                                    \
     }                                                                                        \
+    /* RealFFT::new (realfft.rs:80-101): Radix4 twiddles of length n/2, sin_cos table */     \
+    typedef struct { size_t n, half; cx_##SUF* tw; cx_##SUF w8[2]; T* sn; T* cs; cx_##SUF* buf; } plan_##SUF; \
+    static plan_##SUF* plan_new_##SUF(size_t n) {                                            \
+        if (n % 2 || n < 2) return NULL;                                                     \
+        size_t half = n / 2;                                                                 \
+        if (half & (half - 1)) return NULL; /* Radix4 asserts a power of two */              \
+        plan_##SUF* p = (plan_##SUF*)calloc(1, sizeof(plan_##SUF));                          \
+        p->n = n; p->half = half;                                                            \
+        p->tw = (cx_##SUF*)malloc(half * sizeof(cx_##SUF));                                  \
+        for (size_t i = 0; i < half; ++i) p->tw[i] = twiddle_##SUF(i, half);                 \
+        p->w8[0] = twiddle_##SUF(1, 8); p->w8[1] = twiddle_##SUF(3, 8);                      \
+        p->sn = (T*)malloc(half * sizeof(T)); p->cs = (T*)malloc(half * sizeof(T));          \
+        const T pi = (T)M_PI; const T halflen = (T)half;                                     \
+        for (size_t k = 0; k < half; ++k) {           /* realfft.rs:88-93 */                 \
+            T ang = (T)k * pi / halflen;                                                     \
+            p->sn[k] = SUF##_sin(ang); p->cs[k] = SUF##_cos(ang);                            \
+        }                                                                                    \
+        p->buf = (cx_##SUF*)malloc((half + 1) * sizeof(cx_##SUF));                           \
+        return p;                                                                            \
+    }                                                                                        \
+    static void plan_free_##SUF(plan_##SUF* p) {                                             \
+        if (!p) return;                                                                      \
+        free(p->tw); free(p->sn); free(p->cs); free(p->buf); free(p);                        \
+    }                                                                                        \
     int or_cfft_radix4_##SUF(const T* in, size_t len, T* out) {                              \
         if (len == 0 || (len & (len - 1))) return -1;                                        \
-        cfft_##SUF((const cx_##SUF*)in, len, (cx_##SUF*)out);                                \
+        cx_##SUF* tw = (cx_##SUF*)malloc(len * sizeof(cx_##SUF));                            \
+        for (size_t i = 0; i < len; ++i) tw[i] = twiddle_##SUF(i, len);                      \
+        cx_##SUF w8[2] = {twiddle_##SUF(1, 8), twiddle_##SUF(3, 8)};                         \
+        cfft_tab_##SUF((const cx_##SUF*)in, len, (cx_##SUF*)out, tw, w8);                    \
+        free(tw);                                                                            \
         return 0;                                                                            \
     }                                                                                        \
-    /* realfft.rs:105-159 RealFFT::process */                                                \
-    int or_rfft_##SUF(const T* in, size_t n, T* out) {                                       \
-        if (n % 2 || n < 2) return -1;                                                       \
-        size_t half = n / 2;                                                                 \
-        if (half & (half - 1)) return -1; /* Radix4 asserts a power of two */                \
-        cx_##SUF* buf = (cx_##SUF*)malloc((half + 1) * sizeof(cx_##SUF));                    \
-        cfft_##SUF((const cx_##SUF*)in, half, buf); /* realfft.rs:130-138 */                 \
+    /* realfft.rs:105-159 RealFFT::process with a plan */                                    \
+    static void rfft_plan_##SUF(plan_##SUF* p, const T* in, T* out) {                        \
+        const size_t half = p->half;                                                         \
+        cx_##SUF* buf = p->buf;                                                              \
+        cfft_tab_##SUF((const cx_##SUF*)in, half, buf, p->tw, p->w8); /* realfft.rs:130-138 */ \
         buf[half] = buf[0];                                 /* realfft.rs:140 */             \
-        const T pi = (T)M_PI; const T halflen = (T)half;                                     \
         cx_##SUF* o = (cx_##SUF*)out;                                                        \
         for (size_t k = 0; k < half; ++k) { /* realfft.rs:142-156 (zip4 over rev) */         \
-            T kk = (T)k;                                                                     \
-            T ang = kk * pi / halflen;              /* realfft.rs:90-91 */                   \
-            T s = SUF##_sin(ang), c = SUF##_cos(ang);                                        \
+            T s = p->sn[k], c = p->cs[k];                                                    \
             cx_##SUF b = buf[k], r = buf[half - k];                                          \
             T xr = (T)0.5 * (((b.re + r.re) + c * (b.im + r.im)) - s * (b.re - r.re));       \
             T xi = (T)0.5 * (((b.im - r.im) - s * (b.im + r.im)) - c * (b.re - r.re));       \
             o[k].re = xr; o[k].im = xi;                                                      \
         }                                                                                    \
         o[half].re = buf[0].re - buf[0].im; o[half].im = (T)0; /* realfft.rs:157 */          \
-        free(buf);                                                                           \
+    }                                                                                        \
+    /* one RealFFT::new per call (the reference's per-frame re-plan, lib.rs:455) */          \
+    int or_rfft_##SUF(const T* in, size_t n, T* out) {                                       \
+        plan_##SUF* p = plan_new_##SUF(n);                                                   \
+        if (!p) return -1;                                                                   \
+        rfft_plan_##SUF(p, in, out);                                                         \
+        plan_free_##SUF(p);                                                                  \
         return 0;                                                                            \
     }
 
@@ -309,14 +346,15 @@ size_t or_perform_stft_f32(const float* x, size_t n, size_t win, size_t hop, siz
                            const float* window, float* out) {
     size_t T = or_frames_literal_f32(x, n, win, hop, n_fft, window, NULL);
     if (T == 0) return 0;
-    if (n_fft % 2) return 0;                           /* RealFFT::new returns Err -> unwrap */
+    plan_f32* p = plan_new_f32(n_fft);                 /* RealFFT::new returns Err -> unwrap */
+    if (!p) return 0;
     float* frames = (float*)malloc(T * n_fft * sizeof(float));
     or_frames_literal_f32(x, n, win, hop, n_fft, window, frames);
     size_t F = n_fft / 2 + 1;
-    for (size_t t = 0; t < T; ++t) {                   /* lib.rs:449-467, one plan per frame */
-        if (or_rfft_f32(frames + t * n_fft, n_fft, out + t * F * 2) != 0) { free(frames); return 0; }
-    }
+    /* lib.rs:459-467: one plan for every frame (bit-identical to a plan per frame, :449-458) */
+    for (size_t t = 0; t < T; ++t) rfft_plan_f32(p, frames + t * n_fft, out + t * F * 2);
     free(frames);
+    plan_free_f32(p);
     return T;
 }
 
@@ -697,4 +735,66 @@ void or_track_params(uint32_t sr, float win_ms, size_t t_overlap, size_t f_overl
     *hop = h <= 0.0f ? 0 : (size_t)h;
     *win = *hop * t_overlap;                           /* lib.rs:45 */
     *n_fft = or_calc_proper_n_fft(*win) * f_overlap;   /* lib.rs:46 */
+}
+
+/* ------------------------------------------------------------------------------------ */
+/* One track through the reference's spectrogram stage, the CPU baseline's unit of work:    */
+/* channel-sum downmix of interleaved PCM (lib.rs:42), perform_stft with one plan           */
+/* (lib.rs:459-467), |X| (lib.rs:124), then per `kind`: 0 |X|; 1 mel + amp dB (lib.rs:130-  */
+/* 134); 2 amp dB (lib.rs:126-129); 3 power dB (decibel.rs:91-100). out: [T, F] or [T, M].  */
+/* Returns T (0 where the reference panics).                                               */
+/* ------------------------------------------------------------------------------------ */
+size_t or_track_spec_f32(const float* pcm, size_t n, size_t channels, size_t win, size_t hop,
+                         size_t n_fft, int kind, const float* mel_fb, size_t n_mel, float* out) {
+    float* mono = (float*)malloc((n ? n : 1) * sizeof(float));
+    for (size_t i = 0; i < n; ++i) {                   /* sum_axis(Axis(0)): 0 + c0 + c1 ... */
+        float acc = 0.0f;
+        for (size_t c = 0; c < channels; ++c) acc = acc + pcm[i * channels + c];
+        mono[i] = acc;
+    }
+    size_t T = or_stft_n_frames(n, win, hop);
+    size_t F = n_fft / 2 + 1;
+    if (T == 0) { free(mono); return 0; }
+    float* X = (float*)malloc(T * F * 2 * sizeof(float));
+    if (or_perform_stft_f32(mono, n, win, hop, n_fft, NULL, X) != T) { free(mono); free(X); return 0; }
+    free(mono);
+    if (kind == 3) {
+        or_norm_sqr_f32(X, T * F, out);
+        or_power_to_db_default_f32(out, T * F);
+        free(X);
+        return T;
+    }
+    float* mag = kind == 1 ? (float*)malloc(T * F * sizeof(float)) : out;
+    or_norm_f32(X, T * F, mag);
+    free(X);
+    if (kind == 1) {
+        or_dot_f32(mag, mel_fb, T, F, n_mel, out);
+        free(mag);
+        or_amp_to_db_default_f32(out, T * n_mel);
+    } else if (kind == 2) {
+        or_amp_to_db_default_f32(out, T * F);
+    }
+    return T;
+}
+
+/* |X| of pre-built frames [T, n_fft] (rows t0..t1), each frame through RealFFT::process and
+ * norm (lib.rs:124). replan != 0: a fresh RealFFT::new per frame, the reference's single-track
+ * parallel path (lib.rs:449-458); else one plan for the rows (lib.rs:459-467). */
+int or_rfft_mag_rows_f32(const float* frames, size_t n_fft, size_t t0, size_t t1, int replan,
+                         float* out) {
+    const size_t F = n_fft / 2 + 1;
+    float* X = (float*)malloc(F * 2 * sizeof(float));
+    plan_f32* p = replan ? NULL : plan_new_f32(n_fft);
+    if (!replan && !p) { free(X); return -1; }
+    for (size_t t = t0; t < t1; ++t) {
+        if (replan) {
+            if (or_rfft_f32(frames + t * n_fft, n_fft, X) != 0) { free(X); return -1; }
+        } else {
+            rfft_plan_f32(p, frames + t * n_fft, X);
+        }
+        or_norm_f32(X, F, out + t * F);
+    }
+    plan_free_f32(p);
+    free(X);
+    return 0;
 }

@@ -112,6 +112,16 @@ int or_wav_to_image(const float* wav, size_t n, uint32_t nwidth, uint32_t nheigh
 void or_track_params(uint32_t sr, float win_ms, size_t t_overlap, size_t f_overlap,
                      size_t* win, size_t* hop, size_t* n_fft);
 
+/* ---- one track through the spectrogram stage (CPU baseline unit of work) ----
+ * interleaved PCM -> channel sum (lib.rs:42) -> perform_stft, one plan (lib.rs:459-467) -> |X|
+ * (lib.rs:124) -> kind 0 |X|, 1 mel + amp dB (lib.rs:130-134), 2 amp dB, 3 power dB. */
+size_t or_track_spec_f32(const float* pcm, size_t n, size_t channels, size_t win, size_t hop,
+                         size_t n_fft, int kind, const float* mel_fb, size_t n_mel, float* out);
+
+/* |X| of pre-built frames [T, n_fft], rows t0..t1 (replan: RealFFT::new per frame, lib.rs:455). */
+int or_rfft_mag_rows_f32(const float* frames, size_t n_fft, size_t t0, size_t t1, int replan,
+                         float* out);
+
 #ifdef __cplusplus
 }
 #endif

@@ -60,6 +60,9 @@ def lib():
             "or_resize_lanczos3_f32": (None, [_f32p, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32, _f32p]),
             "or_grey_to_rgb": (_sz, [_f32p, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32, _u8p]),
             "or_wav_to_image": (C.c_int, [_f32p, _sz, C.c_uint32, C.c_uint32, C.c_float, C.c_float, _u8p]),
+            "or_track_spec_f32": (_sz, [C.c_void_p, _sz, _sz, _sz, _sz, _sz, C.c_int, C.c_void_p, _sz,
+                                        C.c_void_p]),
+            "or_rfft_mag_rows_f32": (C.c_int, [C.c_void_p, _sz, _sz, _sz, C.c_int, C.c_void_p]),
             "or_track_params": (None, [C.c_uint32, C.c_float, _sz, _sz, C.POINTER(_sz), C.POINTER(_sz), C.POINTER(_sz)]),
         }
         for name, (res, args) in sigs.items():
@@ -219,9 +222,11 @@ def calc_mel_fb(sr, n_fft, n_mel, fmin=0.0, fmax=None, do_norm=True, dtype=np.fl
 
 def calc_mel_fb_default(sr, n_fft):
     F = n_fft // 2 + 1
-    buf = np.empty(F * F, np.float32)
-    n_mel = lib().or_calc_mel_fb_default_f32(sr, n_fft, buf.ctypes.data_as(C.c_void_p))
-    return buf[: F * n_mel].reshape(F, n_mel).copy()
+    n_mel = lib().or_calc_mel_fb_default_f32(sr, n_fft, None)  # size query
+    buf = np.empty(F * max(n_mel, 1), np.float32)
+    got = lib().or_calc_mel_fb_default_f32(sr, n_fft, buf.ctypes.data_as(C.c_void_p))
+    assert got == n_mel
+    return buf[: F * n_mel].reshape(F, n_mel)
 
 
 def dot(a, b):
@@ -282,3 +287,33 @@ def track_params(sr, win_ms=40.0, t_overlap=4, f_overlap=1):
     win, hop, nfft = _sz(), _sz(), _sz()
     lib().or_track_params(sr, win_ms, t_overlap, f_overlap, C.byref(win), C.byref(hop), C.byref(nfft))
     return win.value, hop.value, nfft.value
+
+
+TRACK_MAG, TRACK_MEL_DB, TRACK_AMP_DB, TRACK_POWER_DB = 0, 1, 2, 3
+
+
+def track_spec(pcm, win, hop, n_fft, kind, mel_fb=None):
+    """or_track_spec_f32: interleaved f32 PCM [n, ch] (or [n]) through the whole spectrogram
+    stage in one C call (the GIL is released: the CPU baseline runs these on a thread pool)."""
+    pcm = _c32(pcm)
+    n = pcm.shape[0]
+    ch = 1 if pcm.ndim == 1 else pcm.shape[1]
+    T = lib().or_stft_n_frames(n, win, hop)
+    if T == 0:
+        raise ValueError("reference panics for this (n, win, hop)")
+    fb = None if mel_fb is None else _c32(mel_fb)
+    cols = fb.shape[1] if kind == TRACK_MEL_DB else n_fft // 2 + 1
+    out = np.empty((T, cols), np.float32)
+    got = lib().or_track_spec_f32(pcm.ctypes.data, n, ch, win, hop, n_fft, kind,
+                                  None if fb is None else fb.ctypes.data, 0 if fb is None else fb.shape[1],
+                                  out.ctypes.data)
+    assert got == T, (got, T)
+    return out
+
+
+def rfft_mag_rows(frames, t0, t1, out, replan=True):
+    """|rfft| of frames[t0:t1] into out[t0:t1] (frames [T, n_fft], out [T, F] f32, C-contiguous;
+    one C call, the GIL released)."""
+    assert frames.flags.c_contiguous and out.flags.c_contiguous and frames.dtype == np.float32
+    rc = lib().or_rfft_mag_rows_f32(frames.ctypes.data, frames.shape[1], t0, t1, int(replan), out.ctypes.data)
+    assert rc == 0

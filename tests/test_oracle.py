@@ -75,9 +75,12 @@ def test_mel_works_is_stale_slaney(kats):
     assert np.abs(unit_sum[:8, 0] - np.array(k["first8_of_filter0"])).max() > 1e-3  # stale
 
 
-@pytest.mark.parametrize("sr", [400, 1000, 8000, 16000, 24000, 44100, 48000, 96000])
-def test_mel_default_property(sr):  # mel.rs:135-165 (n_fft 2^5 .. 2^12 here for time)
-    for e in range(5, 13):
+@pytest.mark.parametrize("sr", [400, 800, 1000, 2000, 4000, 8000, 16000, 24000, 44100, 48000,
+                                88200, 96000])
+def test_mel_default_property(sr, kats):  # mel.rs:135-165: the reference's whole grid
+    k = kats["mel_default_property"]
+    assert sr in k["srs"]
+    for e in range(*k["n_fft_exp"]):  # n_fft 2^5 .. 2^14
         n_fft = 2 ** e
         fb = O.calc_mel_fb_default(sr, n_fft)
         assert (fb.sum(axis=0) > 0).all()
@@ -150,3 +153,22 @@ def test_resize_identity_weights_sum_to_one():
     assert out.shape == (40, 11)
     const = np.full((17, 29), 0.5, np.float32)
     assert np.abs(O.resize_lanczos3(const, 13, 7) - 0.5).max() < 1e-6
+
+
+@pytest.mark.parametrize("channels", [1, 2])
+def test_track_spec_is_the_composition(channels):
+    """or_track_spec_f32 (the CPU baseline's one call per track, one FFT plan per track as
+    lib.rs:459-467) equals the composition of the oracle's functions bit for bit."""
+    rng = np.random.default_rng(channels)
+    pcm = (rng.standard_normal((30011, channels)) * 0.3).astype(np.float32)
+    mono = np.zeros(pcm.shape[0], np.float32)
+    for c in range(channels):
+        mono = (mono + pcm[:, c]).astype(np.float32)
+    X = O.perform_stft(mono, 2048, 512, 2048)
+    fb = O.calc_mel_fb(48000, 2048, 128)
+    cases = {O.TRACK_MAG: O.norm(X), O.TRACK_MEL_DB: O.amp_to_db_default(O.dot(O.norm(X), fb)),
+             O.TRACK_AMP_DB: O.amp_to_db_default(O.norm(X)),
+             O.TRACK_POWER_DB: O.power_to_db_default(O.norm_sqr(X))}
+    for kind, ref in cases.items():
+        got = O.track_spec(pcm, 2048, 512, 2048, kind, fb if kind == O.TRACK_MEL_DB else None)
+        assert got.view(np.uint32).tolist() == ref.view(np.uint32).tolist(), kind
