@@ -31,6 +31,8 @@ import time
 ROOT = os.path.dirname(os.path.abspath(__file__))
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s HBM3E (spec)
 METRIC = "STFT frames/sec (n_fft=2048 hop=512) at 1/2/4/8 GPUs; % HBM roofline"
+KERNEL_NAMES = {1: "thesia::stft_kernel (general)", 2: "thesia::stft2_kernel (general, 4 waves/SIMD)",
+                3: "thesia::stft3_kernel (streaming)", 5: "thesia::stft5_kernel (streaming, n_fft 2048)"}
 
 
 def parse():
@@ -58,6 +60,9 @@ def parse():
                    help="CPU baseline threads (0: OMP_NUM_THREADS if set, else the affinity mask)")
     p.add_argument("--variants", default="", help="experiment (needs THESIA_LIB=lib/libthesia_exp.so): "
                    "comma list of THESIA_STFT_VARIANT values to A/B (interleaved rounds, one process)")
+    p.add_argument("--kernel", type=int, default=0, help="force a fused kernel (1/2/3/5; 0 = automatic)")
+    p.add_argument("--kernels", default="", help="A/B of named kernels on the product library: comma list "
+                   "of kernel ids (interleaved rounds, one process), e.g. 3,5")
     p.add_argument("--selftest", action="store_true",
                    help="launcher / reduction plumbing only: no GPU, no thesia (CPU tests)")
     p.add_argument("--selftest-fail-rank", type=int, default=-1, help=argparse.SUPPRESS)
@@ -291,9 +296,11 @@ def rfft_roofline(args, din, offs, lens, fmt, n_local, n_samples):
     plan = engine.Plan(args.n_fft, args.n_fft, args.hop, engine.OUT_COMPLEX, sr=args.sr)
     frames = engine.Batch.frames_for(plan, lens)
     dout = engine.DeviceBuffer(frames * plan.row_bins * 8)
-    b = engine.Batch(plan, din, offs, lens, dout, input_format=fmt, channels=args.channels)
+    b = engine.Batch(plan, din, offs, lens, dout, input_format=fmt, channels=args.channels,
+                     kernel=args.kernel)
     b.run_timed(2)
     kms = b.run_timed(5) / 5
+    kname = KERNEL_NAMES.get(b.kernel, "?")
     in_el = 4 if args.input == "f32" else 2
     abytes = n_local * n_samples * args.channels * in_el + frames * plan.row_bins * 8
     achieved = abytes / (kms * 1e-3) / 1e9
@@ -302,7 +309,7 @@ def rfft_roofline(args, din, offs, lens, fmt, n_local, n_samples):
     return {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": achieved / HBM_PEAK_GBS, "kernel_ms": kms, "algorithmic_bytes_per_launch": abytes,
             "frames_per_s": frames / (kms * 1e-3),
-            "kernel": "thesia::stft3_kernel, complex output (downmix+frame+window+rFFT)"}
+            "kernel": kname + ", complex output (downmix+frame+window+rFFT)"}
 
 
 def traffic_from_profile(workload_key):
@@ -446,7 +453,8 @@ def main_worker(args):
     lens = np.full(n_local, n_samples, np.uint64)
     frames = engine.Batch.frames_for(plan, lens)
     dout = engine.DeviceBuffer(frames * plan.row_bins * (8 if kind == engine.OUT_COMPLEX else 4))
-    batch = engine.Batch(plan, din, offs, lens, dout, input_format=fmt, channels=args.channels)
+    batch = engine.Batch(plan, din, offs, lens, dout, input_format=fmt, channels=args.channels,
+                         kernel=args.kernel)
     assert batch.total_frames == frames
 
     for _ in range(args.warmup):
@@ -474,6 +482,19 @@ def main_worker(args):
         if rank == 0:
             print(json.dumps({"variants_kernel_ms": {str(v): {"median": float(np.median(t)), "min": float(min(t))}
                                                      for v, t in res.items()}}), flush=True)
+
+    if args.kernels:
+        ks = [int(v) for v in args.kernels.split(",")]
+        res = {k: [] for k in ks}
+        for _ in range(5):  # interleaved rounds
+            for k in ks:
+                batch.set_option(engine.OPT_KERNEL, k)
+                batch.run_timed(1)
+                res[k].append(batch.run_timed(3) / 3)
+        batch.set_option(engine.OPT_KERNEL, args.kernel)
+        if rank == 0:
+            print(json.dumps({"kernels_ms": {str(k): {"median": float(np.median(t)), "min": float(min(t))}
+                                             for k, t in res.items()}}), flush=True)
 
     # kernel duration from HIP events on the launch stream (roofline numerator / denominator)
     kms = batch.run_timed(max(args.steps, 5)) / max(args.steps, 5)
@@ -519,8 +540,7 @@ def main_worker(args):
             "unit": "GB/s",
             "frac": achieved / HBM_PEAK_GBS,
             "traffic": traffic_from_profile(wkey),
-            "kernel": {1: "thesia::stft_kernel (general)", 2: "thesia::stft2_kernel (general, 4 waves/SIMD)",
-                       3: "thesia::stft3_kernel (streaming)"}.get(batch.kernel, "?")
+            "kernel": KERNEL_NAMES.get(batch.kernel, "?")
                       + ": downmix+frame+window+rFFT+" + {"mel_db": "|X|+mel+dB", "amp_db": "|X|+dB",
                                                            "power_db": "|X|^2+dB", "complex": "complex out"}[args.output]
                       + ", one launch",

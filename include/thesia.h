@@ -170,20 +170,22 @@ int thesia_batch_kernel_info(const thesia_batch* batch, int* lds_bytes, int* til
                              int* grid);
 
 /* Which fused kernel runs the batch: 1 stft_kernel (general), 2 stft2_kernel (4 waves/SIMD),
- * 3 stft3_kernel (streaming; win = n_fft, hop = n_fft/4). */
+ * 3 stft3_kernel (streaming; win = n_fft, hop = n_fft/4), 5 stft5_kernel (streaming, n_fft 2048:
+ * untangle pairs co-resident in a lane). */
 int thesia_batch_kernel(const thesia_batch* batch, int* kernel);
 
 /* Named alternatives of a batch (none changes what is computed, only how; all results stay
  * within the parity contract). Not part of the reference surface. */
 typedef enum {
-    /* 0 = automatic (streaming kernel where its geometry allows), 1 / 2 / 3 = force that
+    /* 0 = automatic (streaming kernel where its geometry allows), 1 / 2 / 3 / 5 = force that
      * kernel (THESIA_ERR_UNSUPPORTED if it cannot run the geometry) */
     THESIA_BATCH_OPT_KERNEL = 1,
     /* at most this many workgroups per launch (0 = one full occupancy wave of the device);
      * small values make every frame stream walk many frames */
     THESIA_BATCH_OPT_MAX_BLOCKS = 2,
     /* 1 = the other output-row store method of the streaming kernel (LDS-staged 16-byte stores
-     * for complex rows / lane-wise stores for linear rows; n_fft 2048 stereo f32 only) */
+     * for complex rows / lane-wise stores for linear rows; stft3_kernel at n_fft 2048 stereo
+     * f32 only) */
     THESIA_BATCH_OPT_ROW_STORE = 3
 } thesia_batch_option;
 int thesia_batch_set_option(thesia_batch* batch, int option, int64_t value);

@@ -233,6 +233,38 @@ static int build_mel4(Plan* p) {
     if (!rc) rc = p->mel4_wt.upload(wt.data(), wt.size() * sizeof(float));
     p->mel4_rounds = (int)R;
     p->mel4_wt_rows = rows;
+    // the same rounds as one stream of 4-step chunks (stft5 mel4p)
+    {
+        std::vector<int> xo;
+        bool ok = true;
+        for (size_t r = 0; r < R && ok; ++r) {
+            const int nch = rounds[r].y / 4;
+            if (rounds[r].y <= 0 || rounds[r].y % 4 != 0 || rounds[r].x != (int)(xo.size() / L) * 4) ok = false;
+            for (int cc = 0; cc < nch && ok; ++cc)
+                for (int j = 0; j < L; ++j) {
+                    const int km = k0m[r * L + j];
+                    const int v = ((km & 0xFFFF) + 16 * cc) | (((km >> 16) & 0x7FFF) << 16) |
+                                  (cc == nch - 1 ? (int)0x80000000u : 0);
+                    xo.push_back(v);
+                }
+        }
+        // the kernel runs a fixed 4 or 8 chunks (no guards: guarded loads made the compiler's
+        // LDS wait counts assume the shorter path); padding chunks read bin 0 with zero weights
+        // and never emit
+        const int C = ok ? (int)(xo.size() / L) : 0;
+        const int CP = C == 0 || C > 8 ? 0 : C <= 4 ? 4 : 8;
+        if (CP) {
+            xo.resize((size_t)CP * L, 0);
+            if (rows < (size_t)CP * 4) {
+                wt.resize((size_t)CP * 4 * L * 4, 0.0f);
+                rows = (size_t)CP * 4;
+                p->mel4_wt_rows = rows;
+                if (!rc) rc = p->mel4_wt.upload(wt.data(), wt.size() * sizeof(float));
+            }
+        }
+        p->mel_chunks = CP;
+        if (!rc && p->mel_chunks) rc = p->mel_xo.upload(xo.data(), xo.size() * sizeof(int));
+    }
     return rc;
 }
 
@@ -418,13 +450,18 @@ int batch_create(Plan* plan, const thesia_batch_desc& d, Batch** out) {
     L.mel4_round = plan->mel4_round.as<int2>();
     L.mel4_k0 = plan->mel4_k0.as<int>();
     L.mel4_wt = plan->mel4_wt.as<float4>();
+    L.mel_chunks = plan->mel_chunks;
+    L.mel_xo = plan->mel_xo.as<int>();
     L.out = d.d_output;
     // kernel choice: the streaming kernel for its geometry, else the 4-waves/SIMD kernel for
     // its sizes, else the general one (thesia_batch_set_option can force another one)
     b->k3_ok = plan->use_v2 && stft3_supports((int)plan->n_fft, (int)plan->win, (int)plan->hop,
                                               d.input_format, (int)d.channels) &&
                stft3_lds_bytes(L) <= 163840;  // the mel weights must fit LDS (else stft2)
-    b->kernel = b->k3_ok ? 3 : plan->use_v2 ? 2 : 1;
+    b->k5_ok = b->k3_ok && stft5_supports((int)plan->n_fft, (int)plan->win, (int)plan->hop,
+                                          d.input_format, (int)d.channels) &&
+               stft5_lds_bytes(L) <= 163840;
+    b->kernel = b->auto_kernel();
     if (hipEventCreate(&b->ev0) != hipSuccess || hipEventCreate(&b->ev1) != hipSuccess) {
         delete b;
         return set_error(THESIA_ERR_DEVICE, "hipEventCreate failed");
@@ -436,10 +473,11 @@ int batch_create(Plan* plan, const thesia_batch_desc& d, Batch** out) {
 int batch_set_option(Batch* b, int option, int64_t value) {
     switch (option) {
         case THESIA_BATCH_OPT_KERNEL:
-            if (value == 0) b->kernel = b->k3_ok ? 3 : b->plan->use_v2 ? 2 : 1;
+            if (value == 0) b->kernel = b->auto_kernel();
             else if (value == 1) b->kernel = 1;
             else if (value == 2 && stft2_supports((int)b->plan->n_fft)) b->kernel = 2;
             else if (value == 3 && b->k3_ok) b->kernel = 3;
+            else if (value == 5 && b->k5_ok) b->kernel = 5;
             else return set_error(THESIA_ERR_UNSUPPORTED, "kernel " + std::to_string(value) +
                                                              " does not run this batch's geometry");
             return THESIA_OK;
@@ -447,6 +485,11 @@ int batch_set_option(Batch* b, int option, int64_t value) {
             if (value < 0 || value > (1 << 30)) return set_error(THESIA_ERR_INVALID_ARG, "max_blocks out of range");
             b->launch.grid = (int)value;
             return THESIA_OK;
+#ifdef THESIA_STAMPS
+        case 100:  // diagnostic build: device buffer for the stft5 phase stamps (scripts/stamps.py)
+            b->launch.stamps = reinterpret_cast<unsigned long long*>(value);
+            return THESIA_OK;
+#endif
         case THESIA_BATCH_OPT_ROW_STORE:
             if (value < 0 || value > 1) return set_error(THESIA_ERR_INVALID_ARG, "row_store must be 0 or 1");
             b->launch.row_alt = (int)value;
@@ -459,7 +502,8 @@ int batch_set_option(Batch* b, int option, int64_t value) {
 int batch_run(Batch* b, hipStream_t s) {
     if (!s) s = default_stream();
     int rc = -2;
-    if (b->kernel >= 3) rc = launch_stft3(b->launch, s);
+    if (b->kernel == 5) rc = launch_stft5(b->launch, s);
+    if (rc == -2 && b->kernel >= 3) rc = launch_stft3(b->launch, s);
     if (rc == -2 && b->kernel >= 2) rc = launch_stft2(b->launch, s);
     if (rc == -2) rc = launch_stft(b->launch, s);
     if (rc == -2) return set_error(THESIA_ERR_UNSUPPORTED, "unsupported n_fft");

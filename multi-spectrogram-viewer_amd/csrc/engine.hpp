@@ -63,6 +63,8 @@ struct Plan {
     size_t mel_wt_rows = 0;  // padded band lengths summed over the rounds
     DevBuf mel4_round, mel4_k0, mel4_wt;  // stft2_kernel layout (float4 steps)
     int mel4_rounds = 0;
+    DevBuf mel_xo;      // the rounds as a chunk stream (kernels.hpp mel_xo)
+    int mel_chunks = 0;
     size_t mel4_wt_rows = 0;
     bool use_v2 = false;  // stft2_kernel runs this plan (n_fft 256..2048)
     size_t row_bins() const;
@@ -78,8 +80,12 @@ struct Batch {
     DevBuf d_in_off, d_len, d_frame0;
     uint64_t total_frames = 0;
     StftLaunch launch{};
-    int kernel = 1;  // 1 stft_kernel, 2 stft2_kernel, 3 stft3_kernel (streaming)
+    int kernel = 1;  // 1 stft_kernel, 2 stft2_kernel, 3 stft3_kernel, 5 stft5_kernel (streaming)
     bool k3_ok = false;  // the streaming kernel supports this batch's geometry
+    bool k5_ok = false;  // ... and so does its n_fft 2048 variant (stft5_kernel)
+    // automatic choice: stft5 for n_fft 2048, stft3 for its other streaming geometries, then
+    // the 4-waves/SIMD kernel for its sizes, else the general one
+    int auto_kernel() const { return k5_ok ? 5 : k3_ok ? 3 : plan->use_v2 ? 2 : 1; }
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     ~Batch();
 };

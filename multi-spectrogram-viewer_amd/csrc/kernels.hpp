@@ -62,11 +62,19 @@ struct StftLaunch {
     const int2* mel4_round = nullptr;
     const int* mel4_k0 = nullptr;
     const float4* mel4_wt = nullptr;
+    // the same rounds as one stream of 4-step chunks (stft5's pipelined mel, mel4p): chunk c
+    // reads weight rows 4c .. 4c+3 (the rounds' rows are contiguous) and, in lane j, the |X|
+    // floats from mel_xo[c*L + j] & 0xFFFF; bits 16..30 hold the lane's mel, bit 31 marks the
+    // last chunk of its round. 0 chunks when the plan does not fit (<= 8 chunks).
+    int mel_chunks = 0;
+    const int* mel_xo = nullptr;
     // output
     void* out = nullptr;  // packed rows: frame g at out + g * row_elems
     // scheduling / named alternatives (thesia_batch_set_option)
     int grid = 0;     // 0 => computed from occupancy, else at most this many blocks
     int row_alt = 0;  // 1: the other row-store method (stft3 n_fft 2048 stereo f32)
+    // diagnostic builds only (-DTHESIA_STAMPS, scripts/stamps.py): per-wave phase cycle sums
+    unsigned long long* stamps = nullptr;
 };
 
 // Returns 0 on success, -2 for an unsupported n_fft.
@@ -80,6 +88,10 @@ int stft2_kernel_info(int n_fft, int* lds_bytes, int* tile_frames, int* lanes_pe
 int launch_stft3(const StftLaunch& a, hipStream_t stream);
 bool stft3_supports(int n_fft, int win, int hop, int in_format, int channels);
 int stft3_lds_bytes(const StftLaunch& a);  // dynamic LDS of the launch (> 163840: cannot run)
+// stft5_kernel (streaming, n_fft 2048 only, co-resident untangle pairs; stft5_kernels.hip)
+int launch_stft5(const StftLaunch& a, hipStream_t stream);
+bool stft5_supports(int n_fft, int win, int hop, int in_format, int channels);
+int stft5_lds_bytes(const StftLaunch& a);
 // LDS bytes / frames per block pass / lanes per frame of the kernel for n_fft.
 int stft_kernel_info(int n_fft, int* lds_bytes, int* tile_frames, int* lanes_per_frame);
 

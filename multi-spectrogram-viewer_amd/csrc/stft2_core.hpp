@@ -411,6 +411,65 @@ __device__ __forceinline__ void mel4(const StftLaunch& a, const float* region, c
     for (int r = PR; r < R; ++r) round(rounds[r], k0[r * L + j]);
 }
 
+// mel4 as a software pipeline (a.mel_chunks = CMAX = 4 or 8: the rounds as a stream of 4-step chunks,
+// engine.cpp build_mel4): the 8 LDS reads of chunk c + 1 are issued before the fma chain of
+// chunk c, so a chunk's LDS latency hides under the previous chunk's chain instead of stalling
+// the wave once per batch (stamps: the mel phase spent 2/3 of its cycles waiting). Chunk c reads
+// weight rows 4c..4c+3 (immediate offsets) and the |X| floats at xo[c] & 0xFFFF; the per-lane
+// chunk words come from one LDS round trip up front. Same k-ascending chain per mel as mel4
+// (bit-exact with it).
+template <int NC, int CMAX>
+__device__ __forceinline__ void mel4p(const StftLaunch& a, const float* region, const float4* wt,
+                                      const int* xo_tab, int j, uint64_t g, bool valid) {
+    constexpr int L = Geo2<NC>::L;
+    const int n_mels = a.n_mels;
+    const bool db = a.out_kind == OUT_MEL_AMP_DB;
+    float* out = static_cast<float*>(a.out) + g * (uint64_t)n_mels;
+    // a.mel_chunks == CMAX (the host pads the stream to 4 or 8 chunks)
+    int xo[CMAX];
+#pragma unroll
+    for (int c = 0; c < CMAX; ++c) xo[c] = xo_tab[c * L + j];
+    const float4* wp = wt + j;
+    auto load = [&](auto cc, float4 (&w)[4], float4 (&x)[4]) {
+        constexpr int c = decltype(cc)::value;
+        const float4* xp = reinterpret_cast<const float4*>(region + (xo[c] & 0xFFFF));
+#pragma unroll
+        for (int u = 0; u < 4; ++u) w[u] = wp[(4 * c + u) * L];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) x[u] = xp[u];
+    };
+    float acc = 0.0f;
+    auto chain = [&](auto cc, const float4 (&w)[4], const float4 (&x)[4]) {
+        constexpr int c = decltype(cc)::value;
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            acc = __builtin_fmaf(x[u].x, w[u].x, acc);
+            acc = __builtin_fmaf(x[u].y, w[u].y, acc);
+            acc = __builtin_fmaf(x[u].z, w[u].z, acc);
+            acc = __builtin_fmaf(x[u].w, w[u].w, acc);
+        }
+        if (xo[c] < 0) {  // the round's last chunk: this lane's mel is done
+            const int m = (xo[c] >> 16) & 0x7FFF;
+            if (valid && m < n_mels) st_out(out + m, db ? db_of(acc, a.log_amin, 1e-18f, 20.0f) : acc);
+            acc = 0.0f;
+        }
+    };
+    float4 w0[4], x0[4], w1[4], x1[4];
+    load(std::integral_constant<int, 0>{}, w0, x0);
+    static_for<0, CMAX>([&](auto cc) {
+        constexpr int c = decltype(cc)::value;
+        if constexpr (c + 1 < CMAX) {
+            if constexpr ((c & 1) == 0) load(std::integral_constant<int, c + 1>{}, w1, x1);
+            else load(std::integral_constant<int, c + 1>{}, w0, x0);
+        }
+        // keep the next chunk's reads ahead of this chunk's chain (the scheduler would sink
+        // them next to their use and the pipeline would collapse)
+        __builtin_amdgcn_sched_barrier(0);
+        if constexpr ((c & 1) == 0) chain(cc, w0, x0);
+        else chain(cc, w1, x1);
+    });
+}
+
 // previous mel4 (per-round dependent setup reads), kept for in-process A/B (stft3 VAR bit6)
 template <int NC, int U = 4>
 __device__ __forceinline__ void mel4_v1(const StftLaunch& a, const float* region, const float4* wt,

@@ -14,96 +14,13 @@
 // hides under the previous frame's FFT. Frames whose new samples cross a track end (reflect
 // padding, lib.rs:410-435) or start a stream / track reload all n_fft samples (direct or
 // reflected). The mel weights are copied into LDS once per block.
-#include "stft2_core.hpp"
+#include "stft3_core.hpp"
 
 #include <cstdlib>
 #include <type_traits>
 
 namespace thesia {
 
-// WV waves per block, one block per CU: WV / 4 waves per SIMD (8: 2 waves/SIMD, 256 VGPRs;
-// 12: 3 waves/SIMD, 168 VGPRs).
-template <int NC, int WV = kWaves>
-struct Geo3 {
-    using G2 = Geo2<NC>;
-    static constexpr int L = G2::L, P = G2::P, FPW = G2::FPW;
-    // the wide (ds_read_b128) transpose for the headline size, L = 32 (fft2 WIDE)
-    static constexpr bool WIDE = L == 32;
-    static constexpr int RS = WIDE ? (P * fft2_stride<NC>(true) + 3) / 4 * 4 : G2::RS;
-    static constexpr int SH = P / 4;                      // points per lane a hop moves
-    static constexpr int BLOCK = 64 * WV;
-    static constexpr int STREAMS = WV * FPW;              // streams (= frames in flight) per block
-    static constexpr int TW_FLOATS = 2 * P * L;           // W_NC^{j*k1}, [P][L] float2
-    // window per lane: row j holds (w[2m], w[2m+1]) for m = L*n1 + j, n1 < P, read as float4;
-    // row stride 2P + 4 floats keeps 16 lanes of a ds_read_b128 group on distinct banks
-    static constexpr int WL_STRIDE = 2 * P + 4;
-    static constexpr int WL_FLOATS = L * WL_STRIDE;
-    static constexpr int BASE_FLOATS = WL_FLOATS + TW_FLOATS + STREAMS * RS;
-    // linear / complex kinds stage the whole output row in the stream's region (plus up to 3
-    // floats of alignment shift) so it leaves as 16-byte aligned stores
-    static constexpr int ROW_FLOATS_OK(int ok) { return ok == 0 ? 2 * G2::F : G2::F; }
-    static constexpr int RS_OK(bool staged, int ok) {
-        return !staged ? RS : (RS > (ROW_FLOATS_OK(ok) + 3 + 3) / 4 * 4 ? RS : (ROW_FLOATS_OK(ok) + 3 + 3) / 4 * 4);
-    }
-    static constexpr int BASE_FLOATS_OK(bool staged, int ok) { return WL_FLOATS + TW_FLOATS + STREAMS * RS_OK(staged, ok); }
-    static_assert(P % 4 == 0, "hop = n_fft/4 must move whole points per lane");
-};
-
-// Which kinds stage their output row (measured): linear kinds yes (power dB 6.25
-// vs 6.58 ms), complex no (7.50 vs 7.41 ms; HBM write traffic equals the algorithmic bytes
-// either way). VAR bit10 flips the choice.
-constexpr bool stage_rows(int ok, int var) {
-    return ok == 1 ? (var & 1024) == 0 : ok == 0 ? (var & 1024) != 0 : false;
-}
-
-// A row of nfl floats staged in LDS (row element e at stage[sh + e], sh = the row's global
-// float offset mod 4) written with 16-byte aligned stores: whole float4 chunks from the L lanes
-// of the frame, the row's partial first/last chunk float by float. Rows of 1025 floats
-// (linear kinds) or 1025 float2 (complex) are not 16-byte aligned, so lane-wise 4- or 8-byte
-// stores of them leave partial 64-byte segments that HBM writes back twice.
-template <int L>
-__device__ __forceinline__ void store_row_b128(float* row, int sh, const float* stage, int nfl, int j) {
-    float* ab = row - sh;  // 16-byte aligned
-    const int nch = (sh + nfl + 3) >> 2;
-    for (int i = j; i < nch; i += L) {
-        const int e0 = 4 * i;
-        if (e0 >= sh && e0 + 4 <= sh + nfl) {
-            const float4 v = *reinterpret_cast<const float4*>(__builtin_assume_aligned(stage + e0, 16));
-            *reinterpret_cast<float4*>(__builtin_assume_aligned(ab + e0, 16)) = v;
-        } else {
-#pragma unroll
-            for (int e = 0; e < 4; ++e)
-                if (e0 + e >= sh && e0 + e < sh + nfl) ab[e0 + e] = stage[e0 + e];
-        }
-    }
-}
-
-// Reflect-padded, downmixed samples of a frame (no window): the uniform rule of
-// load_frame_generic (stft_common.hpp) for win = n_fft.
-template <int NC, int INF>
-__device__ __forceinline__ void load_raw_generic(const StftLaunch& a, float* region, int j,
-                                                 int64_t start, int64_t n, uint64_t base, int C,
-                                                 bool fold, float2 (&raw)[Geo2<NC>::P]) {
-    constexpr int L = Geo2<NC>::L, P = Geo2<NC>::P;
-#pragma unroll
-    for (int e = 0; e < 2; ++e) {
-        wave_lds_sync();
-        for (int n1 = 0; n1 < P; ++n1) {
-            const int m = L * n1 + j;
-            int64_t i = start + 2 * m + e;
-            if (i < 0) i = -i;
-            if (i > n - 1) i = 2 * (n - 1) - i;
-            i = i < 0 ? 0 : (i > n - 1 ? n - 1 : i);
-            region[m] = read_sample<INF>(a.in, base, i, C, fold);
-        }
-        wave_lds_sync();
-        static_for<0, P>([&](auto ic) {
-            constexpr int n1 = decltype(ic)::value;
-            const float r = region[L * n1 + j];
-            if (e == 0) raw[n1].x = r; else raw[n1].y = r;
-        });
-    }
-}
 
 // OK: 0 complex, 1 linear kinds, 2 mel kinds. C: 1 mono, 2 stereo (interleaved); INF: f32 / s16.
 // VAR (experiments, THESIA_STFT_VARIANT): bit0 = per-pair partner exchange instead of the

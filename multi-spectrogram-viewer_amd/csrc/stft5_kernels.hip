@@ -1,0 +1,504 @@
+// stft5_kernels.hip -- the streaming STFT kernel for n_fft 2048 (NC = 1024 complex points),
+// win = n_fft, hop = n_fft/4: the headline geometry of BASELINE.json (configs C2-C5).
+//
+// Same contract and the same streaming register ring as stft3_kernel (stft3_kernels.hip: each
+// wave runs two frame streams on its 32-lane halves; a stream's downmixed samples stay in
+// registers and a hop loads only its new samples). What changes is the second FFT stage, so
+// that the realfft untangle (realfft.rs:140-157) needs no cross-lane exchange, and with it the
+// register budget, so that THREE waves share a SIMD (168 VGPRs) instead of two:
+//
+//   NC = 32 x 32. Stage 1 (lane j = n2): Y[j][k1] = DFT-32 over n1 of z[32 n1 + j], times
+//   W_1024^{j k1}; LDS transpose. In stft3, lane j then runs the DFT-32 of column k1 = j and
+//   holds the bins k = j + 32 k2, whose untangle partners NC - k = (32 - j) + 32 (31 - k2) live
+//   in lane 32 - j (one ds_bpermute per value). Here lane j reads TWO transpose rows, its own
+//   column A = j and the partner column B = (32 - j) mod 32, and splits both DFT-32s by their
+//   first radix-2 step: the even outputs of A (a DFT-16 of A[n] + A[n+16]) and the odd outputs
+//   of B (a DFT-16 of (B[n] - B[n+16]) W_32^n). Bin A + 64 i = E[i] then pairs with
+//   NC - A - 64 i = B + 32 (31 - 2 i) = O[15 - i] in the same lane. The arithmetic is that of
+//   one DFT-32 per lane, as before; the exchange becomes 8 more ds_read_b128 per transpose pass.
+//   Lane 0 (A = B = 0) pairs its own outputs differently (O with O, E with E, E[0] and E[8]
+//   with themselves: bins 0, NC and NC/2); per-slot selects cover it, as in stft3.
+//
+// Registers: no partner batch (32 VGPRs in stft3), the stage-1 twiddles read 4 float4 at a
+// time, the next hop's loads issued after the transposes (when the frame's registers are at
+// their fewest), the sqrt batch per half frame: 3 waves per SIMD, 12 waves (24 streams) per
+// CU. The two frames of a wave keep their LDS regions on opposite halves of the 64 banks.
+#include "stft3_core.hpp"
+
+#include <type_traits>
+
+namespace thesia {
+
+#ifdef THESIA_MARKS
+#define MARK5(x, i) asm volatile("; MARK " #x)
+#elif defined(THESIA_STAMPS)
+// diagnostic build (scripts/stamps.py): the cycles since the previous mark go to phase i
+#define MARK5(x, i)                                                                        \
+    do {                                                                                   \
+        __builtin_amdgcn_sched_barrier(0);                                                 \
+        unsigned long long t_;                                                             \
+        asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_)::"memory");         \
+        __builtin_amdgcn_sched_barrier(0);                                                 \
+        st_acc[i] += t_ - st_last;                                                         \
+        st_last = t_;                                                                      \
+    } while (0)
+#else
+#define MARK5(x, i)
+#endif
+
+#ifndef THESIA_WV5
+#define THESIA_WV5 8
+#endif
+#ifndef THESIA_TWC5
+#define THESIA_TWC5 8
+#endif
+struct Geo5 {
+    static constexpr int NC = 1024, L = 32, P = 32, FPW = 2, F = NC + 1, SH = P / 4;
+    static constexpr int S = L + 4;       // transpose row stride (16 lanes of a b128 read: distinct banks)
+    static constexpr int WV = THESIA_WV5;  // waves per block: 4 per SIMD x WV/4
+    static constexpr int BLOCK = 64 * WV;
+    static constexpr int STREAMS = WV * FPW;
+    // region per stream: the transpose (P * S = 1152 floats), the |X| row (1028) or a staged
+    // linear row (F + 6); RS = 1184 = 32 mod 64 puts the wave's two frames on opposite bank
+    // halves (RS_MIN when the mel weights leave no room for it)
+    static constexpr int RS = 1184, RS_MIN = 1152;
+    static constexpr int WL_STRIDE = 2 * P + 4, WL_FLOATS = L * WL_STRIDE;
+    static constexpr int TW_FLOATS = 2 * P * L;
+    static constexpr int TAB_FLOATS = WL_FLOATS + TW_FLOATS;
+    static constexpr int TWC = THESIA_TWC5;  // stage-1 twiddle float4 reads per batch
+    static constexpr int PF_POS = WV == 8 ? 0 : 2;  // where the next hop's loads issue
+    static_assert(RS_MIN >= P * S && RS_MIN >= F + 6 && RS_MIN % 4 == 0 && RS % 4 == 0, "region");
+};
+
+// (sin, cos)(pi (kb + 64 i) / NC) from the lane's base (sin, cos)(pi kb / NC): rotation by
+// pi i / 16, compile-time constants (f64-rounded), as stft3's untangle does per 32 bins.
+template <int I>
+__device__ __forceinline__ void rot16(float2 ub, float& s, float& co) {
+    if constexpr (I == 0) {
+        s = ub.x;
+        co = ub.y;
+    } else {
+        constexpr float cb = ce_tw_re(I, 32);
+        constexpr float sb = -ce_tw_im(I, 32);
+        s = __builtin_fmaf(ub.x, cb, ub.y * sb);
+        co = __builtin_fmaf(ub.y, cb, -(ub.x * sb));
+    }
+}
+
+// The realfft untangle of slots I0 <= i < I1 (see the header): calls
+// epi(k, re, im, integral_constant<2 (i - I0) + h>) for bin k (h = 0) and NC - k (h = 1).
+// v[ce_pos(16, i)] = E[i], v[16 + ce_pos(16, i)] = O[i].
+template <int I0, int I1, class Epi>
+__device__ __forceinline__ void untangle5(const float2 (&v)[32], bool lane0, float2 ub_lo,
+                                          float2 ub_hi, int kb_lo, int j, Epi&& epi) {
+    constexpr int NC = Geo5::NC;
+    static_for<I0, I1>([&](auto ic) {
+        constexpr int i = decltype(ic)::value;
+        // (constexpr positions: ce_pos is recursive, a runtime call would index v dynamically)
+        constexpr int pe = ce_pos(16, i), po = 16 + ce_pos(16, 15 - i), pob = 16 + ce_pos(16, i);
+        constexpr int per = ce_pos(16, (16 - i) & 15);
+        float2 b = v[pe];
+        float2 r = v[po];
+        if constexpr (i < 8) {  // lane 0: O[i] with O[15 - i] (bins 32 + 64 i, NC - 32 - 64 i)
+            const float2 o = v[pob];
+            b.x = lane0 ? o.x : b.x;
+            b.y = lane0 ? o.y : b.y;
+        } else if constexpr (i == 8) {  // lane 0: E[8] with itself (bin NC/2)
+            r.x = lane0 ? b.x : r.x;
+            r.y = lane0 ? b.y : r.y;
+        } else {  // lane 0: E[i] with E[16 - i] (bins 64 i, NC - 64 i)
+            const float2 e = v[per];
+            r.x = lane0 ? e.x : r.x;
+            r.y = lane0 ? e.y : r.y;
+        }
+        float s, co;
+        rot16<i>(i < 8 ? ub_lo : ub_hi, s, co);
+        const int k = (i < 8 ? kb_lo : j) + 64 * i;
+        // realfft.rs:148-154 on the pair (Z_k, Z_{NC-k}); the 1/2 is in the window
+        const float ar = b.x + r.x, ai = b.y - r.y;
+        const float br = b.x - r.x, bi = b.y + r.y;
+        const float p = __builtin_fmaf(co, br, s * bi);
+        const float q = __builtin_fmaf(co, bi, -(s * br));
+        const float x1r = ar + q, x1i = ai - p;
+        float x2r = ar - q, x2i = -ai - p;
+        if constexpr (i == 8) {  // lane 0's self pair: bin NC/2 is the first output only
+            x2r = lane0 ? x1r : x2r;
+            x2i = lane0 ? x1i : x2i;
+        }
+        epi(k, x1r, x1i, std::integral_constant<int, 2 * (i - I0)>{});
+        epi(NC - k, x2r, x2i, std::integral_constant<int, 2 * (i - I0) + 1>{});
+    });
+}
+
+// OK: 0 complex, 1 linear kinds, 2 mel kinds. C: 1 mono, 2 stereo (interleaved); INF: f32 / s16.
+template <int OK, int C, int INF>
+__global__ void __launch_bounds__(Geo5::BLOCK, Geo5::WV / 4)
+stft5_kernel(StftLaunch a, uint64_t fps, int rs) {
+    using G = Geo5;
+    using CK = Chunk<C, INF>;
+    using CT = typename CK::T;
+    using ET = typename std::conditional<INF == IN_S16, int16_t, float>::type;
+    constexpr int NC = G::NC, P = G::P, L = G::L, FPW = G::FPW, F = G::F, SH = G::SH, S = G::S;
+    constexpr int kBlock = G::BLOCK;
+    constexpr bool kStage = OK == 1;  // linear kinds: LDS-staged 16-byte row stores
+
+    extern __shared__ __attribute__((aligned(16))) float lds[];
+    float* wtl = lds;
+    float2* twtab = reinterpret_cast<float2*>(lds + G::WL_FLOATS);
+    float* work = lds + G::WL_FLOATS + G::TW_FLOATS;
+    float4* mel_lds = reinterpret_cast<float4*>(lds + G::TAB_FLOATS + G::STREAMS * rs);
+    int* k0_lds = reinterpret_cast<int*>(mel_lds + (OK == 2 ? a.mel4_rows * L : 0));
+    int2* rd_lds = reinterpret_cast<int2*>(k0_lds + (OK == 2 ? a.mel4_rounds * L : 0));
+    int* xo_lds = reinterpret_cast<int*>(rd_lds + (OK == 2 ? a.mel4_rounds : 0));
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int slot = lane / L, j = lane % L;
+    const bool lane0 = j == 0;
+    const int jb = (L - j) & (L - 1);  // the partner column B
+
+    for (int i = threadIdx.x; i < 2 * NC; i += kBlock) {  // w/2 is exact (realfft's 1/2)
+        const int m = i >> 1, jj = m % L, n1 = m / L;
+        wtl[jj * G::WL_STRIDE + 2 * n1 + (i & 1)] = a.wpad[i] * 0.5f;
+    }
+    if constexpr (OK == 2) {
+        const int nw = a.mel4_rows * L;
+        for (int i = threadIdx.x; i < nw; i += kBlock) mel_lds[i] = a.mel4_wt[i];
+        for (int i = threadIdx.x; i < a.mel4_rounds * L; i += kBlock) k0_lds[i] = a.mel4_k0[i];
+        for (int i = threadIdx.x; i < a.mel4_rounds; i += kBlock) rd_lds[i] = a.mel4_round[i];
+        for (int i = threadIdx.x; i < a.mel_chunks * L; i += kBlock) xo_lds[i] = a.mel_xo[i];
+    }
+    // stage-1 twiddles with k1 pairs interleaved: [k1/2][j][k1&1]
+    for (int i = threadIdx.x; i < P * L; i += kBlock) {
+        const int k1 = i / L, jj = i % L;
+        twtab[((k1 >> 1) * L + jj) * 2 + (k1 & 1)] = a.tw3[i];
+    }
+    // untangle bases: slots 0..7 start at bin kb_lo (lane 0: 32), slots 8..15 at bin j
+    float2 ub_lo = a.sincos[lane0 ? 32 : j], ub_hi = a.sincos[j];
+    const int kb_lo = lane0 ? 32 : j;
+    __syncthreads();
+
+    const uint64_t total = a.total_frames;
+    const uint64_t stream = ((uint64_t)blockIdx.x * G::WV + wave) * FPW + slot;
+    const uint64_t g0 = stream * fps;
+    const uint64_t g1 = g0 + fps < total ? g0 + fps : total;
+    const int hop = a.hop;
+    float* region = work + (wave * FPW + slot) * rs;
+    const ET* in = static_cast<const ET*>(a.in);
+
+    float2 raw[P];
+    CT pre[SH];
+    bool pre_ok = false;
+    int hint = -1;
+    uint64_t g_beg = 1, g_end = 0, base = 0;
+    int64_t n = 0;
+#ifdef THESIA_STAMPS
+    unsigned long long st_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    unsigned long long st_last;
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(st_last)::"memory");
+#endif
+    for (uint64_t it = 0; it < fps; ++it) {  // wave-uniform trip count
+        // wave priority phases (stft3): loads / window / FFT at 0, untangle / |X|
+        // / mel / stores at 2
+        __builtin_amdgcn_s_setprio(0);
+        MARK5(top, 7);
+        const uint64_t g = g0 + it;
+        const bool valid = g < g1;
+        asm volatile("" : "+v"(ub_lo.x), "+v"(ub_lo.y), "+v"(ub_hi.x), "+v"(ub_hi.y));
+        // opaque per frame: keeps the per-lane offsets (window row, transpose rows, untangle
+        // bins) inside the loop instead of hoisted as loop invariants into dozens of VGPRs
+        int wj = j, wjb = jb, wkb = kb_lo;
+        asm volatile("" : "+v"(wj), "+v"(wjb), "+v"(wkb));
+        const float4* wrow = reinterpret_cast<const float4*>(wtl + wj * G::WL_STRIDE);
+        int64_t start = 0;
+        if (valid) {
+            if (g >= g_end || g < g_beg) {
+                hint = find_track(a.trk_frame0, a.n_tracks, g, hint);
+                g_beg = a.trk_frame0[hint];
+                g_end = a.trk_frame0[hint + 1];
+                n = (int64_t)a.trk_len[hint];
+                base = a.trk_in_off[hint];
+            }
+            start = (int64_t)(g - g_beg) * hop - NC;  // half_win = NC, pad_left = 0
+        }
+        // ---- the frame's raw samples: shift by SH points + the prefetched hop ----
+        if (pre_ok) {
+#pragma unroll
+            for (int n1 = 0; n1 < P - SH; ++n1) raw[n1] = raw[n1 + SH];
+#pragma unroll
+            for (int q = 0; q < SH; ++q) raw[P - SH + q] = CK::mix(pre[q]);
+        } else if (valid && start >= 0 && start + 2 * NC <= n && ((base + (uint64_t)start * C) % (2 * C)) == 0) {
+            const CT* src = reinterpret_cast<const CT*>(in + base + (uint64_t)start * C) + j;
+            static_for<0, P / 8>([&](auto gc) {
+                constexpr int g8 = decltype(gc)::value;
+                static_for<0, 8>([&](auto ic) {
+                    constexpr int n1 = 8 * g8 + decltype(ic)::value;
+                    raw[n1] = CK::mix(src[L * n1]);
+                });
+                pin_range<8 * g8, 8 * g8 + 8>(raw);
+            });
+        } else if (valid) {
+            load_raw_generic_ool<NC, INF>(a, region, j, start, n, base, C, a.fold != 0, raw);
+        } else {
+#pragma unroll
+            for (int n1 = 0; n1 < P; ++n1) raw[n1] = make_float2(0.f, 0.f);
+        }
+        MARK5(loaded, 0);
+        // window (lib.rs:379, with the 1/2 of realfft.rs:148-154 folded in)
+        float2 v[P];
+        static_for<0, P / 2>([&](auto qc) {
+            constexpr int q = decltype(qc)::value;
+            const float4 w = wrow[q];
+            v[2 * q] = make_float2(raw[2 * q].x * w.x, raw[2 * q].y * w.y);
+            v[2 * q + 1] = make_float2(raw[2 * q + 1].x * w.z, raw[2 * q + 1].y * w.w);
+        });
+        // ---- prefetch the next frame's hop of new samples (its points P-SH .. P-1): right
+        // after the window at 2 waves/SIMD (a whole frame to land, as stft3), after the
+        // untangle at 3 (register budget) ----
+        auto prefetch = [&]() {
+            const int64_t nstart = start + hop;
+            const bool nxt = valid && g + 1 < g1 && g + 1 < g_end && nstart + 2 * NC <= n &&
+                             nstart + 2 * L * (P - SH) >= 0 &&
+                             ((base + (uint64_t)(nstart + 2 * L * (P - SH)) * C) % (2 * C)) == 0;
+            if (nxt) {
+                const CT* src = reinterpret_cast<const CT*>(in + base + (uint64_t)(nstart + 2 * L * (P - SH)) * C) + j;
+#pragma unroll
+                for (int q = 0; q < SH; ++q) pre[q] = src[L * q];
+            }
+            pre_ok = nxt;
+        };
+        if constexpr (G::PF_POS == 0) prefetch();
+        // ---- stage 1: DFT-32 over n1, twiddles W_NC^{j k1} ----
+        pin(v);
+        dif_fft<P, 1, 0, P>(v);
+        pin(v);
+        MARK5(stage1, 1);
+        {
+            const float4* tp = reinterpret_cast<const float4*>(twtab) + wj;
+            static_for<0, P / 2 / G::TWC>([&](auto cc) {
+                constexpr int c0 = decltype(cc)::value * G::TWC;
+                __builtin_amdgcn_sched_barrier(0);
+                float4 tw[G::TWC];
+                static_for<0, G::TWC>([&](auto uc) { tw[decltype(uc)::value] = tp[(c0 + decltype(uc)::value) * L]; });
+                static_for<0, G::TWC>([&](auto uc) {
+                    constexpr int q = c0 + decltype(uc)::value;
+                    if constexpr (q > 0) {
+                        constexpr int pk0 = ce_pos(P, 2 * q);
+                        v[pk0] = cmul(v[pk0], make_float2(tw[decltype(uc)::value].x, tw[decltype(uc)::value].y));
+                    }
+                    constexpr int pk1 = ce_pos(P, 2 * q + 1);
+                    v[pk1] = cmul(v[pk1], make_float2(tw[decltype(uc)::value].z, tw[decltype(uc)::value].w));
+                });
+            });
+        }
+        MARK5(twiddled, 2);
+        // ---- transpose (re, then im): rows A = j and B = 32 - j, first radix-2 step ----
+        // v[n] <- A[n] + A[n + 16]; v[16 + n] <- B[n] - B[n + 16] (n < 16)
+#pragma unroll
+        for (int e = 0; e < 2; ++e) {
+            wave_lds_sync();
+            static_for<0, P>([&](auto kc) {
+                constexpr int k1 = decltype(kc)::value;
+                constexpr int pk = ce_pos(P, k1);
+                region[k1 * S + j] = e == 0 ? v[pk].x : v[pk].y;
+            });
+            wave_lds_sync();
+            // row A lands in the component just written out: A[n] into v[n].e (e = re / im;
+            // explicit branches on the unrolled e: a reference select would put v in scratch)
+            const float4* ra = static_cast<const float4*>(__builtin_assume_aligned(region + wj * S, 16));
+            const float4* rb = static_cast<const float4*>(__builtin_assume_aligned(region + wjb * S, 16));
+            auto put = [&](float2& x, float val) {
+                if (e == 0) x.x = val; else x.y = val;
+            };
+            auto get = [&](const float2& x) { return e == 0 ? x.x : x.y; };
+            static_for<0, 8>([&](auto qc) {
+                constexpr int q = decltype(qc)::value;
+                const float4 t = ra[q];
+                put(v[4 * q], t.x); put(v[4 * q + 1], t.y); put(v[4 * q + 2], t.z); put(v[4 * q + 3], t.w);
+            });
+            static_for<0, 16>([&](auto nc) {  // even outputs of A: A[n] + A[n + 16]
+                constexpr int nn = decltype(nc)::value;
+                put(v[nn], get(v[nn]) + get(v[nn + 16]));
+            });
+            // row B, a half at a time: v[16 + n].e = B[n] - B[n + 16]
+            static_for<0, 2>([&](auto hc) {
+                constexpr int h = decltype(hc)::value;
+                __builtin_amdgcn_sched_barrier(0);
+                float4 xb[4];
+                xb[0] = rb[2 * h]; xb[1] = rb[2 * h + 1]; xb[2] = rb[2 * h + 4]; xb[3] = rb[2 * h + 5];
+                static_for<0, 2>([&](auto uc) {
+                    constexpr int u = decltype(uc)::value, n0 = 4 * (2 * h + u);
+                    put(v[16 + n0], xb[u].x - xb[u + 2].x);
+                    put(v[17 + n0], xb[u].y - xb[u + 2].y);
+                    put(v[18 + n0], xb[u].z - xb[u + 2].z);
+                    put(v[19 + n0], xb[u].w - xb[u + 2].w);
+                });
+            });
+        }
+        wave_lds_sync();
+        MARK5(transposed, 3);
+        if constexpr (G::PF_POS == 1) prefetch();
+        MARK5(prefetched, 4);
+        // ---- stage 2: W_32^n on B's differences, then the two DFT-16s ----
+        static_for<1, 16>([&](auto nc) {
+            constexpr int nn = decltype(nc)::value;
+            v[16 + nn] = twc<32, nn>(v[16 + nn]);
+        });
+        pin(v);
+        dif_fft<16, 1, 0, P>(v);
+        dif_fft<16, 1, 16, P>(v);
+        pin(v);
+        __builtin_amdgcn_s_setprio(2);
+        MARK5(stage2, 5);
+        if constexpr (OK == 2) {
+            // |X| (lib.rs:124) per half frame: the |X|^2 of 16 bins, their v_sqrt, the row writes
+            auto half = [&](auto h0) {
+                constexpr int I0 = decltype(h0)::value;
+                float mag[16];
+                untangle5<I0, I0 + 8>(v, lane0, ub_lo, ub_hi, wkb, wj, [&](int, float xr, float xi, auto sc) {
+                    mag[decltype(sc)::value] = __builtin_fmaf(xr, xr, xi * xi);
+                });
+                pin_f(mag);
+#pragma unroll
+                for (int i = 0; i < 16; ++i) mag[i] = __builtin_amdgcn_sqrtf(mag[i]);
+                pin_f(mag);
+                float* lo = region + wkb;      // bins kb + 64 i (slots < 8; wkb = j for j > 0)
+                float* hi = region + (NC - wj); // bins NC - j - 64 i
+                float* lo0 = region + NC - wkb;
+                static_for<0, 8>([&](auto ic) {
+                    constexpr int i = I0 + decltype(ic)::value;
+                    if constexpr (i < 8) {
+                        lo[64 * i] = mag[2 * (i - I0)];
+                        lo0[-64 * i] = mag[2 * (i - I0) + 1];
+                    } else {
+                        region[wj + 64 * i] = mag[2 * (i - I0)];
+                        hi[-64 * i] = mag[2 * (i - I0) + 1];
+                    }
+                });
+            };
+            half(std::integral_constant<int, 0>{});
+            half(std::integral_constant<int, 8>{});
+            if (lane0) {  // E[0] with itself: bins 0 and NC (s = 0, co = 1)
+                const float2 e0 = v[0];
+                const float ar = e0.x + e0.x, bi = e0.y + e0.y, x0 = ar + bi, xn = ar - bi;
+                region[0] = __builtin_amdgcn_sqrtf(__builtin_fmaf(x0, x0, 0.0f));
+                region[NC] = __builtin_amdgcn_sqrtf(__builtin_fmaf(xn, xn, 0.0f));
+#pragma unroll
+                for (int k = F; k < Geo2<NC>::F4; ++k) region[k] = 0.0f;
+            }
+            wave_lds_sync();
+            if constexpr (G::PF_POS == 2) prefetch();
+            MARK5(untangled, 6);
+            if (a.mel_chunks == 8) mel4p<NC, 8>(a, region, mel_lds, xo_lds, j, g, valid);
+            else if (a.mel_chunks == 4) mel4p<NC, 4>(a, region, mel_lds, xo_lds, j, g, valid);
+            else mel4<NC, 8, 1>(a, region, mel_lds, rd_lds, k0_lds, j, g, valid);
+        } else if constexpr (OK == 0) {  // lane-wise 8-byte stores
+            if constexpr (G::PF_POS == 2) prefetch();
+            float2* crow = reinterpret_cast<float2*>(a.out) + g * F;
+            auto st = [&](int k, float xr, float xi, auto) {
+                if (valid) st_out(crow + k, make_float2(xr, xi));
+            };
+            untangle5<0, 16>(v, lane0, ub_lo, ub_hi, wkb, wj, st);
+            if (lane0 && valid) {
+                const float2 e0 = v[0];
+                const float ar = e0.x + e0.x, bi = e0.y + e0.y;
+                st_out(crow, make_float2(ar + bi, 0.0f));
+                st_out(crow + NC, make_float2(ar - bi, 0.0f));
+            }
+        } else {
+            static_assert(kStage, "linear kinds stage their rows");
+            const int kind = a.out_kind;
+            const bool power = kind == OUT_POWER || kind == OUT_POWER_DB;
+            const bool db = kind == OUT_AMP_DB || kind == OUT_POWER_DB;
+            float* frow = static_cast<float*>(a.out) + g * F;
+            const int sh = (int)((reinterpret_cast<uintptr_t>(frow) >> 2) & 3);
+            float* stg = region + sh;
+            auto val_of = [&](float xr, float xi) {
+                const float p2 = __builtin_fmaf(xr, xr, xi * xi);
+                float val = power ? p2 : __builtin_amdgcn_sqrtf(p2);
+                if (db) val = power ? db_of(val, a.log_amin, 1e-36f, 10.0f)
+                                    : db_of(val, a.log_amin, 1e-18f, 20.0f);
+                return val;
+            };
+            untangle5<0, 16>(v, lane0, ub_lo, ub_hi, wkb, wj, [&](int k, float xr, float xi, auto) {
+                stg[k] = val_of(xr, xi);
+            });
+            if (lane0) {
+                const float2 e0 = v[0];
+                const float ar = e0.x + e0.x, bi = e0.y + e0.y;
+                stg[0] = val_of(ar + bi, 0.0f);
+                stg[NC] = val_of(ar - bi, 0.0f);
+            }
+            wave_lds_sync();
+            if constexpr (G::PF_POS == 2) prefetch();
+            if (valid) store_row_b128<L>(frow, sh, region, F, j);
+        }
+    }
+#ifdef THESIA_STAMPS
+    MARK5(end, 7);
+    if (a.stamps && lane == 0) {  // vector stores (lane-indexed address)
+        unsigned long long* o = a.stamps + ((uint64_t)blockIdx.x * G::WV + wave) * 9 + lane;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) o[i] = st_acc[i];
+        o[8] = fps;
+    }
+#endif
+}
+
+// --------------------------------------------------------------------------------------
+// host-side dispatch
+// --------------------------------------------------------------------------------------
+template <int OK>
+static int lds5_bytes(const StftLaunch& a, int rs) {
+    return (Geo5::TAB_FLOATS + Geo5::STREAMS * rs +
+            (OK == 2 ? (a.mel4_rows * 4 + a.mel4_rounds + a.mel_chunks) * Geo5::L + 2 * a.mel4_rounds : 0)) * 4;
+}
+template <int OK>
+static int region_stride5(const StftLaunch& a) {
+    return lds5_bytes<OK>(a, Geo5::RS) <= 163840 ? Geo5::RS : Geo5::RS_MIN;
+}
+
+template <int OK, int C, int INF>
+static int launch5_k(const StftLaunch& a, hipStream_t stream) {
+    const int rs = region_stride5<OK>(a);
+    const int lds = lds5_bytes<OK>(a, rs);
+    if (lds > 163840) return -2;
+    auto kern = stft5_kernel<OK, C, INF>;
+    if (hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
+                            hipFuncAttributeMaxDynamicSharedMemorySize, lds) != hipSuccess)
+        return -1;
+    if (a.total_frames == 0) return 0;
+    constexpr uint64_t per_block = Geo5::STREAMS;
+    int grid = grid_for(reinterpret_cast<const void*>(kern), Geo5::BLOCK, lds,
+                        (a.total_frames + per_block - 1) / per_block, a.grid);
+    const uint64_t streams = (uint64_t)grid * per_block;
+    const uint64_t fps = (a.total_frames + streams - 1) / streams;
+    grid = (int)((a.total_frames + fps * per_block - 1) / (fps * per_block));
+    hipLaunchKernelGGL(kern, dim3(grid), dim3(Geo5::BLOCK), lds, stream, a, fps, rs);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+template <int C, int INF>
+static int launch5_c(const StftLaunch& a, hipStream_t s) {
+    if (a.out_kind == OUT_COMPLEX) return launch5_k<0, C, INF>(a, s);
+    if (a.out_kind == OUT_MEL || a.out_kind == OUT_MEL_AMP_DB) return launch5_k<2, C, INF>(a, s);
+    return launch5_k<1, C, INF>(a, s);
+}
+
+int stft5_lds_bytes(const StftLaunch& a) {
+    const bool mel = a.out_kind == OUT_MEL || a.out_kind == OUT_MEL_AMP_DB;
+    return a.out_kind == OUT_COMPLEX ? lds5_bytes<0>(a, region_stride5<0>(a))
+           : mel ? lds5_bytes<2>(a, region_stride5<2>(a)) : lds5_bytes<1>(a, region_stride5<1>(a));
+}
+
+bool stft5_supports(int n_fft, int win, int hop, int in_format, int channels) {
+    return n_fft == 2048 && win == n_fft && hop * 4 == n_fft &&
+           (in_format == IN_F32 || in_format == IN_S16) && (channels == 1 || channels == 2);
+}
+
+int launch_stft5(const StftLaunch& a, hipStream_t s) {
+    if (a.n_fft != 2048) return -2;
+    if (a.in_format == IN_S16)
+        return a.channels == 2 ? launch5_c<2, IN_S16>(a, s) : launch5_c<1, IN_S16>(a, s);
+    return a.channels == 2 ? launch5_c<2, IN_F32>(a, s) : launch5_c<1, IN_F32>(a, s);
+}
+
+}  // namespace thesia

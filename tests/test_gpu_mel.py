@@ -55,7 +55,7 @@ def _tracks(rng, channels, fmt, lens):
     return out
 
 
-@pytest.mark.parametrize("kernel", [3, 2])
+@pytest.mark.parametrize("kernel", [5, 3, 2])
 @pytest.mark.parametrize("n_mels,sr", [(128, 48000), (40, 48000), (200, 44100), (0, 48000), (0, 22050)])
 @pytest.mark.parametrize("channels", [1, 2])
 def test_mel_is_the_dot_of_the_kernels_own_magnitude(kernel, n_mels, sr, channels):
@@ -123,6 +123,7 @@ def test_kernel_choice_and_unsupported_force():
     """The streaming kernel by default for its geometry; forcing a kernel that cannot run the
     geometry is an error, not a silent fallback."""
     x = np.zeros((4096, 2), np.float32)
+    _run(engine.OUT_MEL_AMP_DB, [x], 2, engine.IN_F32, n_mels=128, kernel=5)
     _run(engine.OUT_MEL_AMP_DB, [x], 2, engine.IN_F32, n_mels=128, kernel=3)
     plan = engine.Plan(2048, 1920, 480, engine.OUT_AMP_DB)  # viewer geometry: not streaming
     din = engine.DeviceBuffer.from_host(x[:, 0].copy())
@@ -132,6 +133,8 @@ def test_kernel_choice_and_unsupported_force():
     import thesia
     with pytest.raises(thesia.ThesiaError):
         b.set_option(engine.OPT_KERNEL, 3)
+    with pytest.raises(thesia.ThesiaError):
+        b.set_option(engine.OPT_KERNEL, 5)
 
 
 _VARIANT_CHILD = r"""
@@ -145,7 +148,7 @@ plan = engine.Plan(2048, 2048, 512, engine.OUT_MEL_AMP_DB, sr=48000, n_mels=128)
 din = engine.DeviceBuffer.from_host(x)
 T = engine.Batch.frames_for(plan, [48000])
 dout = engine.DeviceBuffer(T * 128 * 4)
-b = engine.Batch(plan, din, [0], [48000], dout, channels=2)
+b = engine.Batch(plan, din, [0], [48000], dout, channels=2, kernel=3)  # the experiments' kernel
 b.run()
 engine.synchronize()
 print(hashlib.sha256(dout.to_host(np.uint8).tobytes()).hexdigest(), b.kernel)

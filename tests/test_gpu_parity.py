@@ -1,6 +1,6 @@
 """Parity on the exact measured configurations and end to end.
 
-  bench   the headline bench line's own workload and kernel: stft3_kernel on stereo f32
+  bench   the headline bench line's own workload and kernel: stft5_kernel on stereo f32
           interleaved tracks from the device generator bench.py uses (whose bytes must equal its
           host twin), 30 s tracks, mel-128 amp dB vs the oracle (lib.rs:112-136).
   C1      BASELINE.json configs[0]: the 48 kHz sample substitute (tests/fixtures.py), n_fft 1024
@@ -44,7 +44,7 @@ def test_bench_config_exact():
     assert T == 2813 * n_tracks
     dout = engine.DeviceBuffer(T * 128 * 4)
     b = engine.Batch(plan, din, offs, [n] * n_tracks, dout, input_format=engine.IN_F32, channels=ch)
-    assert b.kernel == 3
+    assert b.kernel == 5  # the bench's kernel (stft5_kernel, the n_fft 2048 default)
     b.run()
     engine.synchronize()
     got = dout.to_host(np.float32, (T, 128))

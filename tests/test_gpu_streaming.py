@@ -48,7 +48,7 @@ def _run(n_fft, tracks, channels, fmt, gap, kernel, max_blocks=3):
     return [out[int(b.frame0[i]):int(b.frame0[i + 1])] for i in range(len(tracks))]
 
 
-@pytest.mark.parametrize("n_fft,kernel", [(256, 3), (1024, 3), (2048, 3), (2048, 2), (512, 1)])
+@pytest.mark.parametrize("n_fft,kernel", [(256, 3), (1024, 3), (2048, 5), (2048, 3), (2048, 2), (512, 1)])
 @pytest.mark.parametrize("channels,fmt", [(1, engine.IN_F32), (2, engine.IN_F32), (2, engine.IN_S16),
                                           (1, engine.IN_S16)])
 @pytest.mark.parametrize("gap", [0, 3])
@@ -77,16 +77,16 @@ _LIN_KINDS = [engine.OUT_MAG, engine.OUT_POWER, engine.OUT_AMP_DB, engine.OUT_PO
 @pytest.mark.parametrize("n_fft", [256, 2048])
 @pytest.mark.parametrize("kind", _LIN_KINDS + [engine.OUT_COMPLEX])
 @pytest.mark.parametrize("shift", [0, 1, 2, 3])
-@pytest.mark.parametrize("row_store", [0, 1])
-def test_row_stores_any_output_alignment(n_fft, kind, shift, row_store):
+@pytest.mark.parametrize("row_store,kernel", [(0, 3), (1, 3), (0, 5)])
+def test_row_stores_any_output_alignment(n_fft, kind, shift, row_store, kernel):
     """Output rows of F floats / F float2 are not 16-byte aligned; the LDS-staged float4 row
     stores (stft3 store_row_b128: linear kinds by default, complex with the ROW_STORE option) must write
     exactly the row whatever the output pointer's alignment, and nothing outside the batch's
     rows (guard floats on both sides stay untouched)."""
     if kind == engine.OUT_COMPLEX and shift % 2:
         pytest.skip("complex rows are float2: 8-byte aligned output")
-    if row_store and n_fft != 2048:
-        pytest.skip("the other store method is compiled for n_fft 2048 stereo f32 only")
+    if (row_store or kernel == 5) and n_fft != 2048:
+        pytest.skip("the other store method / stft5_kernel: n_fft 2048 only")
     rng = np.random.default_rng(n_fft + 7 * kind + shift)
     hop = n_fft // 4
     lens = [n_fft - 1, 5 * n_fft + 3, 33 * hop + 1, 2 * n_fft]
@@ -103,8 +103,8 @@ def test_row_stores_any_output_alignment(n_fft, kind, shift, row_store):
     dout = engine.DeviceBuffer.from_host(host)
     ptr = dout.ptr.value + (guard + shift) * 4
     b = engine.Batch(plan, din, offs, lens, ptr, input_format=engine.IN_F32, channels=2,
-                     max_blocks=3, row_store=row_store)
-    assert b.kernel == 3
+                     max_blocks=3, row_store=row_store, kernel=kernel)
+    assert b.kernel == kernel
     b.run()
     engine.synchronize()
     res = dout.to_host(np.float32)
