@@ -83,9 +83,13 @@ struct Batch {
     int kernel = 1;  // 1 stft_kernel, 2 stft2_kernel, 3 stft3_kernel, 5 stft5_kernel (streaming)
     bool k3_ok = false;  // the streaming kernel supports this batch's geometry
     bool k5_ok = false;  // ... and so does its n_fft 2048 variant (stft5_kernel)
-    // automatic choice: stft5 for n_fft 2048, stft3 for its other streaming geometries, then
+    // automatic choice: stft5 for the mel kinds at n_fft 2048 (measured faster there; slower
+    // for complex / linear rows), stft3 for the other streaming geometries, then
     // the 4-waves/SIMD kernel for its sizes, else the general one
-    int auto_kernel() const { return k5_ok ? 5 : k3_ok ? 3 : plan->use_v2 ? 2 : 1; }
+    int auto_kernel() const {
+        const bool mel = launch.out_kind == OUT_MEL || launch.out_kind == OUT_MEL_AMP_DB;
+        return k5_ok && mel ? 5 : k3_ok ? 3 : plan->use_v2 ? 2 : 1;
+    }
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     ~Batch();
 };

@@ -49,6 +49,15 @@ namespace thesia {
 #ifndef THESIA_WV5
 #define THESIA_WV5 8
 #endif
+#ifndef THESIA_WF5
+#define THESIA_WF5 1
+#endif
+#ifndef THESIA_BH5
+#define THESIA_BH5 1
+#endif
+#ifndef THESIA_SC5
+#define THESIA_SC5 1
+#endif
 #ifndef THESIA_TWC5
 #define THESIA_TWC5 8
 #endif
@@ -66,6 +75,7 @@ struct Geo5 {
     static constexpr int TW_FLOATS = 2 * P * L;
     static constexpr int TAB_FLOATS = WL_FLOATS + TW_FLOATS;
     static constexpr int TWC = THESIA_TWC5;  // stage-1 twiddle float4 reads per batch
+    static constexpr int BH = THESIA_BH5;    // parts the partner row B is read in
     static constexpr int PF_POS = WV == 8 ? 0 : 2;  // where the next hop's loads issue
     static_assert(RS_MIN >= P * S && RS_MIN >= F + 6 && RS_MIN % 4 == 0 && RS % 4 == 0, "region");
 };
@@ -88,9 +98,22 @@ __device__ __forceinline__ void rot16(float2 ub, float& s, float& co) {
 // The realfft untangle of slots I0 <= i < I1 (see the header): calls
 // epi(k, re, im, integral_constant<2 (i - I0) + h>) for bin k (h = 0) and NC - k (h = 1).
 // v[ce_pos(16, i)] = E[i], v[16 + ce_pos(16, i)] = O[i].
-template <int I0, int I1, class Epi>
-__device__ __forceinline__ void untangle5(const float2 (&v)[32], bool lane0, float2 ub_lo,
-                                          float2 ub_hi, int kb_lo, int j, Epi&& epi) {
+// rotation sources: the (sin, cos) of slot i rotated per frame from the two bases, or read
+// from a per-lane table computed once (THESIA_SC5: 32 VGPRs for 64 VALU per frame pair)
+struct RotBases {
+    float2 lo, hi;
+    template <int I>
+    __device__ __forceinline__ void get(float& s, float& co) const { rot16<I>(I < 8 ? lo : hi, s, co); }
+};
+struct RotTable {
+    const float2 (&t)[16];
+    template <int I>
+    __device__ __forceinline__ void get(float& s, float& co) const { s = t[I].x; co = t[I].y; }
+};
+
+template <int I0, int I1, class Rot, class Epi>
+__device__ __forceinline__ void untangle5(const float2 (&v)[32], bool lane0, const Rot& rot,
+                                          int kb_lo, int j, Epi&& epi) {
     constexpr int NC = Geo5::NC;
     static_for<I0, I1>([&](auto ic) {
         constexpr int i = decltype(ic)::value;
@@ -112,7 +135,7 @@ __device__ __forceinline__ void untangle5(const float2 (&v)[32], bool lane0, flo
             r.y = lane0 ? e.y : r.y;
         }
         float s, co;
-        rot16<i>(i < 8 ? ub_lo : ub_hi, s, co);
+        rot.template get<i>(s, co);
         const int k = (i < 8 ? kb_lo : j) + 64 * i;
         // realfft.rs:148-154 on the pair (Z_k, Z_{NC-k}); the 1/2 is in the window
         const float ar = b.x + r.x, ai = b.y - r.y;
@@ -173,6 +196,14 @@ stft5_kernel(StftLaunch a, uint64_t fps, int rs) {
     }
     // untangle bases: slots 0..7 start at bin kb_lo (lane 0: 32), slots 8..15 at bin j
     float2 ub_lo = a.sincos[lane0 ? 32 : j], ub_hi = a.sincos[j];
+#if THESIA_SC5
+    float2 sct[16];
+    static_for<0, 16>([&](auto ic) {
+        constexpr int i = decltype(ic)::value;
+        rot16<i>(i < 8 ? ub_lo : ub_hi, sct[i].x, sct[i].y);
+    });
+    const RotTable rot{sct};
+#endif
     const int kb_lo = lane0 ? 32 : j;
     __syncthreads();
 
@@ -202,7 +233,10 @@ stft5_kernel(StftLaunch a, uint64_t fps, int rs) {
         MARK5(top, 7);
         const uint64_t g = g0 + it;
         const bool valid = g < g1;
+#if !THESIA_SC5
         asm volatile("" : "+v"(ub_lo.x), "+v"(ub_lo.y), "+v"(ub_hi.x), "+v"(ub_hi.y));
+        const RotBases rot{ub_lo, ub_hi};
+#endif
         // opaque per frame: keeps the per-lane offsets (window row, transpose rows, untangle
         // bins) inside the loop instead of hoisted as loop invariants into dozens of VGPRs
         int wj = j, wjb = jb, wkb = kb_lo;
@@ -242,14 +276,6 @@ stft5_kernel(StftLaunch a, uint64_t fps, int rs) {
             for (int n1 = 0; n1 < P; ++n1) raw[n1] = make_float2(0.f, 0.f);
         }
         MARK5(loaded, 0);
-        // window (lib.rs:379, with the 1/2 of realfft.rs:148-154 folded in)
-        float2 v[P];
-        static_for<0, P / 2>([&](auto qc) {
-            constexpr int q = decltype(qc)::value;
-            const float4 w = wrow[q];
-            v[2 * q] = make_float2(raw[2 * q].x * w.x, raw[2 * q].y * w.y);
-            v[2 * q + 1] = make_float2(raw[2 * q + 1].x * w.z, raw[2 * q + 1].y * w.w);
-        });
         // ---- prefetch the next frame's hop of new samples (its points P-SH .. P-1): right
         // after the window at 2 waves/SIMD (a whole frame to land, as stft3), after the
         // untangle at 3 (register budget) ----
@@ -267,9 +293,53 @@ stft5_kernel(StftLaunch a, uint64_t fps, int rs) {
         };
         if constexpr (G::PF_POS == 0) prefetch();
         // ---- stage 1: DFT-32 over n1, twiddles W_NC^{j k1} ----
+#if THESIA_WF5
+        // window (lib.rs:379, with the 1/2 of realfft.rs:148-154 folded in) inside the first
+        // radix-4 level of the DFT-32 (dif_fft's N = 32 level): the products of inputs 2 and 3
+        // are formed once and the ones of inputs 0 and 1 ride in the butterfly fmas (12 VALU per
+        // butterfly instead of 16)
+        float2 v[P];
+        static_for<0, 4>([&](auto jc) {
+            constexpr int jp = decltype(jc)::value;
+            const float4 wq[4] = {wrow[jp], wrow[jp + 4], wrow[jp + 8], wrow[jp + 12]};
+            static_for<0, 2>([&](auto hc) {
+                constexpr int h = decltype(hc)::value, jj = 2 * jp + h;
+                auto wv = [&](int t) {
+                    return h == 0 ? make_float2(wq[t].x, wq[t].y) : make_float2(wq[t].z, wq[t].w);
+                };
+                const float2 w0 = wv(0), w1 = wv(1), w2 = wv(2), w3 = wv(3);
+                const float2 a0 = raw[jj], a1 = raw[jj + 8], a2 = raw[jj + 16], a3 = raw[jj + 24];
+                const float2 m2 = make_float2(a2.x * w2.x, a2.y * w2.y);
+                const float2 m3 = make_float2(a3.x * w3.x, a3.y * w3.y);
+                const float2 t0 = make_float2(__builtin_fmaf(a0.x, w0.x, m2.x), __builtin_fmaf(a0.y, w0.y, m2.y));
+                const float2 t1 = make_float2(__builtin_fmaf(a0.x, w0.x, -m2.x), __builtin_fmaf(a0.y, w0.y, -m2.y));
+                const float2 t2 = make_float2(__builtin_fmaf(a1.x, w1.x, m3.x), __builtin_fmaf(a1.y, w1.y, m3.y));
+                const float2 t3 = mul_negi(make_float2(__builtin_fmaf(a1.x, w1.x, -m3.x), __builtin_fmaf(a1.y, w1.y, -m3.y)));
+                v[jj] = cadd(t0, t2);
+                v[jj + 8] = twc<32, jj>(cadd(t1, t3));
+                v[jj + 16] = twc<32, 2 * jj>(csub(t0, t2));
+                v[jj + 24] = twc<32, 3 * jj>(csub(t1, t3));
+            });
+        });
+        pin(v);
+        dif_fft<8, 1, 0, P>(v);
+        dif_fft<8, 1, 8, P>(v);
+        dif_fft<8, 1, 16, P>(v);
+        dif_fft<8, 1, 24, P>(v);
+        pin(v);
+#else
+        // window (lib.rs:379, with the 1/2 of realfft.rs:148-154 folded in)
+        float2 v[P];
+        static_for<0, P / 2>([&](auto qc) {
+            constexpr int q = decltype(qc)::value;
+            const float4 w = wrow[q];
+            v[2 * q] = make_float2(raw[2 * q].x * w.x, raw[2 * q].y * w.y);
+            v[2 * q + 1] = make_float2(raw[2 * q + 1].x * w.z, raw[2 * q + 1].y * w.w);
+        });
         pin(v);
         dif_fft<P, 1, 0, P>(v);
         pin(v);
+#endif
         MARK5(stage1, 1);
         {
             const float4* tp = reinterpret_cast<const float4*>(twtab) + wj;
@@ -318,18 +388,22 @@ stft5_kernel(StftLaunch a, uint64_t fps, int rs) {
                 constexpr int nn = decltype(nc)::value;
                 put(v[nn], get(v[nn]) + get(v[nn + 16]));
             });
-            // row B, a half at a time: v[16 + n].e = B[n] - B[n + 16]
-            static_for<0, 2>([&](auto hc) {
-                constexpr int h = decltype(hc)::value;
-                __builtin_amdgcn_sched_barrier(0);
-                float4 xb[4];
-                xb[0] = rb[2 * h]; xb[1] = rb[2 * h + 1]; xb[2] = rb[2 * h + 4]; xb[3] = rb[2 * h + 5];
-                static_for<0, 2>([&](auto uc) {
-                    constexpr int u = decltype(uc)::value, n0 = 4 * (2 * h + u);
-                    put(v[16 + n0], xb[u].x - xb[u + 2].x);
-                    put(v[17 + n0], xb[u].y - xb[u + 2].y);
-                    put(v[18 + n0], xb[u].z - xb[u + 2].z);
-                    put(v[19 + n0], xb[u].w - xb[u + 2].w);
+            // row B (in THESIA_BH5 parts): v[16 + n].e = B[n] - B[n + 16]
+            static_for<0, G::BH>([&](auto hc) {
+                constexpr int h = decltype(hc)::value, QP = 4 / G::BH;  // float4 pairs per part
+                if constexpr (G::BH > 1) __builtin_amdgcn_sched_barrier(0);
+                float4 xb[2 * QP];
+                static_for<0, QP>([&](auto qc) {
+                    constexpr int q = h * QP + decltype(qc)::value;
+                    xb[decltype(qc)::value] = rb[q];
+                    xb[QP + decltype(qc)::value] = rb[q + 4];
+                });
+                static_for<0, QP>([&](auto uc) {
+                    constexpr int u = decltype(uc)::value, n0 = 4 * (h * QP + u);
+                    put(v[16 + n0], xb[u].x - xb[u + QP].x);
+                    put(v[17 + n0], xb[u].y - xb[u + QP].y);
+                    put(v[18 + n0], xb[u].z - xb[u + QP].z);
+                    put(v[19 + n0], xb[u].w - xb[u + QP].w);
                 });
             });
         }
@@ -353,7 +427,7 @@ stft5_kernel(StftLaunch a, uint64_t fps, int rs) {
             auto half = [&](auto h0) {
                 constexpr int I0 = decltype(h0)::value;
                 float mag[16];
-                untangle5<I0, I0 + 8>(v, lane0, ub_lo, ub_hi, wkb, wj, [&](int, float xr, float xi, auto sc) {
+                untangle5<I0, I0 + 8>(v, lane0, rot, wkb, wj, [&](int, float xr, float xi, auto sc) {
                     mag[decltype(sc)::value] = __builtin_fmaf(xr, xr, xi * xi);
                 });
                 pin_f(mag);
@@ -396,7 +470,7 @@ stft5_kernel(StftLaunch a, uint64_t fps, int rs) {
             auto st = [&](int k, float xr, float xi, auto) {
                 if (valid) st_out(crow + k, make_float2(xr, xi));
             };
-            untangle5<0, 16>(v, lane0, ub_lo, ub_hi, wkb, wj, st);
+            untangle5<0, 16>(v, lane0, rot, wkb, wj, st);
             if (lane0 && valid) {
                 const float2 e0 = v[0];
                 const float ar = e0.x + e0.x, bi = e0.y + e0.y;
@@ -418,7 +492,7 @@ stft5_kernel(StftLaunch a, uint64_t fps, int rs) {
                                     : db_of(val, a.log_amin, 1e-18f, 20.0f);
                 return val;
             };
-            untangle5<0, 16>(v, lane0, ub_lo, ub_hi, wkb, wj, [&](int k, float xr, float xi, auto) {
+            untangle5<0, 16>(v, lane0, rot, wkb, wj, [&](int k, float xr, float xi, auto) {
                 stg[k] = val_of(xr, xi);
             });
             if (lane0) {
