@@ -268,6 +268,19 @@ static int build_mel4(Plan* p) {
     return rc;
 }
 
+// rustfft's prepare_radix4 (oracle cfft_tab): spec[j] = sig[...] in the digit order the
+// radix-4 passes expect; run on indices it gives the source of every position
+static void prepare_radix4_order(size_t size, const int* sig, int* spec, size_t stride) {
+    if (size == 16) {
+        for (size_t i = 0; i < 4; ++i) prepare_radix4_order(4, sig + i * stride, spec + i * 4, stride * 4);
+    } else if (size == 8 || size == 4) {
+        for (size_t i = 0; i < size; ++i) spec[i] = sig[i * stride];
+    } else {
+        for (size_t i = 0; i < 4; ++i)
+            prepare_radix4_order(size / 4, sig + i * stride, spec + i * (size / 4), stride * 4);
+    }
+}
+
 int plan_create(const thesia_plan_desc& d, Plan** out) {
     *out = nullptr;
     if (!is_pow2(d.n_fft) || d.n_fft < 2 || d.n_fft > 4096)
@@ -344,6 +357,22 @@ int plan_create(const thesia_plan_desc& d, Plan** out) {
     if (!rc) rc = p->tw2.upload(tw2.data(), tw2.size() * sizeof(float));
     if (!rc) rc = p->tw3.upload(tw3.data(), tw3.size() * sizeof(float));
     if (!rc) rc = p->sincos.upload(sc.data(), sc.size() * sizeof(float));
+    // the reference-order kernel: rustfft prepare_radix4 positions (oracle cfft_tab) and the
+    // base butterfly_8 twiddles
+    if (!rc) {
+        const size_t NC = p->NC;
+        std::vector<int> src(std::max<size_t>(NC, 1)), pos(std::max<size_t>(NC, 1));
+        for (size_t i = 0; i < NC; ++i) src[i] = (int)i;
+        if (NC > 4) {
+            std::vector<int> idn(src);
+            prepare_radix4_order(NC, idn.data(), src.data(), 1);
+        }
+        for (size_t jj = 0; jj < NC; ++jj) pos[(size_t)src[jj]] = (int)jj;
+        rc = p->xpos.upload(pos.data(), pos.size() * sizeof(int));
+        const double a1 = -2.0 * 3.14159265358979323846 * 1.0 / 8.0, a3 = -2.0 * 3.14159265358979323846 * 3.0 / 8.0;
+        p->xw8[0] = (float)std::cos(a1); p->xw8[1] = (float)std::sin(a1);
+        p->xw8[2] = (float)std::cos(a3); p->xw8[3] = (float)std::sin(a3);
+    }
     if (!rc && (d.output == THESIA_OUT_MEL || d.output == THESIA_OUT_MEL_AMP_DB)) {
         const size_t F = p->NC + 1;
         if (d.mel_fb) {
@@ -360,6 +389,25 @@ int plan_create(const thesia_plan_desc& d, Plan** out) {
         }
         if (!rc) rc = build_mel(p);
         if (!rc) rc = build_mel4(p);
+        if (!rc) {  // the reference-order kernel: each mel's nonzero band, weights flat
+            const size_t M = p->n_mels;
+            std::vector<int4> band(std::max<size_t>(M, 1), int4{0, 0, 0, 0});
+            std::vector<float> w;
+            for (size_t m = 0; m < M; ++m) {
+                long lo = -1, hi = -1;
+                for (size_t k = 0; k < F; ++k)
+                    if (p->mel_fb[k * M + m] != 0.0f) {
+                        if (lo < 0) lo = (long)k;
+                        hi = (long)k + 1;
+                    }
+                if (lo < 0) lo = hi = 0;
+                band[m] = int4{(int)lo, (int)(hi - lo), (int)w.size(), 0};
+                for (long k = lo; k < hi; ++k) w.push_back(p->mel_fb[(size_t)k * M + m]);
+            }
+            if (w.empty()) w.push_back(0.0f);
+            rc = p->xmel_band.upload(band.data(), band.size() * sizeof(int4));
+            if (!rc) rc = p->xmel_w.upload(w.data(), w.size() * sizeof(float));
+        }
     }
     if (!rc) {
         p->use_v2 = stft2_supports((int)d.n_fft);
@@ -450,6 +498,10 @@ int batch_create(Plan* plan, const thesia_batch_desc& d, Batch** out) {
     L.mel4_round = plan->mel4_round.as<int2>();
     L.mel4_k0 = plan->mel4_k0.as<int>();
     L.mel4_wt = plan->mel4_wt.as<float4>();
+    L.xpos = plan->xpos.as<int>();
+    for (int i = 0; i < 4; ++i) L.xw8[i] = plan->xw8[i];
+    L.xmel_band = plan->xmel_band.as<int4>();
+    L.xmel_w = plan->xmel_w.as<float>();
     L.mel_chunks = plan->mel_chunks;
     L.mel_xo = plan->mel_xo.as<int>();
     L.out = d.d_output;
@@ -478,6 +530,7 @@ int batch_set_option(Batch* b, int option, int64_t value) {
             else if (value == 2 && stft2_supports((int)b->plan->n_fft)) b->kernel = 2;
             else if (value == 3 && b->k3_ok) b->kernel = 3;
             else if (value == 5 && b->k5_ok) b->kernel = 5;
+            else if (value == 9 && stftx_lds_bytes((int)b->plan->n_fft) <= 163840) b->kernel = 9;
             else return set_error(THESIA_ERR_UNSUPPORTED, "kernel " + std::to_string(value) +
                                                              " does not run this batch's geometry");
             return THESIA_OK;
@@ -502,6 +555,11 @@ int batch_set_option(Batch* b, int option, int64_t value) {
 int batch_run(Batch* b, hipStream_t s) {
     if (!s) s = default_stream();
     int rc = -2;
+    if (b->kernel == 9) {
+        rc = launch_stftx(b->launch, s);
+        if (rc) return set_error(rc == -2 ? THESIA_ERR_UNSUPPORTED : THESIA_ERR_DEVICE, "stftx launch failed");
+        return THESIA_OK;
+    }
     if (b->kernel == 5) rc = launch_stft5(b->launch, s);
     if (rc == -2 && b->kernel >= 3) rc = launch_stft3(b->launch, s);
     if (rc == -2 && b->kernel >= 2) rc = launch_stft2(b->launch, s);

@@ -64,6 +64,8 @@ struct Plan {
     DevBuf mel4_round, mel4_k0, mel4_wt;  // stft2_kernel layout (float4 steps)
     int mel4_rounds = 0;
     DevBuf mel_xo;      // the rounds as a chunk stream (kernels.hpp mel_xo)
+    DevBuf xpos, xmel_band, xmel_w;  // the reference-order kernel's tables (stftx)
+    float xw8[4] = {0.f, 0.f, 0.f, 0.f};
     int mel_chunks = 0;
     size_t mel4_wt_rows = 0;
     bool use_v2 = false;  // stft2_kernel runs this plan (n_fft 256..2048)
@@ -80,7 +82,9 @@ struct Batch {
     DevBuf d_in_off, d_len, d_frame0;
     uint64_t total_frames = 0;
     StftLaunch launch{};
-    int kernel = 1;  // 1 stft_kernel, 2 stft2_kernel, 3 stft3_kernel, 5 stft5_kernel (streaming)
+    // 1 stft_kernel, 2 stft2_kernel, 3 stft3_kernel, 5 stft5_kernel (streaming), 9 stftx_kernel
+    // (reference operation order)
+    int kernel = 1;
     bool k3_ok = false;  // the streaming kernel supports this batch's geometry
     bool k5_ok = false;  // ... and so does its n_fft 2048 variant (stft5_kernel)
     // automatic choice: stft5 for the mel kinds at n_fft 2048 (measured faster there; slower

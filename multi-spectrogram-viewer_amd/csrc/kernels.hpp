@@ -73,6 +73,13 @@ struct StftLaunch {
     // scheduling / named alternatives (thesia_batch_set_option)
     int grid = 0;     // 0 => computed from occupancy, else at most this many blocks
     int row_alt = 0;  // 1: the other row-store method (stft3 n_fft 2048 stereo f32)
+    // the reference-order kernel (stftx_kernels.hip): input point m sits at xpos[m] of the
+    // rustfft prepare_radix4 order; xw8 = {twiddle(1, 8), twiddle(3, 8)}; per mel m its nonzero
+    // band {first bin, bins, offset into xmel_w}
+    const int* xpos = nullptr;
+    float xw8[4] = {0.f, 0.f, 0.f, 0.f};
+    const int4* xmel_band = nullptr;
+    const float* xmel_w = nullptr;
     // diagnostic builds only (-DTHESIA_STAMPS, scripts/stamps.py): per-wave phase cycle sums
     unsigned long long* stamps = nullptr;
 };
@@ -88,6 +95,9 @@ int stft2_kernel_info(int n_fft, int* lds_bytes, int* tile_frames, int* lanes_pe
 int launch_stft3(const StftLaunch& a, hipStream_t stream);
 bool stft3_supports(int n_fft, int win, int hop, int in_format, int channels);
 int stft3_lds_bytes(const StftLaunch& a);  // dynamic LDS of the launch (> 163840: cannot run)
+// stftx_kernel (every n_fft: the reference's operation order, bit-exact with the oracle)
+int launch_stftx(const StftLaunch& a, hipStream_t stream);
+int stftx_lds_bytes(int n_fft);
 // stft5_kernel (streaming, n_fft 2048 only, co-resident untangle pairs; stft5_kernels.hip)
 int launch_stft5(const StftLaunch& a, hipStream_t stream);
 bool stft5_supports(int n_fft, int win, int hop, int in_format, int channels);

@@ -126,7 +126,10 @@ int MultiTrack::compute_spec(uint64_t id) {
     Batch* b = nullptr;
     rc = batch_create(plan, bd, &b);
     if (rc) return rc;
-    rc = batch_run(b, default_stream());
+    // the viewer path computes in the reference's operation order (stftx_kernel): its images
+    // are the oracle pipeline's bytes
+    rc = batch_set_option(b, THESIA_BATCH_OPT_KERNEL, 9);
+    if (!rc) rc = batch_run(b, default_stream());
     if (!rc) {
         hipError_t e = hipStreamSynchronize(default_stream());
         if (e != hipSuccess) rc = set_error(THESIA_ERR_DEVICE, hipGetErrorString(e));
