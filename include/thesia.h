@@ -231,14 +231,29 @@ int thesia_grey_to_rgb_device(const float* d_grey, uint32_t width, uint32_t heig
  * [nheight, nwidth[i], 3] lands at d_rgb + rgb_off[i] (host arrays of n entries). */
 int thesia_minmax_segments_device(const float* d_spec, const uint64_t* row0, size_t bins,
                                   size_t n, float* max, float* min, int* has_nan);
-/* Process-wide choice of the batched display path's launch structure: 0 = every track of a
- * call in one launch per stage (default), 1 = per-track launches (the reference's one image
- * at a time structure; a cross-check, byte-identical). */
+/* Process-wide choice of the batched display path's launch structure (all byte-identical):
+ * 0 = the fused path (default; grey + vertical Lanczos3 in one pass over the spectrogram, then
+ * horizontal Lanczos3 + colormap, every track of a call in each launch), 1 = per-track
+ * launches (the reference's one image at a time structure),
+ * 2 = every track in one launch per stage: grey, vertical, horizontal + colormap. */
 int thesia_set_render_path(int path);
 int thesia_render_rgb_batch_device(const float* d_spec, const uint64_t* row0, size_t bins,
                                    size_t n, const float* up_ratio, const uint32_t* nwidth,
                                    uint32_t nheight, float max, float min, uint8_t* d_rgb,
                                    const uint64_t* rgb_off);
+
+/* Several geometry groups in one call (group k: spectrogram buffer d_specs[k] of bins[k]
+ * floats per row, ns[k] tracks with row table row0s[k] of ns[k]+1 entries); the per-track
+ * arrays (max/min/has_nan out; up_ratio, nwidth, rgb_off in) are concatenated in group order.
+ * Same results as one single-group call per group, with one table upload and one stream
+ * synchronisation for the whole call instead of one per group. */
+int thesia_minmax_segments_multi(size_t n_groups, const float* const* d_specs,
+                                 const uint64_t* const* row0s, const size_t* bins, const size_t* ns,
+                                 float* max, float* min, int* has_nan);
+int thesia_render_rgb_multi(size_t n_groups, const float* const* d_specs, const uint64_t* const* row0s,
+                            const size_t* bins, const size_t* ns, const float* up_ratio,
+                            const uint32_t* nwidth, uint32_t nheight, float max, float min,
+                            uint8_t* d_rgb, const uint64_t* rgb_off);
 
 /* ---------------------------------------------------------------------------------- */
 /* MultiTrack -- lib.rs:72-365 (the viewer's stateful surface)                          */

@@ -444,6 +444,45 @@ int thesia_render_rgb_batch_device(const float* d_spec, const uint64_t* row0, si
     GUARD_END
 }
 
+int thesia_minmax_segments_multi(size_t n_groups, const float* const* d_specs,
+                                 const uint64_t* const* row0s, const size_t* bins, const size_t* ns,
+                                 float* max, float* min, int* has_nan) {
+    GUARD_BEGIN
+    if (n_groups && (!d_specs || !row0s || !bins || !ns || !max || !min || !has_nan))
+        return set_error(THESIA_ERR_INVALID_ARG, "null pointer");
+    for (size_t k = 0; k < n_groups; ++k)
+        if (ns[k] && (!d_specs[k] || !row0s[k])) return set_error(THESIA_ERR_INVALID_ARG, "null pointer");
+    return minmax_segments_multi(n_groups, d_specs, row0s, bins, ns, max, min, has_nan, default_stream());
+    GUARD_END
+}
+
+int thesia_render_rgb_multi(size_t n_groups, const float* const* d_specs, const uint64_t* const* row0s,
+                            const size_t* bins, const size_t* ns, const float* up_ratio,
+                            const uint32_t* nwidth, uint32_t nheight, float max, float min,
+                            uint8_t* d_rgb, const uint64_t* rgb_off) {
+    GUARD_BEGIN
+    size_t tot = 0;
+    if (n_groups && (!d_specs || !row0s || !bins || !ns)) return set_error(THESIA_ERR_INVALID_ARG, "null pointer");
+    for (size_t k = 0; k < n_groups; ++k) {
+        if (ns[k] && (!d_specs[k] || !row0s[k])) return set_error(THESIA_ERR_INVALID_ARG, "null pointer");
+        tot += ns[k];
+    }
+    if (tot && (!up_ratio || !nwidth || !d_rgb || !rgb_off)) return set_error(THESIA_ERR_INVALID_ARG, "null pointer");
+    if (render_path() == 0)
+        return render_rgb_fused(n_groups, d_specs, row0s, bins, ns, up_ratio, nwidth, nheight, max, min,
+                                d_rgb, rgb_off, default_stream());
+    size_t t0 = 0;
+    for (size_t k = 0; k < n_groups; ++k) {
+        const int rc = render_rgb_batch_device(d_specs[k], row0s[k], bins[k], ns[k], up_ratio + t0,
+                                               nwidth + t0, nheight, max, min, d_rgb, rgb_off + t0,
+                                               default_stream());
+        if (rc) return rc;
+        t0 += ns[k];
+    }
+    return THESIA_OK;
+    GUARD_END
+}
+
 int thesia_wav_to_image(const float* wav, size_t n, uint32_t nwidth, uint32_t nheight,
                         float amp_min, float amp_max, uint8_t* out, size_t cap) {
     GUARD_BEGIN

@@ -17,6 +17,26 @@
 #include <cstdlib>
 #include <cstdint>
 
+// compile-time choices A/B'd with scripts/build_variant.sh (defaults = the product)
+#ifndef THESIA_V_ILP
+#define THESIA_V_ILP 1  // grey_vert: four output rows per wave step
+#endif
+#ifndef THESIA_V_FLAT
+#define THESIA_V_FLAT 1  // grey_vert: flattened (frame, row) tile staging
+#endif
+#ifndef THESIA_V_ABL
+#define THESIA_V_ABL 0
+#endif
+#ifndef THESIA_VDEPTH
+#define THESIA_VDEPTH 8  // grey_vert: tile loads in flight per thread
+#endif
+#ifndef THESIA_RYH
+#define THESIA_RYH 16  // horizontal pass: row blocks per image
+#endif
+#ifndef THESIA_H_2ROW
+#define THESIA_H_2ROW 1  // horizontal pass: two rows per block step
+#endif
+
 namespace thesia {
 
 // ------------------------------------------------------------------------------------
@@ -105,40 +125,52 @@ int launch_minmax(const float* x, uint64_t n, float* partial, int* nan_flag, int
 }
 
 // K3 over many tracks at once: segment s = elements [seg0[s], seg0[s+1]) of x; blockIdx.y is
-// the segment, blockIdx.x one of nper blocks striding through it.
-__global__ void minmax_seg_kernel(const float* x, const uint64_t* seg0, int nper, float* partial,
-                                  int* nan_flag) {
+// the segment, blockIdx.x one of nper blocks striding through it. 16-byte loads in the body
+// (the scalar head up to 16-byte alignment and the tail are read lane-wise), four independent
+// running max/min pairs per lane, a wave-level shuffle reduction.
+__device__ __forceinline__ void mm_acc(float v, float& mx, float& mn, int& nan) {
+    if (v != v) nan = 1;
+    mx = fmaxf(mx, v);
+    mn = fminf(mn, v);
+}
+__global__ void __launch_bounds__(256) minmax_seg_kernel(const float* x, const uint64_t* seg0, int nper,
+                                                         float* partial, int* nan_flag) {
     const int seg = blockIdx.y;
     const uint64_t beg = seg0[seg], end = seg0[seg + 1];
-    float mx = -INFINITY, mn = INFINITY;
+    float mx0 = -INFINITY, mn0 = INFINITY, mx1 = -INFINITY, mn1 = INFINITY;
     int nan = 0;
-    for (uint64_t i = beg + blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < end;
-         i += (uint64_t)nper * blockDim.x) {
-        const float v = x[i];
-        if (v != v) nan = 1;
-        mx = fmaxf(mx, v);
-        mn = fminf(mn, v);
+    const uint64_t n = end - beg;
+    const float* p = x + beg;
+    uint64_t head = (uint64_t)((4 - ((reinterpret_cast<uintptr_t>(p) >> 2) & 3)) & 3);
+    head = head < n ? head : n;
+    const uint64_t n4 = (n - head) / 4;
+    const uint64_t tid = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x, stride = (uint64_t)nper * blockDim.x;
+    if (tid < head) mm_acc(p[tid], mx0, mn0, nan);
+    const float4* p4 = reinterpret_cast<const float4*>(p + head);
+    for (uint64_t i = tid; i < n4; i += stride) {
+        const float4 v = p4[i];
+        mm_acc(v.x, mx0, mn0, nan);
+        mm_acc(v.y, mx1, mn1, nan);
+        mm_acc(v.z, mx0, mn0, nan);
+        mm_acc(v.w, mx1, mn1, nan);
     }
-    __shared__ float smx[256], smn[256];
-    __shared__ int snan;
-    if (threadIdx.x == 0) snan = 0;
-    __syncthreads();
-    smx[threadIdx.x] = mx;
-    smn[threadIdx.x] = mn;
-    if (nan) snan = 1;
-    __syncthreads();
-    for (int st = 128; st > 0; st >>= 1) {
-        if ((int)threadIdx.x < st) {
-            smx[threadIdx.x] = fmaxf(smx[threadIdx.x], smx[threadIdx.x + st]);
-            smn[threadIdx.x] = fminf(smn[threadIdx.x], smn[threadIdx.x + st]);
-        }
-        __syncthreads();
+    for (uint64_t i = head + 4 * n4 + tid; i < n; i += stride) mm_acc(p[i], mx0, mn0, nan);
+    float mx = fmaxf(mx0, mx1), mn = fminf(mn0, mn1);
+    for (int o = 32; o > 0; o >>= 1) {
+        mx = fmaxf(mx, __shfl_xor(mx, o, 64));
+        mn = fminf(mn, __shfl_xor(mn, o, 64));
     }
+    nan = __any(nan) ? 1 : 0;
+    __shared__ float smx[4], smn[4];
+    __shared__ int snan[4];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    if (lane == 0) { smx[wave] = mx; smn[wave] = mn; snan[wave] = nan; }
+    __syncthreads();
     if (threadIdx.x == 0) {
         const uint64_t o = ((uint64_t)seg * nper + blockIdx.x) * 2;
-        partial[o] = smx[0];
-        partial[o + 1] = smn[0];
-        if (snan) atomicOr(nan_flag + seg, 1);
+        partial[o] = fmaxf(fmaxf(smx[0], smx[1]), fmaxf(smx[2], smx[3]));
+        partial[o + 1] = fminf(fminf(smn[0], smn[1]), fminf(smn[2], smn[3]));
+        if (snan[0] | snan[1] | snan[2] | snan[3]) atomicOr(nan_flag + seg, 1);
     }
 }
 
@@ -406,8 +438,111 @@ __global__ void __launch_bounds__(256) resize_h_rgb_batch_kernel(uint32_t nh, co
     span = span < 0 ? 0 : (span > span_cap ? span_cap : span);
     const bool fits = !act || (l >= lb && l + n <= lb + span && (n <= kHTaps || wide));
     const bool staged = __syncthreads_and(fits) != 0;
-    for (uint32_t y = blockIdx.y; y < nh; y += gridDim.y) {
-        if (staged) {
+    // the next row's span is loaded into registers while this row is summed (one HBM latency
+    // per row otherwise: the pass was latency-bound), when it fits kHPf floats per thread
+    constexpr int kHPf = 8;
+    const bool pf = staged && span <= kHPf * 256;
+    float nx[kHPf];
+    auto load_row = [&](uint32_t yy) {
+        const float* src = tmp + r.tmp_off + (uint64_t)yy * r.T + lb;
+#pragma unroll
+        for (int p = 0; p < kHPf; ++p) {
+            const int32_t k = tid + 256 * p;
+            nx[p] = k < span ? src[k] : 0.0f;
+        }
+    };
+    auto store_row = [&](uint32_t yy, const uint8_t* sg) {
+        uint8_t* g = rgb + r.rgb_off + ((uint64_t)yy * r.nw + ox0) * 3;
+        const uint32_t mis = (uint32_t)(reinterpret_cast<uintptr_t>(g) & 3);
+        const uint32_t head = mis ? (4 - mis < nb ? 4 - mis : nb) : 0;
+        if ((uint32_t)tid < head) g[tid] = sg[tid];
+        const uint32_t nwords = (nb - head) / 4;
+        uint32_t* gw = reinterpret_cast<uint32_t*>(g + head);
+        for (uint32_t k = tid; k < nwords; k += 256) {
+            const uint32_t b = head + 4 * k;
+            gw[k] = (uint32_t)sg[b] | ((uint32_t)sg[b + 1] << 8) | ((uint32_t)sg[b + 2] << 16) |
+                    ((uint32_t)sg[b + 3] << 24);
+        }
+        for (uint32_t b = head + 4 * nwords + tid; b < nb; b += 256) g[b] = sg[b];
+    };
+    // rows below oz: their tmp rows are +0 (never formed) -> colormap(+0), no tmp reads
+    uint32_t ys = blockIdx.y;
+    if (r.oz > ys) {
+        if (act) colormap_px(0.0f, cm, seg + 3 * tid);
+        __syncthreads();
+        for (; ys < r.oz && ys < nh; ys += gridDim.y) store_row(ys, seg);
+        __syncthreads();
+    }
+#if THESIA_H_2ROW
+    if (pf && abl == 0) {
+        // two rows per step (y and y + G): two independent sum chains per column over the
+        // same weights, both rows' spans prefetched a step ahead
+        float* rin1 = reinterpret_cast<float*>(cm + 32);
+        uint8_t* seg1 = reinterpret_cast<uint8_t*>(rin1 + span_cap + kHTaps);
+        for (int k = tid; k < span_cap + kHTaps; k += 256) rin1[k] = 0.0f;
+        const uint32_t G = gridDim.y;
+        float nx1[kHPf];
+        auto load_row1 = [&](uint32_t yy) {
+            const float* src = tmp + r.tmp_off + (uint64_t)yy * r.T + lb;
+#pragma unroll
+            for (int p = 0; p < kHPf; ++p) {
+                const int32_t k = tid + 256 * p;
+                nx1[p] = k < span ? src[k] : 0.0f;
+            }
+        };
+        if (ys < nh) load_row(ys);
+        if (ys + G < nh) load_row1(ys + G);
+        for (uint32_t y = ys; y < nh; y += 2 * G) {
+            const bool two = y + G < nh;
+#pragma unroll
+            for (int p = 0; p < kHPf; ++p) {
+                const int32_t k = tid + 256 * p;
+                if (k < span) {
+                    rin[k] = nx[p];
+                    rin1[k] = nx1[p];
+                }
+            }
+            __syncthreads();
+            if (y + 2 * G < nh) load_row(y + 2 * G);
+            if (y + 3 * G < nh) load_row1(y + 3 * G);
+            if (act) {
+                float t0 = 0.0f, t1 = 0.0f;
+                const int base = l - lb;
+                if (n <= kHTaps) {
+#pragma unroll
+                    for (int i = 0; i < kHTaps; ++i) {
+                        t0 += rin[base + i] * w[i];
+                        t1 += rin1[base + i] * w[i];
+                    }
+                } else {
+                    for (int i = 0; i < n; ++i) {
+                        const float wi = wl[i * 256 + tid];
+                        t0 += rin[base + i] * wi;
+                        t1 += rin1[base + i] * wi;
+                    }
+                }
+                colormap_px(t0, cm, seg + 3 * tid);
+                colormap_px(t1, cm, seg1 + 3 * tid);
+            }
+            __syncthreads();
+            store_row(y, seg);
+            if (two) store_row(y + G, seg1);
+            __syncthreads();
+        }
+        return;
+    }
+#endif
+    if (pf && ys < nh) load_row(ys);
+    for (uint32_t y = ys; y < nh; y += gridDim.y) {
+        if (pf) {
+#pragma unroll
+            for (int p = 0; p < kHPf; ++p) {
+                const int32_t k = tid + 256 * p;
+                if (k < span) rin[k] = nx[p];
+            }
+            __syncthreads();
+            if (y + gridDim.y < nh) load_row(y + gridDim.y);
+        } else if (staged) {
             const float* src = tmp + r.tmp_off + (uint64_t)y * r.T + lb;
             if (!(abl & 4))  // ablation (timing only): no row loads
                 for (int32_t k = tid; k < span; k += 256) rin[k] = src[k];
@@ -435,18 +570,7 @@ __global__ void __launch_bounds__(256) resize_h_rgb_batch_kernel(uint32_t nh, co
         }
         __syncthreads();
         if (abl & 2) { __syncthreads(); continue; }  // ablation: no global stores
-        uint8_t* g = rgb + r.rgb_off + ((uint64_t)y * r.nw + ox0) * 3;
-        const uint32_t mis = (uint32_t)(reinterpret_cast<uintptr_t>(g) & 3);
-        const uint32_t head = mis ? (4 - mis < nb ? 4 - mis : nb) : 0;
-        if ((uint32_t)tid < head) g[tid] = seg[tid];
-        const uint32_t nwords = (nb - head) / 4;
-        uint32_t* gw = reinterpret_cast<uint32_t*>(g + head);
-        for (uint32_t k = tid; k < nwords; k += 256) {
-            const uint32_t b = head + 4 * k;
-            gw[k] = (uint32_t)seg[b] | ((uint32_t)seg[b + 1] << 8) | ((uint32_t)seg[b + 2] << 16) |
-                    ((uint32_t)seg[b + 3] << 24);
-        }
-        for (uint32_t b = head + 4 * nwords + tid; b < nb; b += 256) g[b] = seg[b];
+        store_row(y, seg);
         __syncthreads();
     }
 }
@@ -476,11 +600,203 @@ int launch_render_batch(const float* spec, uint32_t bins, float max, float min,
     // colormap; beyond 64 KiB the weights (then the span) stay in HBM (direct path)
     int taps = h_taps > kHTaps ? h_taps : 0;
     int span = h_span;
-    auto lds = [&]() { return (span + kHTaps + taps * 256) * 4 + 256 * 3 + 32; };
+    // span + zeros, wide weights, RGB segment, colormap; then the second row's span + segment
+    auto lds = [&]() { return (2 * (span + kHTaps) + taps * 256) * 4 + 2 * 256 * 3 + 32; };
     if (lds() > 65536) taps = 0;
     if (lds() > 65536) span = 4096;
     hipLaunchKernelGGL(resize_h_rgb_batch_kernel, g3, dim3(256), lds(), s, nh, d_desc, tmp, cmap, rgb,
                        taps, span, abl);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+// ------------------------------------------------------------------------------------
+// Fused display path (launch_render_batch2): grey + vertical Lanczos3 in one pass
+// ------------------------------------------------------------------------------------
+// K4+K5v: a block owns 64 frames x `band` output rows of one track (band: the widest band
+// whose grey rows and weights fit the LDS tile, chosen per launch by the host). The grey values those rows'
+// taps reach (display.rs:44-54: rows above the track's band are the image's zero fill) are formed
+// from the dB spectrogram straight into an LDS tile [grey row][frame] (each frame's bins read
+// contiguously), the band's tap weights into LDS; lane = frame, each wave walks its output rows:
+// tmp[oy][x] = sum_i grey[l + i][x] * w[i] in resize_v_px's order (t = 0; t += in * w), stored
+// along frames (coalesced). The grey image itself is never written (7.7 GB of the C5 step's
+// display traffic in the three-stage path).
+__device__ __forceinline__ float grey_of(float db, float max, float min) {  // grey_px
+    float v = (db - min) / (max - min);
+    v = fmaxf(v, 0.0f);
+    return fminf(v, 1.0f);
+}
+__global__ void __launch_bounds__(256) grey_vert_kernel(const float* spec, uint32_t bins, float max,
+                                                        float min, uint32_t nh, const RenderDesc* d,
+                                                        float* tmp, int tile_cap, int wcap, uint32_t band) {
+    extern __shared__ __attribute__((aligned(16))) float vsm[];
+    const RenderDesc r = d[blockIdx.z];
+    const uint32_t x0 = blockIdx.x * 64, ob = blockIdx.y * band;
+    const uint32_t oy1 = ob + band < nh ? ob + band : nh;
+    const uint32_t oy0 = ob > r.oz ? ob : r.oz;  // rows below oz: +0, never formed (RenderDesc)
+    if (x0 >= r.T || oy0 >= oy1) return;  // block-uniform
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    // grey rows [ya, yb) reached by the band's taps (supports are monotone in oy)
+    const int32_t ya = r.vl[oy0], yb = r.vl[oy1 - 1] + r.vc[oy1 - 1];
+    const int32_t rows = yb - ya;
+    const int32_t w0 = r.vo[oy0], wn = r.vo[oy1 - 1] + r.vc[oy1 - 1] - w0;
+    constexpr int TS = 65;                // tile row stride: the staging writes walk rows
+    int4* meta = reinterpret_cast<int4*>(vsm);  // per band row {tile row, taps, weight offset}
+    float* tile = vsm + 4 * (size_t)band;       // [rows][TS]
+    float* wl = tile + (size_t)tile_cap * TS;
+    const bool staged = rows <= tile_cap && wn <= wcap;
+    const uint32_t x = x0 + lane;
+    const int32_t H = (int32_t)r.H, top = (int32_t)r.H - (int32_t)bins;
+    const float* sp = spec + r.spec_off;
+#if THESIA_V_FLAT
+    if (staged) {
+        // (frame, row) pairs flattened over the block's 256 threads (f = e / rows by a
+        // multiply-high, exact for e < 2^14): consecutive threads read consecutive bins of one
+        // frame (coalesced) and a thread's THESIA_VDEPTH loads are in flight together; the zero
+        // fill above the track's band (y < top) and frames past T are never loaded
+        constexpr int D = THESIA_VDEPTH;
+        const int total = 64 * rows;
+        const uint32_t mrec = rows > 1 ? (uint32_t)((0x100000000ull + rows - 1) / (uint32_t)rows) : 0u;
+        for (int e0 = 0; e0 < total; e0 += 256 * D) {
+            float v[D];
+#pragma unroll
+            for (int i = 0; i < D; ++i) {
+                const uint32_t e = (uint32_t)(e0 + 256 * i + tid);
+                const uint32_t f = rows > 1 ? __umulhi(e, mrec) : e;
+                const int32_t k = (int32_t)(e - f * (uint32_t)rows), y = ya + k;
+                v[i] = 0.0f;
+                if ((int)e < total && y >= top && x0 + f < r.T)
+                    v[i] = sp[(uint64_t)(x0 + f) * bins + (uint32_t)(H - 1 - y)];
+            }
+#pragma unroll
+            for (int i = 0; i < D; ++i) {
+                const uint32_t e = (uint32_t)(e0 + 256 * i + tid);
+                const uint32_t f = rows > 1 ? __umulhi(e, mrec) : e;
+                const int32_t k = (int32_t)(e - f * (uint32_t)rows);
+                if ((int)e < total) tile[k * TS + f] = ya + k >= top ? grey_of(v[i], max, min) : 0.0f;
+            }
+        }
+        for (int32_t i = tid; i < wn; i += 256) wl[i] = r.vw[w0 + i];
+        for (uint32_t j = tid; j < oy1 - oy0; j += 256)
+            meta[j] = make_int4(r.vl[oy0 + j] - ya, r.vc[oy0 + j], r.vo[oy0 + j] - w0, 0);
+    }
+#else
+    if (staged) {
+        // grey row y of frame x is bin H-1-y: the tile's rows run down the frame's bins, so a
+        // wave reading 64 consecutive rows of one frame reads 64 consecutive bins
+        // 4 frames x up to 4 row blocks of loads in flight per wave step (a frame at a time
+        // left each wave waiting out one HBM latency per 64 rows)
+        for (int fb = wave; fb < 64; fb += 16) {
+            float v[4][4];
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const uint32_t xf = x0 + fb + 4 * j;
+                const float* srow = sp + (uint64_t)(xf < r.T ? xf : r.T - 1) * bins;
+#pragma unroll
+                for (int kb = 0; kb < 4; ++kb) {
+                    const int32_t k = kb * 64 + lane, y = ya + k;
+                    v[j][kb] = 0.0f;
+                    if (k < rows && y >= top) v[j][kb] = srow[H - 1 - y];  // zero fill: no load
+                }
+            }
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+#pragma unroll
+                for (int kb = 0; kb < 4; ++kb) {
+                    const int32_t k = kb * 64 + lane, y = ya + k;
+                    if (k < rows) tile[k * TS + fb + 4 * j] = y >= top ? grey_of(v[j][kb], max, min) : 0.0f;
+                }
+        }
+        for (int32_t i = tid; i < wn; i += 256) wl[i] = r.vw[w0 + i];
+    }
+#endif
+    __syncthreads();
+    if (x >= r.T) return;  // no block barrier below
+    float* out = tmp + r.tmp_off + x;
+    uint32_t oy = oy0 + wave;
+#if THESIA_V_ILP
+    if (staged) {
+        // four output rows at a time: four independent chains (each in its own order) keep
+        // the wave issuing while one chain waits on its previous fma
+        for (; oy + 12 < oy1; oy += 16) {
+            int32_t l[4], n[4], wo[4];
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+#if THESIA_V_FLAT
+                const int4 m = meta[oy - oy0 + 4 * q];  // LDS broadcast (no scalar-load wait)
+                l[q] = m.x;
+                n[q] = m.y;
+                wo[q] = m.z;
+#else
+                l[q] = r.vl[oy + 4 * q] - ya;
+                n[q] = r.vc[oy + 4 * q];
+                wo[q] = r.vo[oy + 4 * q] - w0;
+#endif
+            }
+            const int32_t n01 = n[0] > n[1] ? n[0] : n[1], n23 = n[2] > n[3] ? n[2] : n[3];
+            const int32_t nmax = n01 > n23 ? n01 : n23;
+            float t[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+            for (int32_t i = 0; i < nmax; ++i) {
+#pragma unroll
+                for (int q = 0; q < 4; ++q)
+                    if (i < n[q]) t[q] += tile[(l[q] + i) * TS + lane] * wl[wo[q] + i];
+            }
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+#if THESIA_V_ABL & 1  // ablation (timing only): no tmp stores
+                if (t[q] == 1.2345e-30f)
+#endif
+                    out[(uint64_t)(oy + 4 * q) * r.T] = t[q];
+            }
+        }
+    }
+#endif
+    for (; oy < oy1; oy += 4) {
+        const int32_t l = r.vl[oy], n = r.vc[oy];  // row-uniform: scalar loads
+        float t = 0.0f;
+        if (staged) {
+            const float* wr = wl + (r.vo[oy] - w0);
+            const float* col = tile + (l - ya) * TS + lane;
+            for (int32_t i = 0; i < n; ++i) t += col[i * TS] * wr[i];
+        } else {
+            const float* wr = r.vw + r.vo[oy];
+            const float* srow = sp + (uint64_t)x * bins;
+            for (int32_t i = 0; i < n; ++i) {
+                const int32_t y = l + i;
+                t += (y >= top ? grey_of(srow[H - 1 - y], max, min) : 0.0f) * wr[i];
+            }
+        }
+        out[(uint64_t)oy * r.T] = t;
+    }
+}
+
+int launch_render_batch2(const float* spec, uint32_t bins, float max, float min,
+                         const RenderDesc* d_desc, uint32_t n, uint32_t T_max, uint32_t H_max,
+                         uint32_t nw_max, uint32_t nh, int h_taps, int h_span, uint32_t v_band,
+                         int v_rows, int v_wts, float* tmp, const uint8_t* cmap, uint8_t* rgb,
+                         hipStream_t s) {
+    if (n == 0 || nh == 0 || v_band == 0) return 0;
+    if (n > 65535) return -2;
+    (void)H_max;
+    // K4+K5v: the band's grey tile and weights in LDS (bands that do not fit read HBM directly)
+    const int tile_cap = v_rows < 256 ? v_rows : 256, wcap = v_wts < 4096 ? v_wts : 4096;
+    const int lds1 = (tile_cap * 65 + wcap + 4 * (int)v_band) * 4;
+    if (hipFuncSetAttribute(reinterpret_cast<const void*>(grey_vert_kernel),
+                            hipFuncAttributeMaxDynamicSharedMemorySize, lds1) != hipSuccess)
+        return -1;
+    dim3 g1((T_max + 63) / 64, (nh + v_band - 1) / v_band, n);
+    hipLaunchKernelGGL(grey_vert_kernel, g1, dim3(256), lds1, s, spec, bins, max, min, nh, d_desc, tmp,
+                       tile_cap, wcap, v_band);
+    // K5h + K6: the three-stage path's horizontal pass (same intermediate layout [nh][T])
+    const uint32_t ry_h = THESIA_RYH;
+    dim3 g3((nw_max + 255) / 256, nh < ry_h ? nh : ry_h, n);
+    int taps = h_taps > kHTaps ? h_taps : 0;
+    int span = h_span;
+    // span + zeros, wide weights, RGB segment, colormap; then the second row's span + segment
+    auto lds = [&]() { return (2 * (span + kHTaps) + taps * 256) * 4 + 2 * 256 * 3 + 32; };
+    if (lds() > 65536) taps = 0;
+    if (lds() > 65536) span = 4096;
+    hipLaunchKernelGGL(resize_h_rgb_batch_kernel, g3, dim3(256), lds(), s, nh, d_desc, tmp, cmap, rgb,
+                       taps, span, 0);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 

@@ -607,7 +607,7 @@ int minmax_device(const float* d_x, uint64_t n, float* mx, float* mn, bool* nan,
 static int g_render_path = 0;  // thesia_set_render_path
 int render_path() { return __atomic_load_n(&g_render_path, __ATOMIC_RELAXED); }
 int set_render_path(int path) {
-    if (path != 0 && path != 1) return set_error(THESIA_ERR_INVALID_ARG, "render path must be 0 or 1");
+    if (path < 0 || path > 2) return set_error(THESIA_ERR_INVALID_ARG, "render path must be 0, 1 or 2");
     __atomic_store_n(&g_render_path, path, __ATOMIC_RELAXED);
     return THESIA_OK;
 }
@@ -624,6 +624,7 @@ static std::vector<uint8_t> colormap_bytes() {
 struct DevTaps {
     DevBuf left, count, offset, weights;
     int max_taps = 0;
+    std::vector<int32_t> h_left, h_count;  // host copies (block spans of the fused render)
 };
 
 static int dev_taps(uint32_t n, uint32_t nn, const DevTaps** out) {
@@ -644,6 +645,8 @@ static int dev_taps(uint32_t n, uint32_t nn, const DevTaps** out) {
         if (!rc) rc = d->weights.upload(t.weights.data(), t.weights.size() * 4);
         if (rc) return rc;
         d->max_taps = t.max_taps;
+        d->h_left.assign(t.left.begin(), t.left.end());
+        d->h_count.assign(t.count.begin(), t.count.end());
         it = cache.emplace(key, std::move(d)).first;
     }
     *out = it->second.get();
@@ -689,35 +692,232 @@ int grey_to_rgb_device(const float* d_grey, uint32_t w, uint32_t h, uint32_t nw,
     return THESIA_OK;
 }
 
+int minmax_segments_multi(size_t n_groups, const float* const* d_x, const uint64_t* const* row0,
+                          const size_t* bins, const size_t* ns, float* mx, float* mn, int* nan,
+                          hipStream_t s) {
+    // every group's segment table in one upload, the launches back to back, one readback
+    std::vector<uint64_t> seg;
+    std::vector<int> nper(n_groups);
+    std::vector<size_t> seg0(n_groups), part0(n_groups), trk0(n_groups);
+    size_t ntr = 0, npart = 0;
+    for (size_t k = 0; k < n_groups; ++k) {
+        const size_t n = ns[k];
+        seg0[k] = seg.size();
+        part0[k] = npart;
+        trk0[k] = ntr;
+        if (n == 0) continue;
+        // blocks per track: enough to fill the device at the group's total size
+        const uint64_t tot = (row0[k][n] - row0[k][0]) * bins[k];
+        nper[k] = (int)std::min<uint64_t>(64, std::max<uint64_t>(1, (tot / n) / (256 * 4 * 8)));
+        for (size_t i = 0; i <= n; ++i) seg.push_back(row0[k][i] * bins[k]);
+        npart += n * nper[k];
+        ntr += n;
+    }
+    if (ntr == 0) return THESIA_OK;
+    // grow-only per-device workspace (a hipMalloc per call cost more than the reduction)
+    struct Ws { DevBuf seg, part, flag; };
+    static std::mutex ws_mu;
+    static auto& ws_map = *new std::map<int, Ws>();  // leaked, see dev_taps
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    std::lock_guard<std::mutex> lk(ws_mu);
+    Ws& ws = ws_map[dev];
+    auto grow = [](DevBuf& b, size_t bytes) {
+        if (b.bytes >= bytes && b.p) return 0;
+        b.release();
+        return b.alloc(bytes + bytes / 8);
+    };
+    int rc = grow(ws.seg, seg.size() * 8);
+    if (!rc) rc = grow(ws.part, npart * 2 * sizeof(float));
+    if (!rc) rc = grow(ws.flag, ntr * sizeof(int));
+    if (rc) return rc;
+    THESIA_HIP(hipMemcpyAsync(ws.seg.p, seg.data(), seg.size() * 8, hipMemcpyHostToDevice, s));
+    THESIA_HIP(hipMemsetAsync(ws.flag.p, 0, ntr * sizeof(int), s));
+    for (size_t k = 0; k < n_groups; ++k) {
+        if (ns[k] == 0) continue;
+        if (launch_minmax_seg(d_x[k], ws.seg.as<uint64_t>() + seg0[k], (int)ns[k], nper[k],
+                              ws.part.as<float>() + 2 * part0[k], ws.flag.as<int>() + trk0[k], s))
+            return set_error(THESIA_ERR_DEVICE, "minmax_seg launch failed");
+    }
+    std::vector<float> h(npart * 2);
+    std::vector<int> hf(ntr);
+    THESIA_HIP(hipMemcpyAsync(h.data(), ws.part.p, h.size() * sizeof(float), hipMemcpyDeviceToHost, s));
+    THESIA_HIP(hipMemcpyAsync(hf.data(), ws.flag.p, ntr * sizeof(int), hipMemcpyDeviceToHost, s));
+    THESIA_HIP(hipStreamSynchronize(s));
+    for (size_t k = 0; k < n_groups; ++k)
+        for (size_t i = 0; i < ns[k]; ++i) {
+            float a = -INFINITY, b = INFINITY;  // empty track: ndarray-stats EmptyInput -> -inf / +inf
+            const float* p = h.data() + 2 * (part0[k] + i * nper[k]);
+            for (int q = 0; q < nper[k]; ++q) {
+                a = fmaxf(a, p[2 * q]);
+                b = fminf(b, p[2 * q + 1]);
+            }
+            mx[trk0[k] + i] = a;
+            mn[trk0[k] + i] = b;
+            nan[trk0[k] + i] = hf[trk0[k] + i];
+        }
+    return THESIA_OK;
+}
+
 int minmax_segments_device(const float* d_x, const uint64_t* row0, size_t bins, size_t n,
                            float* mx, float* mn, int* nan, hipStream_t s) {
-    if (n == 0) return THESIA_OK;
-    const int nper = 16;
-    std::vector<uint64_t> seg(n + 1);
-    for (size_t i = 0; i <= n; ++i) seg[i] = row0[i] * bins;
-    DevBuf dseg, part, flag;
-    int rc = dseg.upload(seg.data(), seg.size() * 8);
-    if (!rc) rc = part.alloc(n * nper * 2 * sizeof(float));
-    if (!rc) rc = flag.alloc(n * sizeof(int));
-    if (rc) return rc;
-    THESIA_HIP(hipMemsetAsync(flag.p, 0, n * sizeof(int), s));
-    if (launch_minmax_seg(d_x, dseg.as<uint64_t>(), (int)n, nper, part.as<float>(), flag.as<int>(), s))
-        return set_error(THESIA_ERR_DEVICE, "minmax_seg launch failed");
-    std::vector<float> h(n * nper * 2);
-    std::vector<int> hf(n);
-    THESIA_HIP(hipMemcpyAsync(h.data(), part.p, h.size() * sizeof(float), hipMemcpyDeviceToHost, s));
-    THESIA_HIP(hipMemcpyAsync(hf.data(), flag.p, n * sizeof(int), hipMemcpyDeviceToHost, s));
-    THESIA_HIP(hipStreamSynchronize(s));
-    for (size_t i = 0; i < n; ++i) {
-        float a = -INFINITY, b = INFINITY;  // empty track: ndarray-stats EmptyInput -> -inf / +inf
-        for (int k = 0; k < nper; ++k) {
-            a = fmaxf(a, h[(i * nper + k) * 2]);
-            b = fminf(b, h[(i * nper + k) * 2 + 1]);
-        }
-        mx[i] = a;
-        mn[i] = b;
-        nan[i] = hf[i];
+    return minmax_segments_multi(1, &d_x, &row0, &bins, &n, mx, mn, nan, s);
+}
+
+#ifndef THESIA_VBAND
+#define THESIA_VBAND 512  // widest vertical band tried
+#endif
+#ifndef THESIA_VROWS
+#define THESIA_VROWS 128  // grey rows per vertical tile (<= 256; A/B via scripts/build_variant.sh)
+#endif
+
+namespace {
+
+const uint8_t* colormap_device(int* rc) {  // the colormap LUT, once per device
+    static std::mutex mu;
+    static auto& cmaps = *new std::map<int, DevBuf>();  // leaked, see dev_taps
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    std::lock_guard<std::mutex> lk(mu);
+    DevBuf& cm = cmaps[dev];
+    *rc = 0;
+    if (!cm.p) {
+        std::vector<uint8_t> bytes = colormap_bytes();
+        *rc = cm.upload(bytes.data(), bytes.size());
+        if (*rc) return nullptr;
     }
+    return cm.as<uint8_t>();
+}
+
+// One group of the fused display path: tracks sharing one spectrogram buffer and bin count.
+struct FusedGroup {
+    const float* spec = nullptr;
+    uint32_t bins = 0;
+    size_t desc0 = 0, ndesc = 0;  // its RenderDesc range in the call's table
+    uint64_t tmp_tot = 0;         // intermediate floats ([nheight][T] per track)
+    uint32_t T_max = 0, H_max = 0, nw_max = 0, v_band = 1;
+    int h_taps = 0, h_span = 0, v_rows = 1, v_wts = 1;
+};
+
+// Host planning of one group: a RenderDesc per non-empty track (appended to `desc`), the
+// vertical band (the widest whose grey rows <= THESIA_VROWS and weights <= 4096 fit the LDS
+// tile for every track of the group) and the horizontal pass's tap / span bounds.
+int plan_fused_group(const float* d_spec, const uint64_t* row0, size_t bins, size_t n,
+                     const float* up_ratio, const uint32_t* nwidth, uint32_t nheight,
+                     const uint64_t* rgb_off, std::vector<RenderDesc>& desc, FusedGroup& g) {
+    g.spec = d_spec;
+    g.bins = (uint32_t)bins;
+    g.desc0 = desc.size();
+    std::vector<std::pair<const DevTaps*, uint32_t>> vts;  // (vertical taps, oz)
+    for (size_t i = 0; i < n; ++i) {
+        const float hf = roundf((float)bins * up_ratio[i]);  // display.rs:46
+        const uint32_t H = hf > 0.f ? (uint32_t)hf : 0u;
+        if (H < bins) return set_error(THESIA_ERR_INVALID_ARG, "up_ratio < 1 (display.rs:47 underflows)");
+        const uint32_t T = (uint32_t)(row0[i + 1] - row0[i]);
+        if (T == 0 || nwidth[i] == 0) continue;
+        const DevTaps *vt = nullptr, *ht = nullptr;
+        int rc = dev_taps(H, nheight, &vt);
+        if (!rc) rc = dev_taps(T, nwidth[i], &ht);
+        if (rc) return rc;
+        RenderDesc r{};
+        r.spec_off = row0[i] * bins;
+        r.tmp_off = g.tmp_tot;
+        r.rgb_off = rgb_off[i];
+        r.T = T;
+        r.H = H;
+        r.nw = nwidth[i];
+        r.vl = vt->left.as<int32_t>(); r.vc = vt->count.as<int32_t>();
+        r.vo = vt->offset.as<int32_t>(); r.vw = vt->weights.as<float>();
+        r.hl = ht->left.as<int32_t>(); r.hc = ht->count.as<int32_t>();
+        r.ho = ht->offset.as<int32_t>(); r.hw = ht->weights.as<float>();
+        // oz: output rows whose taps end at or above the band's top row H - bins
+        const int32_t top = (int32_t)H - (int32_t)bins;
+        uint32_t oz = 0;
+        while (oz < nheight && vt->h_left[oz] + vt->h_count[oz] <= top) ++oz;
+        r.oz = oz;
+        if (std::find(vts.begin(), vts.end(), std::make_pair(vt, oz)) == vts.end()) vts.emplace_back(vt, oz);
+        g.tmp_tot += (uint64_t)T * nheight;
+        g.h_taps = std::max(g.h_taps, ht->max_taps);
+        g.h_span = std::max<int>(g.h_span, (int)((256.0 * T + nwidth[i] - 1) / nwidth[i]) + ht->max_taps + 8);
+        g.T_max = std::max(g.T_max, T);
+        g.H_max = std::max(g.H_max, H);
+        g.nw_max = std::max(g.nw_max, nwidth[i]);
+        desc.push_back(r);
+    }
+    g.ndesc = desc.size() - g.desc0;
+    auto band_need = [&](uint32_t band, int* rows_out, int* wts_out) {
+        int rows = 1, wts = 1;
+        for (const auto& [vt, oz] : vts)
+            for (uint32_t ob = 0; ob < nheight; ob += band) {
+                const uint32_t o0 = std::max(ob, oz), o1 = std::min(nheight, ob + band) - 1;
+                if (o0 > o1) continue;
+                rows = std::max(rows, vt->h_left[o1] + vt->h_count[o1] - vt->h_left[o0]);
+                int wn = 0;
+                for (uint32_t o = o0; o <= o1; ++o) wn += vt->h_count[o];
+                wts = std::max(wts, wn);
+            }
+        *rows_out = rows;
+        *wts_out = wts;
+        return rows <= THESIA_VROWS && wts <= 4096;
+    };
+    // the widest band that fits (measured: THESIA_VROWS 128 beats 256 on C5, the smaller tile
+    // doubling the blocks resident per CU)
+    g.v_band = THESIA_VBAND;
+    while (!band_need(g.v_band, &g.v_rows, &g.v_wts) && g.v_band > 1) g.v_band /= 2;
+    return THESIA_OK;
+}
+
+}  // namespace
+
+int render_rgb_fused(size_t n_groups, const float* const* d_specs, const uint64_t* const* row0s,
+                     const size_t* bins, const size_t* ns, const float* up_ratio,
+                     const uint32_t* nwidth, uint32_t nheight, float max, float min, uint8_t* d_rgb,
+                     const uint64_t* rgb_off, hipStream_t s) {
+    if (nheight == 0) return THESIA_OK;
+    int rc = 0;
+    const uint8_t* cmap_ptr = colormap_device(&rc);
+    if (rc) return rc;
+    // host planning of every group first, then one table upload and the launches back to
+    // back on the stream (the groups reuse one intermediate: stream order makes that safe)
+    std::vector<RenderDesc> desc;
+    std::vector<FusedGroup> groups(n_groups);
+    uint64_t tmp_max = 1;
+    size_t t0 = 0;
+    for (size_t k = 0; k < n_groups; ++k) {
+        rc = plan_fused_group(d_specs[k], row0s[k], bins[k], ns[k], up_ratio + t0, nwidth + t0, nheight,
+                              rgb_off + t0, desc, groups[k]);
+        if (rc) return rc;
+        tmp_max = std::max<uint64_t>(tmp_max, groups[k].tmp_tot);
+        t0 += ns[k];
+    }
+    if (desc.empty()) return THESIA_OK;
+    struct Ws { DevBuf tmp, desc; };
+    static std::mutex ws_mu;
+    static auto& ws_map = *new std::map<int, Ws>();  // leaked, see dev_taps
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    std::lock_guard<std::mutex> lk(ws_mu);
+    Ws& ws = ws_map[dev];
+    auto grow = [](DevBuf& b, size_t bytes) {
+        if (b.bytes >= bytes && b.p) return 0;
+        b.release();
+        return b.alloc(bytes + bytes / 8);
+    };
+    rc = grow(ws.tmp, tmp_max * sizeof(float));
+    if (!rc) rc = grow(ws.desc, desc.size() * sizeof(RenderDesc));
+    if (rc) return rc;
+    THESIA_HIP(hipMemcpyAsync(ws.desc.p, desc.data(), desc.size() * sizeof(RenderDesc),
+                              hipMemcpyHostToDevice, s));
+    for (const FusedGroup& g : groups)
+        for (size_t b = 0; b < g.ndesc; b += 65535) {  // grid.z limit
+            const uint32_t nb = (uint32_t)std::min<size_t>(65535, g.ndesc - b);
+            if (launch_render_batch2(g.spec, g.bins, max, min, ws.desc.as<RenderDesc>() + g.desc0 + b, nb,
+                                     g.T_max, g.H_max, g.nw_max, nheight, g.h_taps, g.h_span, g.v_band,
+                                     g.v_rows, g.v_wts, ws.tmp.as<float>(), cmap_ptr, d_rgb, s))
+                return set_error(THESIA_ERR_DEVICE, "render batch launch failed");
+        }
+    // the table upload reads `desc` (pageable host memory) until it has run
+    THESIA_HIP(hipStreamSynchronize(s));
     return THESIA_OK;
 }
 
@@ -738,22 +938,16 @@ int render_rgb_batch_device(const float* d_spec, const uint64_t* row0, size_t bi
         grey_max = std::max<size_t>(grey_max, (size_t)H[i] * T);
         tmp_max = std::max<size_t>(tmp_max, (size_t)T * nheight);
     }
-    const uint8_t* cmap_ptr = nullptr;
-    {
-        static std::mutex mu;
-        static auto& cmaps = *new std::map<int, DevBuf>();  // leaked, see dev_taps
-        int dev = 0;
-        (void)hipGetDevice(&dev);
-        std::lock_guard<std::mutex> lk(mu);
-        DevBuf& cm = cmaps[dev];
-        if (!cm.p) {
-            std::vector<uint8_t> bytes = colormap_bytes();
-            int rc = cm.upload(bytes.data(), bytes.size());
-            if (rc) return rc;
-        }
-        cmap_ptr = cm.as<uint8_t>();
-    }
+    int crc = 0;
+    const uint8_t* cmap_ptr = colormap_device(&crc);
+    if (crc) return crc;
     if (render_path() == 0) {
+        const size_t ns[1] = {n};
+        const size_t bs[1] = {bins};
+        return render_rgb_fused(1, &d_spec, &row0, bs, ns, up_ratio, nwidth, nheight, max, min, d_rgb,
+                                rgb_off, s);
+    }
+    if (render_path() == 2) {
         // every track in one launch per stage (launch_render_batch); workspaces for all tracks
         std::vector<RenderDesc> desc;
         desc.reserve(n);

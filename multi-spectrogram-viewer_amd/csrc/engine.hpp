@@ -101,7 +101,9 @@ int batch_create(Plan* plan, const thesia_batch_desc& d, Batch** out);
 int batch_run(Batch* b, hipStream_t s);
 int batch_set_option(Batch* b, int option, int64_t value);  // thesia_batch_set_option
 
-// display path selection (thesia_set_render_path): 0 batched launches, 1 per-track launches
+// display path selection (thesia_set_render_path): 0 fused batched launches (grey + vertical
+// in one pass, then horizontal + colormap), 1 per-track launches, 2 three-stage batched
+// launches (grey, vertical, horizontal + colormap)
 int render_path();
 int set_render_path(int path);
 
@@ -117,6 +119,16 @@ int minmax_segments_device(const float* d_x, const uint64_t* row0, size_t bins, 
                            float* mx, float* mn, int* nan, hipStream_t s);
 // K4-K6 for n tracks packed in one buffer, one stream, one sync: track i's [T_i, bins] dB rows
 // -> grey [H_i, T_i] (H_i = round(bins * up_ratio[i])) -> Lanczos3 -> RGB at rgb_off[i].
+// Several groups (each: one spectrogram buffer, its bin count, ns[k] tracks) in one call: the
+// per-track arrays (up_ratio, nwidth, rgb_off; outputs mx/mn/nan) are concatenated in group
+// order. One host->device table upload and one stream synchronisation per call.
+int minmax_segments_multi(size_t n_groups, const float* const* d_x, const uint64_t* const* row0,
+                          const size_t* bins, const size_t* ns, float* mx, float* mn, int* nan,
+                          hipStream_t s);
+int render_rgb_fused(size_t n_groups, const float* const* d_specs, const uint64_t* const* row0s,
+                     const size_t* bins, const size_t* ns, const float* up_ratio,
+                     const uint32_t* nwidth, uint32_t nheight, float max, float min, uint8_t* d_rgb,
+                     const uint64_t* rgb_off, hipStream_t s);
 int render_rgb_batch_device(const float* d_spec, const uint64_t* row0, size_t bins, size_t n,
                             const float* up_ratio, const uint32_t* nwidth, uint32_t nheight,
                             float max, float min, uint8_t* d_rgb, const uint64_t* rgb_off,

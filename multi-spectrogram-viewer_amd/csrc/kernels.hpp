@@ -117,7 +117,12 @@ int launch_minmax_seg(const float* x, const uint64_t* seg0, int n_seg, int nper,
 // horizontal (T -> nw) Lanczos3 tap tables (device pointers, cached per geometry).
 struct RenderDesc {
     uint64_t spec_off, grey_off, tmp_off, rgb_off;
-    uint32_t T, H, nw, pad;
+    uint32_t T, H, nw;
+    // oz: leading output rows whose vertical taps reach only the zero fill above the track's
+    // band (display.rs:44-54). Their sums are +0 exactly (t = +0; t += 0 * w stays +0), so the
+    // fused path neither forms nor reads them: colormap(+0) rows. 0 = no shortcut.
+    uint32_t oz;
+
     const int32_t *vl, *vc, *vo;
     const float* vw;
     const int32_t *hl, *hc, *ho;
@@ -127,6 +132,16 @@ int launch_render_batch(const float* spec, uint32_t bins, float max, float min,
                         const RenderDesc* d_desc, uint32_t n, uint32_t T_max, uint32_t H_max,
                         uint32_t nw_max, uint32_t nh, int h_taps, int h_span, float* grey,
                         float* tmp, const uint8_t* cmap, uint8_t* rgb, hipStream_t s);
+// The fused display path: grey + vertical Lanczos3 in one pass over the dB spectrogram (the
+// grey image is never materialised), then the batched horizontal Lanczos3 + colormap. Same
+// per-pixel arithmetic and summation order as launch_render_batch (bit-identical bytes).
+// v_band: output rows per vertical block; v_rows / v_wts: the largest grey-row span / weight
+// count of such a band (its LDS tile).
+int launch_render_batch2(const float* spec, uint32_t bins, float max, float min,
+                         const RenderDesc* d_desc, uint32_t n, uint32_t T_max, uint32_t H_max,
+                         uint32_t nw_max, uint32_t nh, int h_taps, int h_span, uint32_t v_band,
+                         int v_rows, int v_wts, float* tmp, const uint8_t* cmap, uint8_t* rgb,
+                         hipStream_t s);
 int launch_spec_to_grey(const float* spec, uint32_t T, uint32_t bins, uint32_t H, float max,
                         float min, float* grey, hipStream_t s);
 int launch_resize_v(const float* in, uint32_t w, uint32_t h, uint32_t nh, const int32_t* left,

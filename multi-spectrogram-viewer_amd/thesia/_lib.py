@@ -96,6 +96,11 @@ _SIGS = {
     "thesia_minmax_segments_device": (_i, [C.c_void_p, _u64p, _sz, _sz, _fp, _fp, C.POINTER(C.c_int)]),
     "thesia_render_rgb_batch_device": (_i, [C.c_void_p, _u64p, _sz, _sz, _fp, C.POINTER(C.c_uint32),
                                             _u32, _f, _f, C.c_void_p, _u64p]),
+    "thesia_minmax_segments_multi": (_i, [_sz, C.POINTER(C.c_void_p), C.POINTER(_u64p), C.POINTER(_sz),
+                                          C.POINTER(_sz), _fp, _fp, C.POINTER(C.c_int)]),
+    "thesia_render_rgb_multi": (_i, [_sz, C.POINTER(C.c_void_p), C.POINTER(_u64p), C.POINTER(_sz),
+                                     C.POINTER(_sz), _fp, C.POINTER(C.c_uint32), _u32, _f, _f, C.c_void_p,
+                                     _u64p]),
     "thesia_mt_create": (_i, [C.POINTER(_vp)]),
     "thesia_mt_destroy": (None, [_vp]),
     "thesia_mt_set_setting": (_i, [_vp, _f, _sz, _sz, _i, _f]),

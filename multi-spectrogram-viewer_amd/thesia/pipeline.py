@@ -39,7 +39,7 @@ class Track:
 class Rendered:
     db: Optional[np.ndarray]  # [T, n_fft/2+1] amp dB (only when keep_db)
     rgb: np.ndarray           # u8 [nheight * nwidth * 3] (display.rs:56-61; a view of the
-                              # group's one device-to-host copy)
+                              # call's one device-to-host copy)
     nwidth: int
     spec_max: float
     spec_min: float
@@ -60,8 +60,8 @@ class RenderPipeline:
 
     def __init__(self, tracks: Sequence[Track], px_per_sec: float = 100.0, nheight: int = 500,
                  db_range: float = 120.0, pinned_output: bool = False):
-        """pinned_output: read the RGB images back into one page-locked host buffer per
-        geometry group (DMA-rate copies); the returned images are then views that the next
+        """pinned_output: read the RGB images back into one page-locked host buffer (one
+        DMA-rate copy per render); the returned images are then views that the next
         render() overwrites. Default: fresh pageable arrays per render()."""
         self.tracks = list(tracks)
         self.pinned_output = pinned_output
@@ -87,15 +87,24 @@ class RenderPipeline:
                 f0, f1 = int(b.frame0[k]), int(b.frame0[k + 1])
                 self.where[i] = (g, f0 * plan.row_bins, f1 - f0, plan.row_bins)
         self.total_frames = sum(grp[3].total_frames for grp in self.groups)
-        # display buffers, sized once
+        # display geometry, fixed for the pipeline's life: every group in one library call
+        # (thesia_minmax_segments_multi / thesia_render_rgb_multi), tracks in group order
         self._geo = []
-        max_rgb = 1
         for i, t in enumerate(self.tracks):
-            _, _, T, bins = self.where[i]
-            nwidth = int(np.float32(px_per_sec) * np.float32(t.pcm.shape[0]) / np.float32(t.sr))
-            self._geo.append(nwidth)
-            max_rgb = max(max_rgb, nwidth * nheight * 3)
-        self._rgb = engine.DeviceBuffer(max_rgb)
+            self._geo.append(int(np.float32(px_per_sec) * np.float32(t.pcm.shape[0]) / np.float32(t.sr)))
+        self._order = np.array([i for idx in groups.values() for i in idx], np.int64)
+        ng = len(self.groups)
+        self._row0 = [np.ascontiguousarray(b.frame0, np.uint64) for _, _, _, b in self.groups]
+        self._c_specs = (C.c_void_p * max(ng, 1))(*[dout.ptr.value for _, _, dout, _ in self.groups])
+        self._c_row0 = (_u64p * max(ng, 1))(*[r.ctypes.data_as(_u64p) for r in self._row0])
+        self._c_bins = (C.c_size_t * max(ng, 1))(*[plan.row_bins for plan, _, _, _ in self.groups])
+        self._c_ns = (C.c_size_t * max(ng, 1))(*[len(idx) for idx in groups.values()])
+        self._nw = np.array([self._geo[i] for i in self._order], np.uint32)
+        self._sizes = self._nw.astype(np.uint64) * nheight * 3
+        self._off = np.concatenate([[0], np.cumsum(self._sizes)[:-1]]).astype(np.uint64)
+        self._rgb_total = int(self._sizes.sum())
+        self._rgb = engine.DeviceBuffer(max(self._rgb_total, 1))
+        self._up = {}  # max_sr -> up_ratio per track (call order)
 
     def run_spectrograms(self) -> None:
         """One kernel launch per geometry group (asynchronous)."""
@@ -107,21 +116,19 @@ class RenderPipeline:
         return C.c_void_p(self.groups[g][2].ptr.value + row0 * 4), T, bins
 
     def ranges(self):
-        """Per-track (max, min) dB (lib.rs:194-207): one segmented reduction per group."""
+        """Per-track (max, min) dB (lib.rs:194-207): one segmented reduction per group, all
+        groups in one library call (one synchronisation)."""
+        n = len(self._order)
+        mx = np.empty(n, np.float32)
+        mn = np.empty(n, np.float32)
+        nan = np.empty(n, np.int32)
+        check(lib.thesia_minmax_segments_multi(len(self.groups), self._c_specs, self._c_row0, self._c_bins,
+                                               self._c_ns, mx.ctypes.data_as(_fp), mn.ctypes.data_as(_fp),
+                                               nan.ctypes.data_as(C.POINTER(C.c_int))))
         out = [None] * len(self.tracks)
-        for g, (plan, _, dout, b) in enumerate(self.groups):
-            idx = [i for i in range(len(self.tracks)) if self.where[i][0] == g]
-            n = len(idx)
-            mx = np.empty(n, np.float32)
-            mn = np.empty(n, np.float32)
-            nan = np.empty(n, np.int32)
-            row0 = np.ascontiguousarray(b.frame0, np.uint64)
-            check(lib.thesia_minmax_segments_device(dout.ptr, row0.ctypes.data_as(_u64p), plan.row_bins,
-                                                    n, mx.ctypes.data_as(_fp), mn.ctypes.data_as(_fp),
-                                                    nan.ctypes.data_as(C.POINTER(C.c_int))))
-            for k, i in enumerate(idx):
-                # ndarray-stats max/min error on NaN -> unwrap_or(-inf / +inf) (lib.rs:198-199)
-                out[i] = (-np.inf, np.inf) if nan[k] else (float(mx[k]), float(mn[k]))
+        for k, i in enumerate(self._order.tolist()):
+            # ndarray-stats max/min error on NaN -> unwrap_or(-inf / +inf) (lib.rs:198-199)
+            out[i] = (-np.inf, np.inf) if nan[k] else (float(mx[k]), float(mn[k]))
         return out
 
     def render(self, group=None, keep_db: bool = False, want_rgb: bool = True) -> List[Rendered]:
@@ -130,37 +137,31 @@ class RenderPipeline:
         lmx, lmn = shard.local_range([r[0] for r in ranges], [r[1] for r in ranges])
         lsr = max((t.sr for t in self.tracks), default=0)
         gmax, gmin, max_sr = shard.global_db_range(lmx, lmn, lsr, db_range=self.db_range, group=group)
+        up = self._up.get(max_sr)
+        if up is None:
+            up = np.array([shard.up_ratio(self.tracks[i].sr, max_sr, freq_scale_mel=False)
+                           for i in self._order.tolist()], np.float32)
+            self._up[max_sr] = up
+        check(lib.thesia_render_rgb_multi(
+            len(self.groups), self._c_specs, self._c_row0, self._c_bins, self._c_ns,
+            up.ctypes.data_as(_fp), self._nw.ctypes.data_as(C.POINTER(C.c_uint32)), self.nheight,
+            gmax, gmin, self._rgb.ptr, self._off.ctypes.data_as(_u64p)))
+        total = self._rgb_total
+        if want_rgb and self.pinned_output:
+            rgb_all = self._pinned_host(0, total)
+            check(lib.thesia_memcpy_d2h(rgb_all.ctypes.data_as(C.c_void_p), self._rgb.ptr, total))
+            rgb_all = rgb_all[:total]
+        else:
+            rgb_all = self._rgb.read(np.uint8, total) if want_rgb else None
         out: List[Optional[Rendered]] = [None] * len(self.tracks)
-        for g, (plan, _, dout, b) in enumerate(self.groups):
-            idx = [i for i in range(len(self.tracks)) if self.where[i][0] == g]
-            n = len(idx)
-            up = np.array([shard.up_ratio(self.tracks[i].sr, max_sr, freq_scale_mel=False) for i in idx],
-                          np.float32)
-            nw = np.array([self._geo[i] for i in idx], np.uint32)
-            sizes = nw.astype(np.uint64) * self.nheight * 3
-            off = np.concatenate([[0], np.cumsum(sizes)[:-1]]).astype(np.uint64)
-            total = int(sizes.sum())
-            if total > self._rgb.nbytes:
-                self._rgb.close()
-                self._rgb = engine.DeviceBuffer(total)
-            row0 = np.ascontiguousarray(b.frame0, np.uint64)
-            check(lib.thesia_render_rgb_batch_device(
-                dout.ptr, row0.ctypes.data_as(_u64p), plan.row_bins, n, up.ctypes.data_as(_fp),
-                nw.ctypes.data_as(C.POINTER(C.c_uint32)), self.nheight, gmax, gmin, self._rgb.ptr,
-                off.ctypes.data_as(_u64p)))
-            if want_rgb and self.pinned_output:
-                rgb_all = self._pinned_host(g, total)
-                check(lib.thesia_memcpy_d2h(rgb_all.ctypes.data_as(C.c_void_p), self._rgb.ptr, total))
-                rgb_all = rgb_all[:total]
-            else:
-                rgb_all = self._rgb.read(np.uint8, total) if want_rgb else None
-            for k, i in enumerate(idx):
-                img = rgb_all[int(off[k]):int(off[k]) + int(sizes[k])] if want_rgb else None
-                db = None
-                if keep_db:
-                    _, row_el, T, bins = self.where[i]
-                    db = dout.read(np.float32, T * bins, row_el).reshape(T, bins)
-                out[i] = Rendered(db, img, int(nw[k]), *ranges[i])
+        for k, i in enumerate(self._order.tolist()):
+            o, sz = int(self._off[k]), int(self._sizes[k])
+            img = rgb_all[o:o + sz] if want_rgb else None
+            db = None
+            if keep_db:
+                g, row_el, T, bins = self.where[i]
+                db = self.groups[g][2].read(np.float32, T * bins, row_el).reshape(T, bins)
+            out[i] = Rendered(db, img, self._geo[i], *ranges[i])
         return out
 
     def display_bytes(self) -> dict:

@@ -94,14 +94,15 @@ def test_c5_mixed_rate_render_pipeline():
         assert r.rgb.tobytes() == img.tobytes(), (t.sr, t.n_fft)  # display path bit-exact
 
 
-@pytest.mark.parametrize("per_track", [False, True])
-@pytest.mark.parametrize("px_per_sec", [73.0, 30.0, 9.0])  # 30: 17-64 taps (LDS weights); 9: > 64 (direct)
-@pytest.mark.parametrize("nheight", [90, 400])  # 400: taller images (H->nheight downsampling ratio ~2.5)
-def test_render_batch_ragged_groups(per_track, px_per_sec, nheight):
-    """Several tracks of different lengths per geometry group: the batched render (one launch
-    per stage for the whole group, blockIdx.z = track) and the per-track launches produce the
-    oracle's bytes for every image (ragged T, nwidth and workspace offsets)."""
-    engine.set_render_path(1 if per_track else 0)
+@pytest.mark.parametrize("path", [0, 1, 2])  # fused / per-track / three-stage batched
+@pytest.mark.parametrize("px_per_sec", [73.0, 30.0, 9.0, 2.0])  # 30: 17-64 taps; 9, 2: wider spans
+@pytest.mark.parametrize("nheight", [90, 400, 600])  # 400, 600: H -> nheight downsampling ~2.5, taller
+def test_render_batch_ragged_groups(path, px_per_sec, nheight):
+    """Several tracks of different lengths per geometry group: the batched renders (one launch
+    per stage for the whole group: fused grey + vertical with a transposed intermediate, or the
+    three-stage one) and the per-track launches produce the oracle's bytes for every image
+    (ragged T, nwidth and workspace offsets; staged and direct horizontal spans)."""
+    engine.set_render_path(path)
     try:
         _ragged(px_per_sec, nheight)
     finally:
