@@ -33,6 +33,9 @@
 #ifndef THESIA_RYH
 #define THESIA_RYH 16  // horizontal pass: row blocks per image
 #endif
+#ifndef THESIA_HKT_MAX
+#define THESIA_HKT_MAX 48  // horizontal pass: most taps held in registers
+#endif
 #ifndef THESIA_H_2ROW
 #define THESIA_H_2ROW 1  // horizontal pass: two rows per block step
 #endif
@@ -135,8 +138,9 @@ __device__ __forceinline__ void mm_acc(float v, float& mx, float& mn, int& nan) 
 }
 __global__ void __launch_bounds__(256) minmax_seg_kernel(const float* x, const uint64_t* seg0, int nper,
                                                          float* partial, int* nan_flag) {
+    // segment i: elements [seg0[2i], seg0[2i+1]) of x
     const int seg = blockIdx.y;
-    const uint64_t beg = seg0[seg], end = seg0[seg + 1];
+    const uint64_t beg = seg0[2 * seg], end = seg0[2 * seg + 1];
     float mx0 = -INFINITY, mn0 = INFINITY, mx1 = -INFINITY, mn1 = INFINITY;
     int nan = 0;
     const uint64_t n = end - beg;
@@ -397,14 +401,15 @@ __device__ __forceinline__ void colormap_px(float t, const uint8_t* cmap, uint8_
 // bytes are assembled in LDS and leave as aligned 32-bit words (3-byte pixels stored lane by
 // lane are byte stores at stride 3). A block whose taps do not fit takes the direct path.
 constexpr int kHTaps = 16;
+template <int KT>
 __global__ void __launch_bounds__(256) resize_h_rgb_batch_kernel(uint32_t nh, const RenderDesc* d,
                                                                  const float* tmp,
                                                                  const uint8_t* cmap, uint8_t* rgb,
                                                                  int ntap, int span_cap, int abl) {
     extern __shared__ __attribute__((aligned(16))) float hsm[];
-    float* rin = hsm;                                       // span_cap + kHTaps floats
-    float* wl = hsm + span_cap + kHTaps;                    // ntap x 256 (when ntap > kHTaps)
-    uint8_t* seg = reinterpret_cast<uint8_t*>(wl + (ntap > kHTaps ? ntap * 256 : 0));
+    float* rin = hsm;                                       // span_cap + KT floats
+    float* wl = hsm + span_cap + KT;                    // ntap x 256 (when ntap > KT)
+    uint8_t* seg = reinterpret_cast<uint8_t*>(wl + (ntap > KT ? ntap * 256 : 0));
     uint8_t* cm = seg + 256 * 3;
     const RenderDesc r = d[blockIdx.z];
     const uint32_t ox0 = blockIdx.x * 256;
@@ -414,7 +419,7 @@ __global__ void __launch_bounds__(256) resize_h_rgb_batch_kernel(uint32_t nh, co
     const uint32_t ox = ox0 + tid;
     const bool act = ox < r.nw;
     int32_t l = 0, n = 0;
-    float w[kHTaps];
+    float w[KT];
     const float* wr = r.hw;
     if (act) {
         l = r.hl[ox];
@@ -422,21 +427,21 @@ __global__ void __launch_bounds__(256) resize_h_rgb_batch_kernel(uint32_t nh, co
         wr = r.hw + r.ho[ox];
     }
 #pragma unroll
-    for (int i = 0; i < kHTaps; ++i) w[i] = (i < n && n <= kHTaps) ? wr[i] : 0.0f;
-    const bool wide = n > kHTaps && n <= ntap && ntap > kHTaps;
+    for (int i = 0; i < KT; ++i) w[i] = (i < n && n <= KT) ? wr[i] : 0.0f;
+    const bool wide = n > KT && n <= ntap && ntap > KT;
     if (wide)
         for (int i = 0; i < n; ++i) wl[i * 256 + tid] = wr[i];
-    // + kHTaps zeros after the span: the register sum runs all kHTaps terms branch-free, the
+    // + KT zeros after the span: the register sum runs all KT terms branch-free, the
     // terms past a column's count being (+0 weight) x (finite value) = +-0, which leave the
     // sum's bits unchanged (t is never -0: it starts at +0 and x + -x rounds to +0)
-    for (int k = tid; k < span_cap + kHTaps; k += 256) rin[k] = 0.0f;
+    for (int k = tid; k < span_cap + KT; k += 256) rin[k] = 0.0f;
     const uint32_t npx = r.nw - ox0 < 256u ? r.nw - ox0 : 256u;
     const uint32_t nb = 3 * npx;
     const int32_t lb = r.hl[ox0];
     const uint32_t last = ox0 + npx - 1;
     int32_t span = r.hl[last] + r.hc[last] - lb;  // supports are monotone in ox
     span = span < 0 ? 0 : (span > span_cap ? span_cap : span);
-    const bool fits = !act || (l >= lb && l + n <= lb + span && (n <= kHTaps || wide));
+    const bool fits = !act || (l >= lb && l + n <= lb + span && (n <= KT || wide));
     const bool staged = __syncthreads_and(fits) != 0;
     // the next row's span is loaded into registers while this row is summed (one HBM latency
     // per row otherwise: the pass was latency-bound), when it fits kHPf floats per thread
@@ -478,8 +483,8 @@ __global__ void __launch_bounds__(256) resize_h_rgb_batch_kernel(uint32_t nh, co
         // two rows per step (y and y + G): two independent sum chains per column over the
         // same weights, both rows' spans prefetched a step ahead
         float* rin1 = reinterpret_cast<float*>(cm + 32);
-        uint8_t* seg1 = reinterpret_cast<uint8_t*>(rin1 + span_cap + kHTaps);
-        for (int k = tid; k < span_cap + kHTaps; k += 256) rin1[k] = 0.0f;
+        uint8_t* seg1 = reinterpret_cast<uint8_t*>(rin1 + span_cap + KT);
+        for (int k = tid; k < span_cap + KT; k += 256) rin1[k] = 0.0f;
         const uint32_t G = gridDim.y;
         float nx1[kHPf];
         auto load_row1 = [&](uint32_t yy) {
@@ -508,9 +513,9 @@ __global__ void __launch_bounds__(256) resize_h_rgb_batch_kernel(uint32_t nh, co
             if (act) {
                 float t0 = 0.0f, t1 = 0.0f;
                 const int base = l - lb;
-                if (n <= kHTaps) {
+                if (n <= KT) {
 #pragma unroll
-                    for (int i = 0; i < kHTaps; ++i) {
+                    for (int i = 0; i < KT; ++i) {
                         t0 += rin[base + i] * w[i];
                         t1 += rin1[base + i] * w[i];
                     }
@@ -552,9 +557,9 @@ __global__ void __launch_bounds__(256) resize_h_rgb_batch_kernel(uint32_t nh, co
             float t = 0.0f;
             if (staged) {
                 const int base = l - lb;
-                if (n <= kHTaps) {
+                if (n <= KT) {
 #pragma unroll
-                    for (int i = 0; i < kHTaps; ++i) t += rin[base + i] * w[i];
+                    for (int i = 0; i < KT; ++i) t += rin[base + i] * w[i];
                 } else {
                     for (int i = 0; i < n; ++i) t += rin[base + i] * wl[i * 256 + tid];
                 }
@@ -604,7 +609,7 @@ int launch_render_batch(const float* spec, uint32_t bins, float max, float min,
     auto lds = [&]() { return (2 * (span + kHTaps) + taps * 256) * 4 + 2 * 256 * 3 + 32; };
     if (lds() > 65536) taps = 0;
     if (lds() > 65536) span = 4096;
-    hipLaunchKernelGGL(resize_h_rgb_batch_kernel, g3, dim3(256), lds(), s, nh, d_desc, tmp, cmap, rgb,
+    hipLaunchKernelGGL(resize_h_rgb_batch_kernel<kHTaps>, g3, dim3(256), lds(), s, nh, d_desc, tmp, cmap, rgb,
                        taps, span, abl);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
@@ -789,14 +794,19 @@ int launch_render_batch2(const float* spec, uint32_t bins, float max, float min,
     // K5h + K6: the three-stage path's horizontal pass (same intermediate layout [nh][T])
     const uint32_t ry_h = THESIA_RYH;
     dim3 g3((nw_max + 255) / 256, nh < ry_h ? nh : ry_h, n);
-    int taps = h_taps > kHTaps ? h_taps : 0;
+    // register weights up to THESIA_HKT_MAX taps (a downsampling group's 20-48 taps as an LDS
+    // weight table took 44 KiB per block: two blocks per CU); more taps: the LDS table
+    const int kt = h_taps <= 16 ? 16 : h_taps <= 32 && THESIA_HKT_MAX >= 32 ? 32
+                 : h_taps <= 48 && THESIA_HKT_MAX >= 48 ? 48 : 16;
+    int taps = h_taps > kt ? h_taps : 0;
     int span = h_span;
     // span + zeros, wide weights, RGB segment, colormap; then the second row's span + segment
-    auto lds = [&]() { return (2 * (span + kHTaps) + taps * 256) * 4 + 2 * 256 * 3 + 32; };
+    auto lds = [&]() { return (2 * (span + kt) + taps * 256) * 4 + 2 * 256 * 3 + 32; };
     if (lds() > 65536) taps = 0;
     if (lds() > 65536) span = 4096;
-    hipLaunchKernelGGL(resize_h_rgb_batch_kernel, g3, dim3(256), lds(), s, nh, d_desc, tmp, cmap, rgb,
-                       taps, span, 0);
+    auto kern = kt == 48 ? resize_h_rgb_batch_kernel<48>
+              : kt == 32 ? resize_h_rgb_batch_kernel<32> : resize_h_rgb_batch_kernel<16>;
+    hipLaunchKernelGGL(kern, g3, dim3(256), lds(), s, nh, d_desc, tmp, cmap, rgb, taps, span, 0);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 

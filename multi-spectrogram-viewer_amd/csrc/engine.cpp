@@ -695,25 +695,32 @@ int grey_to_rgb_device(const float* d_grey, uint32_t w, uint32_t h, uint32_t nw,
 int minmax_segments_multi(size_t n_groups, const float* const* d_x, const uint64_t* const* row0,
                           const size_t* bins, const size_t* ns, float* mx, float* mn, int* nan,
                           hipStream_t s) {
-    // every group's segment table in one upload, the launches back to back, one readback
-    std::vector<uint64_t> seg;
-    std::vector<int> nper(n_groups);
-    std::vector<size_t> seg0(n_groups), part0(n_groups), trk0(n_groups);
-    size_t ntr = 0, npart = 0;
+    // one launch over every group's tracks: segment bounds are element offsets from the lowest
+    // group buffer (one flat device address space), one table upload, one readback
+    const float* base = nullptr;
+    size_t ntr = 0;
+    uint64_t tot = 0;
     for (size_t k = 0; k < n_groups; ++k) {
-        const size_t n = ns[k];
-        seg0[k] = seg.size();
-        part0[k] = npart;
-        trk0[k] = ntr;
-        if (n == 0) continue;
-        // blocks per track: enough to fill the device at the group's total size
-        const uint64_t tot = (row0[k][n] - row0[k][0]) * bins[k];
-        nper[k] = (int)std::min<uint64_t>(64, std::max<uint64_t>(1, (tot / n) / (256 * 4 * 8)));
-        for (size_t i = 0; i <= n; ++i) seg.push_back(row0[k][i] * bins[k]);
-        npart += n * nper[k];
-        ntr += n;
+        if (ns[k] == 0) continue;
+        if (!base || d_x[k] < base) base = d_x[k];
+        ntr += ns[k];
+        tot += (row0[k][ns[k]] - row0[k][0]) * bins[k];
     }
     if (ntr == 0) return THESIA_OK;
+    if (ntr > 65535) return set_error(THESIA_ERR_INVALID_ARG, "more than 65535 tracks in one range call");
+    // [lo, hi) per track: each track closed by its own end, so no segment spans the gap
+    // between two groups' buffers
+    std::vector<uint64_t> lo(ntr), hi(ntr);
+    size_t t = 0;
+    for (size_t k = 0; k < n_groups; ++k) {
+        const uint64_t off = ns[k] ? (uint64_t)(d_x[k] - base) : 0;
+        for (size_t i = 0; i < ns[k]; ++i, ++t) {
+            lo[t] = off + row0[k][i] * bins[k];
+            hi[t] = off + row0[k][i + 1] * bins[k];
+        }
+    }
+    // blocks per track: enough to fill the device at the call's total size
+    const int nper = (int)std::min<uint64_t>(64, std::max<uint64_t>(1, (tot / ntr) / (256 * 4 * 8)));
     // grow-only per-device workspace (a hipMalloc per call cost more than the reduction)
     struct Ws { DevBuf seg, part, flag; };
     static std::mutex ws_mu;
@@ -727,35 +734,34 @@ int minmax_segments_multi(size_t n_groups, const float* const* d_x, const uint64
         b.release();
         return b.alloc(bytes + bytes / 8);
     };
-    int rc = grow(ws.seg, seg.size() * 8);
-    if (!rc) rc = grow(ws.part, npart * 2 * sizeof(float));
+    std::vector<uint64_t> bounds(2 * ntr);
+    for (size_t i = 0; i < ntr; ++i) {
+        bounds[2 * i] = lo[i];
+        bounds[2 * i + 1] = hi[i];
+    }
+    int rc = grow(ws.seg, bounds.size() * 8);
+    if (!rc) rc = grow(ws.part, ntr * nper * 2 * sizeof(float));
     if (!rc) rc = grow(ws.flag, ntr * sizeof(int));
     if (rc) return rc;
-    THESIA_HIP(hipMemcpyAsync(ws.seg.p, seg.data(), seg.size() * 8, hipMemcpyHostToDevice, s));
+    THESIA_HIP(hipMemcpyAsync(ws.seg.p, bounds.data(), bounds.size() * 8, hipMemcpyHostToDevice, s));
     THESIA_HIP(hipMemsetAsync(ws.flag.p, 0, ntr * sizeof(int), s));
-    for (size_t k = 0; k < n_groups; ++k) {
-        if (ns[k] == 0) continue;
-        if (launch_minmax_seg(d_x[k], ws.seg.as<uint64_t>() + seg0[k], (int)ns[k], nper[k],
-                              ws.part.as<float>() + 2 * part0[k], ws.flag.as<int>() + trk0[k], s))
-            return set_error(THESIA_ERR_DEVICE, "minmax_seg launch failed");
-    }
-    std::vector<float> h(npart * 2);
+    if (launch_minmax_seg(base, ws.seg.as<uint64_t>(), (int)ntr, nper, ws.part.as<float>(), ws.flag.as<int>(), s))
+        return set_error(THESIA_ERR_DEVICE, "minmax_seg launch failed");
+    std::vector<float> h(ntr * nper * 2);
     std::vector<int> hf(ntr);
     THESIA_HIP(hipMemcpyAsync(h.data(), ws.part.p, h.size() * sizeof(float), hipMemcpyDeviceToHost, s));
     THESIA_HIP(hipMemcpyAsync(hf.data(), ws.flag.p, ntr * sizeof(int), hipMemcpyDeviceToHost, s));
     THESIA_HIP(hipStreamSynchronize(s));
-    for (size_t k = 0; k < n_groups; ++k)
-        for (size_t i = 0; i < ns[k]; ++i) {
-            float a = -INFINITY, b = INFINITY;  // empty track: ndarray-stats EmptyInput -> -inf / +inf
-            const float* p = h.data() + 2 * (part0[k] + i * nper[k]);
-            for (int q = 0; q < nper[k]; ++q) {
-                a = fmaxf(a, p[2 * q]);
-                b = fminf(b, p[2 * q + 1]);
-            }
-            mx[trk0[k] + i] = a;
-            mn[trk0[k] + i] = b;
-            nan[trk0[k] + i] = hf[trk0[k] + i];
+    for (size_t i = 0; i < ntr; ++i) {
+        float a = -INFINITY, b = INFINITY;  // empty track: ndarray-stats EmptyInput -> -inf / +inf
+        for (int q = 0; q < nper; ++q) {
+            a = fmaxf(a, h[(i * nper + q) * 2]);
+            b = fminf(b, h[(i * nper + q) * 2 + 1]);
         }
+        mx[i] = a;
+        mn[i] = b;
+        nan[i] = hf[i];
+    }
     return THESIA_OK;
 }
 
@@ -877,37 +883,66 @@ int render_rgb_fused(size_t n_groups, const float* const* d_specs, const uint64_
     int rc = 0;
     const uint8_t* cmap_ptr = colormap_device(&rc);
     if (rc) return rc;
-    // host planning of every group first, then one table upload and the launches back to
-    // back on the stream (the groups reuse one intermediate: stream order makes that safe)
-    std::vector<RenderDesc> desc;
-    std::vector<FusedGroup> groups(n_groups);
-    uint64_t tmp_max = 1;
-    size_t t0 = 0;
+    // the plan (descriptor table, bands, tap tables) depends only on the call's geometry: a
+    // call repeating the previous one's geometry (every step of a render loop) reuses the
+    // table already on the device and skips the planning and the upload
+    std::vector<uint8_t> key;
+    auto put = [&key](const void* p, size_t bytes) {
+        const uint8_t* b = static_cast<const uint8_t*>(p);
+        key.insert(key.end(), b, b + bytes);
+    };
+    size_t ntr = 0;
+    put(&n_groups, sizeof n_groups);
+    put(&nheight, sizeof nheight);
+    put(&d_rgb, sizeof d_rgb);
     for (size_t k = 0; k < n_groups; ++k) {
-        rc = plan_fused_group(d_specs[k], row0s[k], bins[k], ns[k], up_ratio + t0, nwidth + t0, nheight,
-                              rgb_off + t0, desc, groups[k]);
-        if (rc) return rc;
-        tmp_max = std::max<uint64_t>(tmp_max, groups[k].tmp_tot);
-        t0 += ns[k];
+        put(&d_specs[k], sizeof(void*));
+        put(&bins[k], sizeof(size_t));
+        put(&ns[k], sizeof(size_t));
+        if (ns[k]) put(row0s[k], (ns[k] + 1) * sizeof(uint64_t));
+        ntr += ns[k];
     }
-    if (desc.empty()) return THESIA_OK;
-    struct Ws { DevBuf tmp, desc; };
+    put(up_ratio, ntr * sizeof(float));
+    put(nwidth, ntr * sizeof(uint32_t));
+    put(rgb_off, ntr * sizeof(uint64_t));
+    struct Ws {
+        DevBuf tmp, desc;
+        std::vector<uint8_t> key;  // geometry of the table in `desc`
+        std::vector<FusedGroup> groups;
+    };
     static std::mutex ws_mu;
     static auto& ws_map = *new std::map<int, Ws>();  // leaked, see dev_taps
     int dev = 0;
     (void)hipGetDevice(&dev);
     std::lock_guard<std::mutex> lk(ws_mu);
     Ws& ws = ws_map[dev];
-    auto grow = [](DevBuf& b, size_t bytes) {
-        if (b.bytes >= bytes && b.p) return 0;
-        b.release();
-        return b.alloc(bytes + bytes / 8);
-    };
-    rc = grow(ws.tmp, tmp_max * sizeof(float));
-    if (!rc) rc = grow(ws.desc, desc.size() * sizeof(RenderDesc));
-    if (rc) return rc;
-    THESIA_HIP(hipMemcpyAsync(ws.desc.p, desc.data(), desc.size() * sizeof(RenderDesc),
-                              hipMemcpyHostToDevice, s));
+    if (ws.key != key) {
+        ws.key.clear();
+        std::vector<RenderDesc> desc;
+        std::vector<FusedGroup> groups(n_groups);
+        uint64_t tmp_max = 1;
+        size_t t0 = 0;
+        for (size_t k = 0; k < n_groups; ++k) {
+            rc = plan_fused_group(d_specs[k], row0s[k], bins[k], ns[k], up_ratio + t0, nwidth + t0, nheight,
+                                  rgb_off + t0, desc, groups[k]);
+            if (rc) return rc;
+            tmp_max = std::max<uint64_t>(tmp_max, groups[k].tmp_tot);
+            t0 += ns[k];
+        }
+        auto grow = [](DevBuf& b, size_t bytes) {
+            if (b.bytes >= bytes && b.p) return 0;
+            b.release();
+            return b.alloc(bytes + bytes / 8);
+        };
+        rc = grow(ws.tmp, tmp_max * sizeof(float));
+        if (!rc) rc = grow(ws.desc, std::max<size_t>(desc.size(), 1) * sizeof(RenderDesc));
+        if (rc) return rc;
+        if (!desc.empty())
+            THESIA_HIP(hipMemcpy(ws.desc.p, desc.data(), desc.size() * sizeof(RenderDesc), hipMemcpyHostToDevice));
+        ws.groups = std::move(groups);
+        ws.key = std::move(key);
+    }
+    const std::vector<FusedGroup>& groups = ws.groups;
     for (const FusedGroup& g : groups)
         for (size_t b = 0; b < g.ndesc; b += 65535) {  // grid.z limit
             const uint32_t nb = (uint32_t)std::min<size_t>(65535, g.ndesc - b);
@@ -916,7 +951,6 @@ int render_rgb_fused(size_t n_groups, const float* const* d_specs, const uint64_
                                      g.v_rows, g.v_wts, ws.tmp.as<float>(), cmap_ptr, d_rgb, s))
                 return set_error(THESIA_ERR_DEVICE, "render batch launch failed");
         }
-    // the table upload reads `desc` (pageable host memory) until it has run
     THESIA_HIP(hipStreamSynchronize(s));
     return THESIA_OK;
 }

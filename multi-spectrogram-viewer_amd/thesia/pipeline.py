@@ -105,6 +105,7 @@ class RenderPipeline:
         self._rgb_total = int(self._sizes.sum())
         self._rgb = engine.DeviceBuffer(max(self._rgb_total, 1))
         self._up = {}  # max_sr -> up_ratio per track (call order)
+        self._max_sr = max((t.sr for t in self.tracks), default=0)
 
     def run_spectrograms(self) -> None:
         """One kernel launch per geometry group (asynchronous)."""
@@ -115,9 +116,10 @@ class RenderPipeline:
         g, row0, T, bins = self.where[i]
         return C.c_void_p(self.groups[g][2].ptr.value + row0 * 4), T, bins
 
-    def ranges(self):
-        """Per-track (max, min) dB (lib.rs:194-207): one segmented reduction per group, all
-        groups in one library call (one synchronisation)."""
+    def _range_arrays(self):
+        """(max, min) dB per track in call order (group order), NaN-holding tracks as -inf /
+        +inf (ndarray-stats max/min error on NaN -> unwrap_or, lib.rs:198-199): one segmented
+        reduction over every group in one library call (one synchronisation)."""
         n = len(self._order)
         mx = np.empty(n, np.float32)
         mn = np.empty(n, np.float32)
@@ -125,18 +127,22 @@ class RenderPipeline:
         check(lib.thesia_minmax_segments_multi(len(self.groups), self._c_specs, self._c_row0, self._c_bins,
                                                self._c_ns, mx.ctypes.data_as(_fp), mn.ctypes.data_as(_fp),
                                                nan.ctypes.data_as(C.POINTER(C.c_int))))
+        bad = nan != 0
+        return np.where(bad, -np.inf, mx.astype(np.float64)), np.where(bad, np.inf, mn.astype(np.float64))
+
+    def ranges(self):
+        """Per-track (max, min) dB (lib.rs:194-207), indexed like self.tracks."""
+        mx, mn = self._range_arrays()
         out = [None] * len(self.tracks)
         for k, i in enumerate(self._order.tolist()):
-            # ndarray-stats max/min error on NaN -> unwrap_or(-inf / +inf) (lib.rs:198-199)
-            out[i] = (-np.inf, np.inf) if nan[k] else (float(mx[k]), float(mn[k]))
+            out[i] = (float(mx[k]), float(mn[k]))
         return out
 
     def render(self, group=None, keep_db: bool = False, want_rgb: bool = True) -> List[Rendered]:
         engine.synchronize()
-        ranges = self.ranges()
-        lmx, lmn = shard.local_range([r[0] for r in ranges], [r[1] for r in ranges])
-        lsr = max((t.sr for t in self.tracks), default=0)
-        gmax, gmin, max_sr = shard.global_db_range(lmx, lmn, lsr, db_range=self.db_range, group=group)
+        mx, mn = self._range_arrays()
+        lmx, lmn = shard.local_range(mx.tolist(), mn.tolist())
+        gmax, gmin, max_sr = shard.global_db_range(lmx, lmn, self._max_sr, db_range=self.db_range, group=group)
         up = self._up.get(max_sr)
         if up is None:
             up = np.array([shard.up_ratio(self.tracks[i].sr, max_sr, freq_scale_mel=False)
@@ -161,7 +167,7 @@ class RenderPipeline:
             if keep_db:
                 g, row_el, T, bins = self.where[i]
                 db = self.groups[g][2].read(np.float32, T * bins, row_el).reshape(T, bins)
-            out[i] = Rendered(db, img, self._geo[i], *ranges[i])
+            out[i] = Rendered(db, img, self._geo[i], float(mx[k]), float(mn[k]))
         return out
 
     def display_bytes(self) -> dict:
