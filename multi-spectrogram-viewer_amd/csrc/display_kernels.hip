@@ -18,12 +18,6 @@
 #include <cstdint>
 
 // compile-time choices A/B'd with scripts/build_variant.sh (defaults = the product)
-#ifndef THESIA_V_ILP
-#define THESIA_V_ILP 1  // grey_vert: four output rows per wave step
-#endif
-#ifndef THESIA_V_FLAT
-#define THESIA_V_FLAT 1  // grey_vert: flattened (frame, row) tile staging
-#endif
 #ifndef THESIA_V_ABL
 #define THESIA_V_ABL 0
 #endif
@@ -632,32 +626,38 @@ __device__ __forceinline__ float grey_of(float db, float max, float min) {  // g
 }
 __global__ void __launch_bounds__(256) grey_vert_kernel(const float* spec, uint32_t bins, float max,
                                                         float min, uint32_t nh, const RenderDesc* d,
-                                                        float* tmp, int tile_cap, int wcap, uint32_t band) {
+                                                        float* tmp, int tile_cap, int kv, uint32_t band) {
     extern __shared__ __attribute__((aligned(16))) float vsm[];
     const RenderDesc r = d[blockIdx.z];
     const uint32_t x0 = blockIdx.x * 64, ob = blockIdx.y * band;
     const uint32_t oy1 = ob + band < nh ? ob + band : nh;
     const uint32_t oy0 = ob > r.oz ? ob : r.oz;  // rows below oz: +0, never formed (RenderDesc)
     if (x0 >= r.T || oy0 >= oy1) return;  // block-uniform
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    // grey rows [ya, yb) reached by the band's taps (supports are monotone in oy)
-    const int32_t ya = r.vl[oy0], yb = r.vl[oy1 - 1] + r.vc[oy1 - 1];
-    const int32_t rows = yb - ya;
-    const int32_t w0 = r.vo[oy0], wn = r.vo[oy1 - 1] + r.vc[oy1 - 1] - w0;
-    constexpr int TS = 65;                // tile row stride: the staging writes walk rows
-    int4* meta = reinterpret_cast<int4*>(vsm);  // per band row {tile row, taps, weight offset}
-    float* tile = vsm + 4 * (size_t)band;       // [rows][TS]
-    float* wl = tile + (size_t)tile_cap * TS;
-    const bool staged = rows <= tile_cap && wn <= wcap;
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    // grey rows [ya, ya + rows) reached by the band's taps, each row's taps padded to kv (a
+    // multiple of 4) with zero weights: supports are monotone in oy, so the last row's padded
+    // support ends the tile. A padded term adds +-0 (zero weight x finite grey) to the sum,
+    // which leaves its bits unchanged (t starts at +0 and x + -x rounds to +0): the sum equals
+    // resize_v_px's t = 0; t += in * w over the row's own taps.
+    const int32_t ya = r.vl[oy0];
+    const int32_t rows = r.vl[oy1 - 1] - ya + kv;
+    const uint32_t nb = oy1 - oy0;
+    constexpr int TS = 65;                    // tile row stride: staging writes walk rows
+    const int mrows = ((int)band + 3) & ~3;   // meta entries, rounded for 16-byte alignment
+    int* meta = reinterpret_cast<int*>(vsm);  // per band row: its first tile row
+    float* tile = vsm + mrows;                // [tile_cap][TS]
+    float* wl = tile + ((tile_cap * TS + 3) & ~3);  // [band][kv], zero-padded per row
+    const bool staged = rows <= tile_cap;
     const uint32_t x = x0 + lane;
     const int32_t H = (int32_t)r.H, top = (int32_t)r.H - (int32_t)bins;
     const float* sp = spec + r.spec_off;
-#if THESIA_V_FLAT
     if (staged) {
         // (frame, row) pairs flattened over the block's 256 threads (f = e / rows by a
         // multiply-high, exact for e < 2^14): consecutive threads read consecutive bins of one
         // frame (coalesced) and a thread's THESIA_VDEPTH loads are in flight together; the zero
-        // fill above the track's band (y < top) and frames past T are never loaded
+        // fill above the track's band (y < top), rows past the image and frames past T are
+        // never loaded
         constexpr int D = THESIA_VDEPTH;
         const int total = 64 * rows;
         const uint32_t mrec = rows > 1 ? (uint32_t)((0x100000000ull + rows - 1) / (uint32_t)rows) : 0u;
@@ -669,82 +669,58 @@ __global__ void __launch_bounds__(256) grey_vert_kernel(const float* spec, uint3
                 const uint32_t f = rows > 1 ? __umulhi(e, mrec) : e;
                 const int32_t k = (int32_t)(e - f * (uint32_t)rows), y = ya + k;
                 v[i] = 0.0f;
-                if ((int)e < total && y >= top && x0 + f < r.T)
+                if ((int)e < total && y >= top && y < H && x0 + f < r.T)
                     v[i] = sp[(uint64_t)(x0 + f) * bins + (uint32_t)(H - 1 - y)];
             }
 #pragma unroll
             for (int i = 0; i < D; ++i) {
                 const uint32_t e = (uint32_t)(e0 + 256 * i + tid);
                 const uint32_t f = rows > 1 ? __umulhi(e, mrec) : e;
-                const int32_t k = (int32_t)(e - f * (uint32_t)rows);
-                if ((int)e < total) tile[k * TS + f] = ya + k >= top ? grey_of(v[i], max, min) : 0.0f;
+                const int32_t k = (int32_t)(e - f * (uint32_t)rows), y = ya + k;
+                if ((int)e < total) tile[k * TS + f] = (y >= top && y < H) ? grey_of(v[i], max, min) : 0.0f;
             }
         }
-        for (int32_t i = tid; i < wn; i += 256) wl[i] = r.vw[w0 + i];
-        for (uint32_t j = tid; j < oy1 - oy0; j += 256)
-            meta[j] = make_int4(r.vl[oy0 + j] - ya, r.vc[oy0 + j], r.vo[oy0 + j] - w0, 0);
-    }
-#else
-    if (staged) {
-        // grey row y of frame x is bin H-1-y: the tile's rows run down the frame's bins, so a
-        // wave reading 64 consecutive rows of one frame reads 64 consecutive bins
-        // 4 frames x up to 4 row blocks of loads in flight per wave step (a frame at a time
-        // left each wave waiting out one HBM latency per 64 rows)
-        for (int fb = wave; fb < 64; fb += 16) {
-            float v[4][4];
-#pragma unroll
-            for (int j = 0; j < 4; ++j) {
-                const uint32_t xf = x0 + fb + 4 * j;
-                const float* srow = sp + (uint64_t)(xf < r.T ? xf : r.T - 1) * bins;
-#pragma unroll
-                for (int kb = 0; kb < 4; ++kb) {
-                    const int32_t k = kb * 64 + lane, y = ya + k;
-                    v[j][kb] = 0.0f;
-                    if (k < rows && y >= top) v[j][kb] = srow[H - 1 - y];  // zero fill: no load
-                }
-            }
-#pragma unroll
-            for (int j = 0; j < 4; ++j)
-#pragma unroll
-                for (int kb = 0; kb < 4; ++kb) {
-                    const int32_t k = kb * 64 + lane, y = ya + k;
-                    if (k < rows) tile[k * TS + fb + 4 * j] = y >= top ? grey_of(v[j][kb], max, min) : 0.0f;
-                }
+        for (uint32_t e = tid; e < nb * (uint32_t)kv; e += 256) {
+            const uint32_t j = e / (uint32_t)kv, i = e - j * (uint32_t)kv;
+            const int32_t n = r.vc[oy0 + j];
+            wl[e] = (int32_t)i < n ? r.vw[r.vo[oy0 + j] + i] : 0.0f;
         }
-        for (int32_t i = tid; i < wn; i += 256) wl[i] = r.vw[w0 + i];
+        for (uint32_t j = tid; j < nb; j += 256) meta[j] = r.vl[oy0 + j] - ya;
     }
-#endif
     __syncthreads();
     if (x >= r.T) return;  // no block barrier below
     float* out = tmp + r.tmp_off + x;
     uint32_t oy = oy0 + wave;
-#if THESIA_V_ILP
     if (staged) {
-        // four output rows at a time: four independent chains (each in its own order) keep
-        // the wave issuing while one chain waits on its previous fma
+        const float4* wl4 = reinterpret_cast<const float4*>(wl);
+        const int kv4 = kv >> 2;
+        const float* col = tile + lane;
+        // four output rows per wave step: four independent chains (each in its own order); a
+        // row's first tile row and its weights are wave-uniform (LDS broadcasts), the grey
+        // values one conflict-free LDS read per tap
         for (; oy + 12 < oy1; oy += 16) {
-            int32_t l[4], n[4], wo[4];
+            int lq[4];
+            const float4* wq[4];
 #pragma unroll
             for (int q = 0; q < 4; ++q) {
-#if THESIA_V_FLAT
-                const int4 m = meta[oy - oy0 + 4 * q];  // LDS broadcast (no scalar-load wait)
-                l[q] = m.x;
-                n[q] = m.y;
-                wo[q] = m.z;
-#else
-                l[q] = r.vl[oy + 4 * q] - ya;
-                n[q] = r.vc[oy + 4 * q];
-                wo[q] = r.vo[oy + 4 * q] - w0;
-#endif
+                const uint32_t j = oy - oy0 + 4 * q;
+                lq[q] = __builtin_amdgcn_readfirstlane(meta[j]);
+                wq[q] = wl4 + j * kv4;
             }
-            const int32_t n01 = n[0] > n[1] ? n[0] : n[1], n23 = n[2] > n[3] ? n[2] : n[3];
-            const int32_t nmax = n01 > n23 ? n01 : n23;
             float t[4] = {0.0f, 0.0f, 0.0f, 0.0f};
-            for (int32_t i = 0; i < nmax; ++i) {
+#if !(THESIA_V_ABL & 2)  // ablation (timing only): no sums
+            for (int i4 = 0; i4 < kv4; ++i4) {
 #pragma unroll
-                for (int q = 0; q < 4; ++q)
-                    if (i < n[q]) t[q] += tile[(l[q] + i) * TS + lane] * wl[wo[q] + i];
+                for (int q = 0; q < 4; ++q) {
+                    const float4 w = wq[q][i4];
+                    const float* c = col + (lq[q] + 4 * i4) * TS;
+                    t[q] += c[0] * w.x;
+                    t[q] += c[TS] * w.y;
+                    t[q] += c[2 * TS] * w.z;
+                    t[q] += c[3 * TS] * w.w;
+                }
             }
+#endif
 #pragma unroll
             for (int q = 0; q < 4; ++q) {
 #if THESIA_V_ABL & 1  // ablation (timing only): no tmp stores
@@ -753,22 +729,32 @@ __global__ void __launch_bounds__(256) grey_vert_kernel(const float* spec, uint3
                     out[(uint64_t)(oy + 4 * q) * r.T] = t[q];
             }
         }
-    }
-#endif
-    for (; oy < oy1; oy += 4) {
-        const int32_t l = r.vl[oy], n = r.vc[oy];  // row-uniform: scalar loads
-        float t = 0.0f;
-        if (staged) {
-            const float* wr = wl + (r.vo[oy] - w0);
-            const float* col = tile + (l - ya) * TS + lane;
-            for (int32_t i = 0; i < n; ++i) t += col[i * TS] * wr[i];
-        } else {
-            const float* wr = r.vw + r.vo[oy];
-            const float* srow = sp + (uint64_t)x * bins;
-            for (int32_t i = 0; i < n; ++i) {
-                const int32_t y = l + i;
-                t += (y >= top ? grey_of(srow[H - 1 - y], max, min) : 0.0f) * wr[i];
+        for (; oy < oy1; oy += 4) {
+            const uint32_t j = oy - oy0;
+            const int l = __builtin_amdgcn_readfirstlane(meta[j]);
+            const float4* w4 = wl4 + j * kv4;
+            float t = 0.0f;
+            for (int i4 = 0; i4 < kv4; ++i4) {
+                const float4 w = w4[i4];
+                const float* c = col + (l + 4 * i4) * TS;
+                t += c[0] * w.x;
+                t += c[TS] * w.y;
+                t += c[2 * TS] * w.z;
+                t += c[3 * TS] * w.w;
             }
+            out[(uint64_t)oy * r.T] = t;
+        }
+        return;
+    }
+    // direct path (a band whose tile does not fit): taps straight from HBM, scalar weights
+    for (; oy < oy1; oy += 4) {
+        const int32_t l = r.vl[oy], n = r.vc[oy];
+        const float* wr = r.vw + r.vo[oy];
+        const float* srow = sp + (uint64_t)x * bins;
+        float t = 0.0f;
+        for (int32_t i = 0; i < n; ++i) {
+            const int32_t y = l + i;
+            t += (y >= top ? grey_of(srow[H - 1 - y], max, min) : 0.0f) * wr[i];
         }
         out[(uint64_t)oy * r.T] = t;
     }
@@ -777,20 +763,23 @@ __global__ void __launch_bounds__(256) grey_vert_kernel(const float* spec, uint3
 int launch_render_batch2(const float* spec, uint32_t bins, float max, float min,
                          const RenderDesc* d_desc, uint32_t n, uint32_t T_max, uint32_t H_max,
                          uint32_t nw_max, uint32_t nh, int h_taps, int h_span, uint32_t v_band,
-                         int v_rows, int v_wts, float* tmp, const uint8_t* cmap, uint8_t* rgb,
+                         int v_rows, int v_kv, float* tmp, const uint8_t* cmap, uint8_t* rgb,
                          hipStream_t s) {
     if (n == 0 || nh == 0 || v_band == 0) return 0;
     if (n > 65535) return -2;
     (void)H_max;
-    // K4+K5v: the band's grey tile and weights in LDS (bands that do not fit read HBM directly)
-    const int tile_cap = v_rows < 256 ? v_rows : 256, wcap = v_wts < 4096 ? v_wts : 4096;
-    const int lds1 = (tile_cap * 65 + wcap + 4 * (int)v_band) * 4;
+    // K4+K5v: the band's grey tile, meta and zero-padded weights in LDS (a band whose tile does
+    // not fit reads HBM directly)
+    const int kv = (v_kv + 3) & ~3;
+    const int tile_cap = v_rows < 256 ? v_rows : 256;
+    const int lds1 = ((((int)v_band + 3) & ~3) + ((tile_cap * 65 + 3) & ~3) + (int)v_band * kv) * 4;
+    if (lds1 > 163840) return -2;
     if (hipFuncSetAttribute(reinterpret_cast<const void*>(grey_vert_kernel),
                             hipFuncAttributeMaxDynamicSharedMemorySize, lds1) != hipSuccess)
         return -1;
     dim3 g1((T_max + 63) / 64, (nh + v_band - 1) / v_band, n);
     hipLaunchKernelGGL(grey_vert_kernel, g1, dim3(256), lds1, s, spec, bins, max, min, nh, d_desc, tmp,
-                       tile_cap, wcap, v_band);
+                       tile_cap, kv, v_band);
     // K5h + K6: the three-stage path's horizontal pass (same intermediate layout [nh][T])
     const uint32_t ry_h = THESIA_RYH;
     dim3 g3((nw_max + 255) / 256, nh < ry_h ? nh : ry_h, n);

@@ -771,7 +771,7 @@ int minmax_segments_device(const float* d_x, const uint64_t* row0, size_t bins, 
 }
 
 #ifndef THESIA_VBAND
-#define THESIA_VBAND 512  // widest vertical band tried
+#define THESIA_VBAND 64  // widest vertical band tried (64 beat 128-512 on C5: more blocks)
 #endif
 #ifndef THESIA_VROWS
 #define THESIA_VROWS 128  // grey rows per vertical tile (<= 256; A/B via scripts/build_variant.sh)
@@ -802,7 +802,7 @@ struct FusedGroup {
     size_t desc0 = 0, ndesc = 0;  // its RenderDesc range in the call's table
     uint64_t tmp_tot = 0;         // intermediate floats ([nheight][T] per track)
     uint32_t T_max = 0, H_max = 0, nw_max = 0, v_band = 1;
-    int h_taps = 0, h_span = 0, v_rows = 1, v_wts = 1;
+    int h_taps = 0, h_span = 0, v_rows = 1, v_kv = 4;
 };
 
 // Host planning of one group: a RenderDesc per non-empty track (appended to `desc`), the
@@ -851,25 +851,24 @@ int plan_fused_group(const float* d_spec, const uint64_t* row0, size_t bins, siz
         desc.push_back(r);
     }
     g.ndesc = desc.size() - g.desc0;
-    auto band_need = [&](uint32_t band, int* rows_out, int* wts_out) {
-        int rows = 1, wts = 1;
+    // taps per row padded to kv (a multiple of 4, zero weights): the tile holds the band's
+    // supports plus kv rows, the weight table band x kv floats
+    int kv = 4;
+    for (const auto& [vt, oz] : vts) kv = std::max(kv, (vt->max_taps + 3) & ~3);
+    g.v_kv = kv;
+    auto band_need = [&](uint32_t band, int* rows_out) {
+        int rows = 1;
         for (const auto& [vt, oz] : vts)
             for (uint32_t ob = 0; ob < nheight; ob += band) {
                 const uint32_t o0 = std::max(ob, oz), o1 = std::min(nheight, ob + band) - 1;
                 if (o0 > o1) continue;
-                rows = std::max(rows, vt->h_left[o1] + vt->h_count[o1] - vt->h_left[o0]);
-                int wn = 0;
-                for (uint32_t o = o0; o <= o1; ++o) wn += vt->h_count[o];
-                wts = std::max(wts, wn);
+                rows = std::max(rows, vt->h_left[o1] - vt->h_left[o0] + kv);
             }
         *rows_out = rows;
-        *wts_out = wts;
-        return rows <= THESIA_VROWS && wts <= 4096;
+        return rows <= THESIA_VROWS && (int)band * kv <= 4096;
     };
-    // the widest band that fits (measured: THESIA_VROWS 128 beats 256 on C5, the smaller tile
-    // doubling the blocks resident per CU)
     g.v_band = THESIA_VBAND;
-    while (!band_need(g.v_band, &g.v_rows, &g.v_wts) && g.v_band > 1) g.v_band /= 2;
+    while (!band_need(g.v_band, &g.v_rows) && g.v_band > 1) g.v_band /= 2;
     return THESIA_OK;
 }
 
@@ -948,7 +947,7 @@ int render_rgb_fused(size_t n_groups, const float* const* d_specs, const uint64_
             const uint32_t nb = (uint32_t)std::min<size_t>(65535, g.ndesc - b);
             if (launch_render_batch2(g.spec, g.bins, max, min, ws.desc.as<RenderDesc>() + g.desc0 + b, nb,
                                      g.T_max, g.H_max, g.nw_max, nheight, g.h_taps, g.h_span, g.v_band,
-                                     g.v_rows, g.v_wts, ws.tmp.as<float>(), cmap_ptr, d_rgb, s))
+                                     g.v_rows, g.v_kv, ws.tmp.as<float>(), cmap_ptr, d_rgb, s))
                 return set_error(THESIA_ERR_DEVICE, "render batch launch failed");
         }
     THESIA_HIP(hipStreamSynchronize(s));

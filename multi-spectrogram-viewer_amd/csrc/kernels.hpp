@@ -135,12 +135,12 @@ int launch_render_batch(const float* spec, uint32_t bins, float max, float min,
 // The fused display path: grey + vertical Lanczos3 in one pass over the dB spectrogram (the
 // grey image is never materialised), then the batched horizontal Lanczos3 + colormap. Same
 // per-pixel arithmetic and summation order as launch_render_batch (bit-identical bytes).
-// v_band: output rows per vertical block; v_rows / v_wts: the largest grey-row span / weight
-// count of such a band (its LDS tile).
+// v_band: output rows per vertical block; v_rows: the largest grey-row span of such a band
+// including the kv padding (its LDS tile); v_kv: taps per row padded to a multiple of 4.
 int launch_render_batch2(const float* spec, uint32_t bins, float max, float min,
                          const RenderDesc* d_desc, uint32_t n, uint32_t T_max, uint32_t H_max,
                          uint32_t nw_max, uint32_t nh, int h_taps, int h_span, uint32_t v_band,
-                         int v_rows, int v_wts, float* tmp, const uint8_t* cmap, uint8_t* rgb,
+                         int v_rows, int v_kv, float* tmp, const uint8_t* cmap, uint8_t* rgb,
                          hipStream_t s);
 int launch_spec_to_grey(const float* spec, uint32_t T, uint32_t bins, uint32_t H, float max,
                         float min, float* grey, hipStream_t s);
