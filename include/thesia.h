@@ -35,6 +35,8 @@ extern "C" {
 #define THESIA_ERR_DEVICE -6
 #define THESIA_ERR_BUFFER_TOO_SMALL -7
 #define THESIA_ERR_NEGATIVE -8     /* reference: assert!(x >= 0) in log_for_db, decibel.rs:34 */
+#define THESIA_ERR_PANIC -9        /* the reference panics for these arguments; the output is
+                                      * still written (documented per function) */
 
 const char* thesia_last_error(void);
 const char* thesia_version(void);
@@ -207,7 +209,17 @@ int thesia_spec_to_grey(const float* spec, size_t T, size_t bins, float up_ratio
 /* grey_to_rgb -- display.rs:56-61 (Lanczos3 resize + colormap). out [nh, nw, 3]. */
 int thesia_grey_to_rgb(const float* grey, uint32_t width, uint32_t height, uint32_t nwidth,
                        uint32_t nheight, uint8_t* out, size_t cap);
-/* wav_to_image -- display.rs:63-115. out [nheight, nwidth, 4] RGBA. */
+/* InvRealFFT -- realfft.rs:167-241 (InvRealFFT::new(length) + process per frame): n_frames
+ * spectra of length/2+1 complex values (re, im interleaved f32) -> n_frames rows of `length`
+ * reals, unnormalised (0.5 * Re of the full inverse DFT, the reference's complex_to_real test),
+ * in the reference's operation order (rustfft 4.0 Radix4, inverse). length even
+ * (THESIA_ERR_INVALID_ARG otherwise, "Length must be even") and a power of two <= 16384
+ * (THESIA_ERR_UNSUPPORTED: Radix4 panics on other sizes). _device: HBM buffers, stream-ordered. */
+int thesia_inv_real_fft_device(const float* d_in, size_t n_frames, size_t length, float* d_out);
+int thesia_inv_real_fft(const float* in, size_t n_frames, size_t length, float* out);
+/* wav_to_image -- display.rs:63-115. out [nheight, nwidth, 4] RGBA. THESIA_ERR_PANIC where
+ * the reference panics (a pixel's sample slice empty or holding NaN, or a column reaching row
+ * nheight, display.rs:95-108); the image is written anyway, such columns clamped / left blank. */
 int thesia_wav_to_image(const float* wav, size_t n, uint32_t nwidth, uint32_t nheight,
                         float amp_min, float amp_max, uint8_t* out, size_t cap);
 
@@ -271,6 +283,10 @@ int thesia_mt_set_setting(thesia_mt* mt, float win_ms, size_t t_overlap, size_t 
  * images". On error nothing is added (the reference would leave a half-added state). */
 int thesia_mt_add_tracks(thesia_mt* mt, const uint64_t* ids, size_t n_ids, const char* paths,
                          int* changed);
+/* WAV files keep their sample encoding up to the device: 8/16/24/32-bit integer or f32 samples
+ * are uploaded as stored (1-4 B per sample) and converted ((x as f32) / 2^(bits-1), 8-bit
+ * unsigned; audio.rs:15-19) and downmixed (lib.rs:42) there. All new tracks of one sample rate
+ * run as one batched spectrogram launch; the call synchronises once. */
 /* Same, from in-memory interleaved f32 PCM (what open_audio_file returns, audio.rs:9-37). */
 int thesia_mt_add_tracks_pcm(thesia_mt* mt, const uint64_t* ids, size_t n_ids,
                              const float* const* pcm, const uint64_t* n_samples,
@@ -281,7 +297,8 @@ int thesia_mt_remove_track(thesia_mt* mt, uint64_t id, int* changed);
 /* get_spec_image(id, px_per_sec, nheight) -> Vec<u8> RGB -- lib.rs:294-298 */
 int thesia_mt_get_spec_image(thesia_mt* mt, uint64_t id, float px_per_sec, uint32_t nheight,
                              uint8_t* out, size_t cap, size_t* needed);
-/* get_wav_image(id, px_per_sec, nheight, amp_min, amp_max) -> Vec<u8> RGBA -- lib.rs:300-313 */
+/* get_wav_image(id, px_per_sec, nheight, amp_min, amp_max) -> Vec<u8> RGBA -- lib.rs:300-313
+ * (THESIA_ERR_PANIC as thesia_wav_to_image, image written) */
 int thesia_mt_get_wav_image(thesia_mt* mt, uint64_t id, float px_per_sec, uint32_t nheight,
                             float amp_min, float amp_max, uint8_t* out, size_t cap,
                             size_t* needed);
@@ -303,6 +320,15 @@ int thesia_mt_get_spec(const thesia_mt* mt, uint64_t id, float* out, size_t cap_
 int thesia_mt_get_grey(const thesia_mt* mt, uint64_t id, float* out, size_t cap_floats,
                        uint32_t* width, uint32_t* height);
 int thesia_mt_track_count(const thesia_mt* mt, size_t* n);
+/* the track's mono wav (audio.rs:9-37 decode + lib.rs:42 channel sum) as held on the device */
+int thesia_mt_get_wav(const thesia_mt* mt, uint64_t id, float* out, size_t cap_floats,
+                      size_t* n_samples);
+
+/* open_audio_file (audio.rs:9-37) on the host, WAV only (hound semantics; the rodio fallback
+ * for FLAC / Vorbis returns THESIA_ERR_UNSUPPORTED): interleaved f32 samples [n][channels].
+ * out may be NULL to query *n_floats. */
+int thesia_open_audio_file(const char* path, float* out, size_t cap_floats, size_t* n_floats,
+                           uint32_t* sr, uint32_t* channels);
 
 #ifdef __cplusplus
 }

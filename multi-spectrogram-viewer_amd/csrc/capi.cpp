@@ -483,6 +483,29 @@ int thesia_render_rgb_multi(size_t n_groups, const float* const* d_specs, const 
     GUARD_END
 }
 
+int thesia_inv_real_fft_device(const float* d_in, size_t n_frames, size_t length, float* d_out) {
+    GUARD_BEGIN
+    if (n_frames && (!d_in || !d_out)) return set_error(THESIA_ERR_INVALID_ARG, "null device pointer");
+    return inv_real_fft_device(d_in, n_frames, length, d_out, default_stream());
+    GUARD_END
+}
+
+int thesia_inv_real_fft(const float* in, size_t n_frames, size_t length, float* out) {
+    GUARD_BEGIN
+    if (n_frames && (!in || !out)) return set_error(THESIA_ERR_INVALID_ARG, "null pointer");
+    if (length % 2) return set_error(THESIA_ERR_INVALID_ARG, "Length must be even (realfft.rs:171)");
+    if (n_frames == 0) return inv_real_fft_device(nullptr, 0, length, nullptr, default_stream());
+    DevBuf din, dout;
+    int rc = din.upload(in, n_frames * (length / 2 + 1) * 2 * sizeof(float));
+    if (!rc) rc = dout.alloc(n_frames * length * sizeof(float));
+    if (!rc) rc = inv_real_fft_device(din.as<float>(), n_frames, length, dout.as<float>(), default_stream());
+    if (rc) return rc;
+    THESIA_HIP(hipStreamSynchronize(default_stream()));
+    THESIA_HIP(hipMemcpy(out, dout.p, n_frames * length * sizeof(float), hipMemcpyDeviceToHost));
+    return THESIA_OK;
+    GUARD_END
+}
+
 int thesia_wav_to_image(const float* wav, size_t n, uint32_t nwidth, uint32_t nheight,
                         float amp_min, float amp_max, uint8_t* out, size_t cap) {
     GUARD_BEGIN
@@ -497,6 +520,9 @@ int thesia_wav_to_image(const float* wav, size_t n, uint32_t nwidth, uint32_t nh
                                       dimg.as<uint8_t>(), &panicked, default_stream());
     if (rc) return rc;
     THESIA_HIP(hipMemcpy(out, dimg.p, bytes, hipMemcpyDeviceToHost));
+    if (panicked)
+        return set_error(THESIA_ERR_PANIC, "the reference panics for these arguments (display.rs:95-108); "
+                                           "the image is written with the column clamped");
     return THESIA_OK;
     GUARD_END
 }
@@ -545,9 +571,11 @@ int thesia_mt_add_tracks(thesia_mt* mt, const uint64_t* ids, size_t n_ids, const
         std::string err;
         int rc = read_wav(pl[i], &wavs[i], &err);
         if (rc) return set_error(rc, err);
-        pcm[i].samples = wavs[i].samples.data();
+        pcm[i].data = wavs[i].raw.data();
+        pcm[i].kind = wavs[i].kind;
+        pcm[i].scale = pcm_scale(wavs[i].kind, wavs[i].bits);
         pcm[i].channels = wavs[i].channels;
-        pcm[i].n_samples = wavs[i].samples.size() / wavs[i].channels;
+        pcm[i].n_samples = wavs[i].n_frames;
         pcm[i].sr = wavs[i].sr;
         pcm[i].path = pl[i];
     }
@@ -564,7 +592,8 @@ int thesia_mt_add_tracks_pcm(thesia_mt* mt, const uint64_t* ids, size_t n_ids,
     std::vector<uint64_t> idv(ids, ids + n_ids);
     std::vector<PcmIn> pcm(n_ids);
     for (size_t i = 0; i < n_ids; ++i) {
-        pcm[i].samples = pcm_in[i];
+        pcm[i].data = pcm_in[i];
+        pcm[i].kind = PCM_F32;
         pcm[i].n_samples = n_samples[i];
         pcm[i].channels = channels[i];
         pcm[i].sr = sr[i];
@@ -583,20 +612,14 @@ int thesia_mt_remove_track(thesia_mt* mt, uint64_t id, int* changed) {
 int thesia_mt_get_spec_image(thesia_mt* mt, uint64_t id, float px_per_sec, uint32_t nheight,
                              uint8_t* out, size_t cap, size_t* needed) {
     GUARD_BEGIN
-    std::vector<uint8_t> img;
-    int rc = M(mt)->spec_image(id, px_per_sec, nheight, &img);
-    if (rc) return rc;
-    return copy_out(img.data(), img.size(), out, cap, needed);
+    return M(mt)->spec_image(id, px_per_sec, nheight, out, cap, needed);
     GUARD_END
 }
 
 int thesia_mt_get_wav_image(thesia_mt* mt, uint64_t id, float px_per_sec, uint32_t nheight,
                             float amp_min, float amp_max, uint8_t* out, size_t cap, size_t* needed) {
     GUARD_BEGIN
-    std::vector<uint8_t> img;
-    int rc = M(mt)->wav_image(id, px_per_sec, nheight, amp_min, amp_max, &img);
-    if (rc) return rc;
-    return copy_out(img.data(), img.size(), out, cap, needed);
+    return M(mt)->wav_image(id, px_per_sec, nheight, amp_min, amp_max, out, cap, needed);
     GUARD_END
 }
 
@@ -645,6 +668,38 @@ int thesia_mt_get_spec(const thesia_mt* mt, uint64_t id, float* out, size_t cap,
     return THESIA_OK;
     GUARD_END
 }
+int thesia_mt_get_wav(const thesia_mt* mt, uint64_t id, float* out, size_t cap, size_t* n) {
+    GUARD_BEGIN
+    std::vector<float> v;
+    int rc = M(mt)->wav_host(id, &v);
+    if (rc) return rc;
+    if (n) *n = v.size();
+    if (!out) return THESIA_OK;
+    if (cap < v.size()) return set_error(THESIA_ERR_BUFFER_TOO_SMALL, "wav buffer too small");
+    std::memcpy(out, v.data(), v.size() * 4);
+    return THESIA_OK;
+    GUARD_END
+}
+
+int thesia_open_audio_file(const char* path, float* out, size_t cap, size_t* n_floats, uint32_t* sr,
+                           uint32_t* channels) {
+    GUARD_BEGIN
+    if (!path) return set_error(THESIA_ERR_INVALID_ARG, "null path");
+    WavData w;
+    std::string err;
+    int rc = read_wav(path, &w, &err);
+    if (rc) return set_error(rc, err);
+    const size_t n = (size_t)w.n_frames * w.channels;
+    if (n_floats) *n_floats = n;
+    if (sr) *sr = w.sr;
+    if (channels) *channels = w.channels;
+    if (!out) return THESIA_OK;
+    if (cap < n) return set_error(THESIA_ERR_BUFFER_TOO_SMALL, "sample buffer too small");
+    decode_pcm_f32(w.raw.data(), w.kind, pcm_scale(w.kind, w.bits), n, out);
+    return THESIA_OK;
+    GUARD_END
+}
+
 int thesia_mt_get_grey(const thesia_mt* mt, uint64_t id, float* out, size_t cap, uint32_t* w,
                        uint32_t* h) {
     GUARD_BEGIN

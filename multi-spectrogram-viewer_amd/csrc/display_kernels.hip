@@ -80,6 +80,67 @@ int launch_downmix(const void* in, int in_format, int channels, uint64_t n, floa
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
+// WAV ingest (audio.rs:9-37 + lib.rs:42): the file's sample bytes -> f32 by hound's rule
+// ((x as f32) / 2^(bits-1), 8-bit unsigned x - 128, float as is), then the channel sum in the
+// order of downmix_kernel. kind: PCM_F32 0, PCM_U8 1, PCM_S16 2, PCM_S24 3, PCM_S32 4 (wav.hpp).
+template <int KIND>
+__device__ __forceinline__ float pcm_at(const uint8_t* raw, float scale, uint64_t i) {
+    if constexpr (KIND == 0) {
+        return reinterpret_cast<const float*>(raw)[i];
+    } else if constexpr (KIND == 1) {
+        return (float)((int32_t)raw[i] - 128) / scale;
+    } else if constexpr (KIND == 2) {
+        return (float)reinterpret_cast<const int16_t*>(raw)[i] / scale;
+    } else if constexpr (KIND == 3) {
+        const uint8_t* p = raw + 3 * i;
+        const int32_t v = (int32_t)((uint32_t)p[0] << 8 | (uint32_t)p[1] << 16 | (uint32_t)p[2] << 24) >> 8;
+        return (float)v / scale;
+    } else {
+        return (float)reinterpret_cast<const int32_t*>(raw)[i] / scale;
+    }
+}
+
+template <int KIND>
+__global__ void decode_downmix_kernel(const uint8_t* raw, float scale, int C, uint64_t n, float* out) {
+    for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n;
+         i += (uint64_t)gridDim.x * blockDim.x) {
+        const uint64_t p = i * (uint64_t)C;
+        float acc = 0.0f;
+        if (C < 8) {
+            for (int c = 0; c < C; ++c) acc = acc + pcm_at<KIND>(raw, scale, p + c);
+        } else {
+            float q[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+            int c = 0;
+            for (; C - c >= 8; c += 8)
+                for (int u = 0; u < 8; ++u) q[u] = q[u] + pcm_at<KIND>(raw, scale, p + c + u);
+            acc = acc + (q[0] + q[4]);
+            acc = acc + (q[1] + q[5]);
+            acc = acc + (q[2] + q[6]);
+            acc = acc + (q[3] + q[7]);
+            for (; c < C; ++c) acc = acc + pcm_at<KIND>(raw, scale, p + c);
+        }
+        out[i] = acc;
+    }
+}
+
+int launch_decode_downmix(const void* raw, int kind, float scale, int channels, uint64_t n, float* out,
+                          hipStream_t s) {
+    if (n == 0) return 0;
+    if (kind < 0 || kind > 4 || channels <= 0) return -2;
+    uint64_t blocks = (n + 255) / 256;
+    if (blocks > 8192) blocks = 8192;
+    const uint8_t* r = static_cast<const uint8_t*>(raw);
+    const dim3 g((unsigned)blocks), b(256);
+    switch (kind) {
+        case 0: hipLaunchKernelGGL(decode_downmix_kernel<0>, g, b, 0, s, r, scale, channels, n, out); break;
+        case 1: hipLaunchKernelGGL(decode_downmix_kernel<1>, g, b, 0, s, r, scale, channels, n, out); break;
+        case 2: hipLaunchKernelGGL(decode_downmix_kernel<2>, g, b, 0, s, r, scale, channels, n, out); break;
+        case 3: hipLaunchKernelGGL(decode_downmix_kernel<3>, g, b, 0, s, r, scale, channels, n, out); break;
+        default: hipLaunchKernelGGL(decode_downmix_kernel<4>, g, b, 0, s, r, scale, channels, n, out); break;
+    }
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
 // ------------------------------------------------------------------------------------
 // K3 per-track max/min (NaN -> flag)
 // ------------------------------------------------------------------------------------

@@ -954,6 +954,41 @@ int render_rgb_fused(size_t n_groups, const float* const* d_specs, const uint64_
     return THESIA_OK;
 }
 
+// InvRealFFT (realfft.rs:167-241) over device buffers: the length's tables come from a Plan
+// of n_fft = length, built once per (device, length) and kept
+int inv_real_fft_device(const float* d_in, size_t n_frames, size_t length, float* d_out, hipStream_t s) {
+    if (length % 2) return set_error(THESIA_ERR_INVALID_ARG, "Length must be even (realfft.rs:171)");
+    if (length < 2 || (length & (length - 1)))
+        return set_error(THESIA_ERR_UNSUPPORTED, "Radix4 needs a power-of-two length/2 (the reference panics)");
+    if (length > (1u << 14)) return set_error(THESIA_ERR_UNSUPPORTED, "length above 16384");
+    static std::mutex mu;
+    static auto& plans = *new std::map<std::pair<int, size_t>, Plan*>();  // leaked, see dev_taps
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    Plan* p = nullptr;
+    {
+        std::lock_guard<std::mutex> lk(mu);
+        auto it = plans.find({dev, length});
+        if (it != plans.end()) {
+            p = it->second;
+        } else {
+            thesia_plan_desc d{};
+            d.sr = 48000;
+            d.n_fft = length;
+            d.win_length = length;
+            d.hop_length = std::max<size_t>(1, length / 4);
+            d.output = THESIA_OUT_COMPLEX;
+            int rc = plan_create(d, &p);
+            if (rc) return rc;
+            plans[{dev, length}] = p;
+        }
+    }
+    if (launch_irfftx(d_in, n_frames, (int)length, p->xpos.as<int>(), p->tw.as<float>(),
+                      p->sincos.as<float>(), p->xw8, d_out, s))
+        return set_error(THESIA_ERR_DEVICE, "irfft launch failed");
+    return THESIA_OK;
+}
+
 int render_rgb_batch_device(const float* d_spec, const uint64_t* row0, size_t bins, size_t n,
                             const float* up_ratio, const uint32_t* nwidth, uint32_t nheight,
                             float max, float min, uint8_t* d_rgb, const uint64_t* rgb_off,

@@ -98,6 +98,11 @@ int stft3_lds_bytes(const StftLaunch& a);  // dynamic LDS of the launch (> 16384
 // stftx_kernel (every n_fft: the reference's operation order, bit-exact with the oracle)
 int launch_stftx(const StftLaunch& a, hipStream_t stream);
 int stftx_lds_bytes(int n_fft);
+// InvRealFFT (realfft.rs:167-241) in the reference's operation order: n_frames spectra of
+// length/2+1 complex (re, im interleaved) -> n_frames rows of `length` reals; tables of the
+// length's Plan (xpos, forward twiddles, sin_cos, base butterfly_8 twiddles)
+int launch_irfftx(const float* in, uint64_t n_frames, int length, const int* xpos, const float* tw1,
+                  const float* sincos, const float* xw8, float* out, hipStream_t s);
 // stft5_kernel (streaming, n_fft 2048 only, co-resident untangle pairs; stft5_kernels.hip)
 int launch_stft5(const StftLaunch& a, hipStream_t stream);
 bool stft5_supports(int n_fft, int win, int hop, int in_format, int channels);
@@ -106,6 +111,9 @@ int stft5_lds_bytes(const StftLaunch& a);
 int stft_kernel_info(int n_fft, int* lds_bytes, int* tile_frames, int* lanes_per_frame);
 
 // ---- display / misc kernels (display_kernels.hip) ----
+// WAV sample bytes (kind: wav.hpp PcmKind) -> f32 (hound, audio.rs:15-19) + channel sum (lib.rs:42)
+int launch_decode_downmix(const void* raw, int kind, float scale, int channels, uint64_t n, float* out,
+                          hipStream_t s);
 int launch_downmix(const void* in, int in_format, int channels, uint64_t n, float* out,
                    hipStream_t s);
 int launch_minmax(const float* x, uint64_t n, float* partial /*[2*nblk]*/, int* nan_flag,

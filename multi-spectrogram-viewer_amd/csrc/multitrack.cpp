@@ -8,6 +8,7 @@
 #include <limits>
 
 #include "host_tables.hpp"
+#include "kernels.hpp"
 #include "wav.hpp"
 
 namespace thesia {
@@ -33,61 +34,9 @@ static std::string file_name_of(const std::string& p) {
     return s == std::string::npos ? p : p.substr(s + 1);
 }
 
-int MultiTrack::add_tracks(const std::vector<uint64_t>& ids, const std::vector<PcmIn>& pcm,
-                           int* changed) {
-    // 1) validate everything first (the reference returns Err mid-loop, lib.rs:174-177,
-    //    leaving earlier tracks inserted without specs; here an error changes nothing)
-    struct Pending { uint64_t id; Track tr; };
-    std::vector<Pending> pend;
-    for (size_t i = 0; i < ids.size(); ++i) {
-        const PcmIn& in = pcm[i];
-        if (in.channels == 0 || in.sr == 0)
-            return set_error(THESIA_ERR_INVALID_ARG, "invalid channels / sample rate");
-        Track tr;
-        tr.path = in.path;
-        tr.sr = in.sr;
-        tr.n = in.n_samples;
-        track_params(in.sr, set_.win_ms, set_.t_overlap, set_.f_overlap, &tr.win, &tr.hop, &tr.n_fft);
-        if (tr.n_fft > 4096 || tr.win == 0)
-            return set_error(THESIA_ERR_UNSUPPORTED, "derived n_fft outside [2, 4096]");
-        if (stft_n_frames(tr.n, tr.win, tr.hop) == 0)
-            return set_error(THESIA_ERR_TOO_SHORT, "track '" + in.path + "' is shorter than the window (lib.rs:413)");
-        // upload interleaved PCM and downmix on the device (lib.rs:42)
-        DevBuf raw;
-        int rc = raw.upload(in.samples, (size_t)in.n_samples * in.channels * sizeof(float));
-        if (!rc) rc = tr.wav.alloc((size_t)std::max<uint64_t>(tr.n, 1) * sizeof(float));
-        if (rc) return rc;
-        if (launch_downmix(raw.p, IN_F32, (int)in.channels, tr.n, tr.wav.as<float>(), default_stream()))
-            return set_error(THESIA_ERR_DEVICE, "downmix launch failed");
-        THESIA_HIP(hipStreamSynchronize(default_stream()));
-        pend.push_back({ids[i], std::move(tr)});
-    }
-    // 2) insert (lib.rs:178-186)
-    for (auto& p : pend) {
-        const float sec = (float)p.tr.n / (float)p.tr.sr;
-        if (sec > max_sec_) {
-            max_sec_ = sec;
-            id_max_sec_ = p.id;
-        }
-        tracks_[p.id] = std::move(p.tr);
-    }
-    // 3) update_specs (lib.rs:142-168): plans per new sr, then one spectrogram per id
-    for (auto& p : pend) {
-        int rc = compute_spec(p.id);
-        if (rc) return rc;
-    }
-    // 4) update_spec_greys (lib.rs:193-263)
-    return update_spec_greys(changed);
-}
-
-int MultiTrack::plan_for(uint32_t sr, const Track& tr, Plan** out) {
-    auto it = plans_.find(sr);
-    if (it != plans_.end()) {
-        *out = it->second;
-        return THESIA_OK;
-    }
+int MultiTrack::make_plan(const Track& tr, Plan** out) const {
     thesia_plan_desc d{};
-    d.sr = sr;
+    d.sr = tr.sr;
     d.win_length = tr.win;
     d.hop_length = tr.hop;
     d.n_fft = tr.n_fft;
@@ -96,55 +45,185 @@ int MultiTrack::plan_for(uint32_t sr, const Track& tr, Plan** out) {
     d.n_mels = 0;        // calc_mel_fb_default, lib.rs:155
     d.fmin = 0.f;
     d.fmax = -1.f;
-    Plan* p = nullptr;
-    int rc = plan_create(d, &p);
-    if (rc) return rc;
-    plans_[sr] = p;
-    *out = p;
-    return THESIA_OK;
+    return plan_create(d, out);
 }
 
-int MultiTrack::compute_spec(uint64_t id) {
-    Track& tr = tracks_.at(id);
-    Plan* plan = nullptr;
-    int rc = plan_for(tr.sr, tr, &plan);
-    if (rc) return rc;
-    tr.bins = plan->row_bins();
-    tr.T = stft_n_frames(tr.n, tr.win, tr.hop);
-    rc = tr.spec.alloc((size_t)tr.T * tr.bins * sizeof(float));
-    if (rc) return rc;
-    const uint64_t off = 0, len = tr.n;
-    thesia_batch_desc bd{};
-    bd.input_format = THESIA_IN_F32;
-    bd.channels = 1;
-    bd.fold_mono = 0;  // the device wav is already the folded channel sum
-    bd.d_input = tr.wav.p;
-    bd.track_offset = &off;
-    bd.track_len = &len;
-    bd.n_tracks = 1;
-    bd.d_output = tr.spec.p;
-    Batch* b = nullptr;
-    rc = batch_create(plan, bd, &b);
-    if (rc) return rc;
-    // the viewer path computes in the reference's operation order (stftx_kernel): its images
-    // are the oracle pipeline's bytes
-    rc = batch_set_option(b, THESIA_BATCH_OPT_KERNEL, 9);
-    if (!rc) rc = batch_run(b, default_stream());
-    if (!rc) {
-        hipError_t e = hipStreamSynchronize(default_stream());
-        if (e != hipSuccess) rc = set_error(THESIA_ERR_DEVICE, hipGetErrorString(e));
+int MultiTrack::add_tracks(const std::vector<uint64_t>& ids, const std::vector<PcmIn>& pcm,
+                           int* changed) {
+    const hipStream_t s = default_stream();
+    // 1) validate every new track before any device work (the reference returns Err mid-loop,
+    //    lib.rs:174-177, leaving earlier tracks inserted without specs; here an error at any
+    //    step changes nothing)
+    std::vector<Track> nt(ids.size());
+    for (size_t i = 0; i < ids.size(); ++i) {
+        const PcmIn& in = pcm[i];
+        if (in.channels == 0 || in.sr == 0)
+            return set_error(THESIA_ERR_INVALID_ARG, "invalid channels / sample rate");
+        if (in.kind < PCM_F32 || in.kind > PCM_S32 || (in.n_samples && !in.data))
+            return set_error(THESIA_ERR_INVALID_ARG, "invalid sample buffer");
+        Track& tr = nt[i];
+        tr.path = in.path;
+        tr.sr = in.sr;
+        tr.n = in.n_samples;
+        track_params(in.sr, set_.win_ms, set_.t_overlap, set_.f_overlap, &tr.win, &tr.hop, &tr.n_fft);
+        if (tr.n_fft > 4096 || tr.win == 0)
+            return set_error(THESIA_ERR_UNSUPPORTED, "derived n_fft outside [2, 4096]");
+        if (stft_n_frames(tr.n, tr.win, tr.hop) == 0)
+            return set_error(THESIA_ERR_TOO_SHORT, "track '" + in.path + "' is shorter than the window (lib.rs:413)");
     }
-    delete b;
-    if (rc) return rc;
-    // per-track max / min (lib.rs:197-200); a NaN makes ndarray-stats return Err -> +-inf
-    float mx, mn;
-    bool nan;
-    rc = minmax_device(tr.spec.as<float>(), (uint64_t)tr.T * tr.bins, &mx, &mn, &nan, default_stream());
-    if (rc) return rc;
-    tr.spec_max = nan ? -INFINITY : mx;
-    tr.spec_min = nan ? INFINITY : mn;
-    tr.has_grey = false;
-    return THESIA_OK;
+    // 2) per sample rate (update_specs, lib.rs:142-168): the new tracks' samples uploaded in
+    //    their file encoding (1-4 B per sample), converted + downmixed on the device into one
+    //    mono pool, one Batch over all of them (the reference-order kernel) into one
+    //    spectrogram pool; a single synchronisation for the whole call
+    std::map<uint32_t, std::vector<size_t>> by_sr;
+    for (size_t i = 0; i < nt.size(); ++i) by_sr[nt[i].sr].push_back(i);
+    std::map<uint32_t, std::unique_ptr<Plan>> new_plans;
+    std::vector<std::unique_ptr<DevBuf>> raws;  // upload staging, freed after the sync
+    struct Group {
+        std::unique_ptr<Batch> batch;
+        std::vector<uint64_t> off, len;
+        const float* spec = nullptr;
+        size_t bins = 0;
+        std::vector<size_t> idx;
+    };
+    std::vector<Group> groups;
+    for (auto& [sr, idx] : by_sr) {
+        Plan* plan = nullptr;
+        auto pit = plans_.find(sr);
+        if (pit != plans_.end()) {
+            plan = pit->second;
+        } else {
+            int rc = make_plan(nt[idx[0]], &plan);
+            if (rc) return rc;
+            new_plans[sr].reset(plan);
+        }
+        Group g;
+        g.idx = idx;
+        uint64_t rb = 0, wf = 0, T_all = 0;
+        std::vector<uint64_t> roff(idx.size());
+        for (size_t k = 0; k < idx.size(); ++k) {
+            const PcmIn& in = pcm[idx[k]];
+            roff[k] = rb;
+            rb += (in.n_samples * in.channels * pcm_bytes(in.kind) + 255) & ~uint64_t(255);
+            g.off.push_back(wf);
+            g.len.push_back(nt[idx[k]].n);
+            wf += (nt[idx[k]].n + 63) & ~uint64_t(63);
+            T_all += stft_n_frames(nt[idx[k]].n, nt[idx[k]].win, nt[idx[k]].hop);
+        }
+        raws.push_back(std::make_unique<DevBuf>());
+        DevBuf& raw = *raws.back();
+        auto wav = std::make_shared<DevBuf>();
+        auto spec = std::make_shared<DevBuf>();
+        g.bins = plan->row_bins();
+        int rc = raw.alloc(std::max<uint64_t>(rb, 1));
+        if (!rc) rc = wav->alloc(std::max<uint64_t>(wf, 1) * sizeof(float));
+        if (!rc) rc = spec->alloc(std::max<uint64_t>(T_all * g.bins, 1) * sizeof(float));
+        if (rc) return rc;
+        for (size_t k = 0; k < idx.size(); ++k) {
+            const PcmIn& in = pcm[idx[k]];
+            const uint64_t bytes = in.n_samples * in.channels * pcm_bytes(in.kind);
+            uint8_t* dst = raw.as<uint8_t>() + roff[k];
+            if (bytes) THESIA_HIP(hipMemcpyAsync(dst, in.data, bytes, hipMemcpyHostToDevice, s));
+            if (launch_decode_downmix(dst, in.kind, in.scale, (int)in.channels, in.n_samples,
+                                      wav->as<float>() + g.off[k], s))
+                return set_error(THESIA_ERR_DEVICE, "decode / downmix launch failed");
+        }
+        thesia_batch_desc bd{};
+        bd.input_format = THESIA_IN_F32;
+        bd.channels = 1;
+        bd.fold_mono = 0;  // the pool holds the folded channel sums already
+        bd.d_input = wav->p;
+        bd.track_offset = g.off.data();
+        bd.track_len = g.len.data();
+        bd.n_tracks = idx.size();
+        bd.d_output = spec->p;
+        Batch* b = nullptr;
+        rc = batch_create(plan, bd, &b);
+        if (rc) return rc;
+        g.batch.reset(b);
+        // the viewer path computes in the reference's operation order (stftx_kernel): its
+        // images are the oracle pipeline's bytes
+        rc = batch_set_option(b, THESIA_BATCH_OPT_KERNEL, 9);
+        if (!rc) rc = batch_run(b, s);
+        if (rc) return rc;
+        g.spec = spec->as<float>();
+        for (size_t k = 0; k < idx.size(); ++k) {
+            Track& tr = nt[idx[k]];
+            tr.wav_pool = wav;
+            tr.wav_off = g.off[k];
+            tr.spec_pool = spec;
+            tr.bins = g.bins;
+            tr.T = b->frame0[k + 1] - b->frame0[k];
+            tr.spec_off = b->frame0[k] * g.bins;
+        }
+        groups.push_back(std::move(g));
+    }
+    {
+        hipError_t e = hipStreamSynchronize(s);
+        if (e != hipSuccess) return set_error(THESIA_ERR_DEVICE, hipGetErrorString(e));
+    }
+    raws.clear();
+    // 3) per-track max / min (lib.rs:197-200; a NaN makes ndarray-stats return Err -> +-inf):
+    //    one launch over every group
+    {
+        std::vector<const float*> specs;
+        std::vector<const uint64_t*> row0s;
+        std::vector<size_t> bins, ns;
+        for (const Group& g : groups) {
+            specs.push_back(g.spec);
+            row0s.push_back(g.batch->frame0.data());
+            bins.push_back(g.bins);
+            ns.push_back(g.idx.size());
+        }
+        std::vector<float> mx(nt.size()), mn(nt.size());
+        std::vector<int> nan(nt.size());
+        int rc = minmax_segments_multi(groups.size(), specs.data(), row0s.data(), bins.data(), ns.data(),
+                                       mx.data(), mn.data(), nan.data(), s);
+        if (rc) return rc;
+        size_t t = 0;
+        for (const Group& g : groups)
+            for (size_t i : g.idx) {
+                nt[i].spec_max = nan[t] ? -INFINITY : mx[t];
+                nt[i].spec_min = nan[t] ? INFINITY : mn[t];
+                ++t;
+            }
+    }
+    groups.clear();
+    // 4) insert (lib.rs:178-186), then update_spec_greys (lib.rs:193-263); if that fails
+    //    (device memory for the grey images) the insertion is rolled back
+    std::map<uint64_t, std::unique_ptr<Track>> undo;  // id -> replaced track (null: was absent)
+    const float max_sec0 = max_sec_;
+    const uint64_t id_max_sec0 = id_max_sec_;
+    for (size_t i = 0; i < ids.size(); ++i) {
+        const uint64_t id = ids[i];
+        if (!undo.count(id)) {
+            auto it = tracks_.find(id);
+            undo[id] = it == tracks_.end() ? nullptr : std::make_unique<Track>(std::move(it->second));
+        }
+        const float sec = (float)nt[i].n / (float)nt[i].sr;
+        if (sec > max_sec_) {
+            max_sec_ = sec;
+            id_max_sec_ = id;
+        }
+        tracks_[id] = std::move(nt[i]);
+    }
+    for (auto& [sr, p] : new_plans) plans_[sr] = p.release();
+    int rc = update_spec_greys(changed);
+    if (rc) {
+        for (auto& [id, old] : undo) {
+            if (old) tracks_[id] = std::move(*old);
+            else tracks_.erase(id);
+        }
+        for (auto it = plans_.begin(); it != plans_.end();) {
+            bool used = false;
+            for (auto& kv : tracks_) used |= kv.second.sr == it->first;
+            if (!used) { delete it->second; it = plans_.erase(it); }
+            else ++it;
+        }
+        max_sec_ = max_sec0;
+        id_max_sec_ = id_max_sec0;
+    }
+    return rc;
 }
 
 // approx 0.4 AbsDiffEq for f32: (if a > b { a - b } else { b - a }) <= eps
@@ -162,30 +241,42 @@ int MultiTrack::update_spec_greys(int* changed_out) {
     mx = fminf(mx, 0.0f);                       // lib.rs:208
     mn = fmaxf(mn, mx - set_.db_range);         // lib.rs:209
     bool changed = false;
-    if (abs_diff_ne(max_db_, mx, 1e-3f)) { max_db_ = mx; changed = true; }  // lib.rs:211-214
-    if (abs_diff_ne(min_db_, mn, 1e-3f)) { min_db_ = mn; changed = true; }  // lib.rs:215-218
+    float max_db = max_db_, min_db = min_db_;
+    if (abs_diff_ne(max_db, mx, 1e-3f)) { max_db = mx; changed = true; }  // lib.rs:211-214
+    if (abs_diff_ne(min_db, mn, 1e-3f)) { min_db = mn; changed = true; }  // lib.rs:215-218
     uint32_t max_sr = 0;
     for (auto& kv : tracks_) max_sr = std::max(max_sr, kv.second.sr);     // lib.rs:220-224
-    if (max_sr_ != max_sr) { max_sr_ = max_sr; changed = true; }
+    if (max_sr_ != max_sr) changed = true;
     // lib.rs:230-261 rebuilds every grey when changed; tracks that never got a grey are
-    // built too (the reference leaves them missing and get_spec_image then panics).
+    // built too (the reference leaves them missing and get_spec_image then panics). Every
+    // new grey buffer is allocated before any state changes (a failure leaves all as it was).
+    struct Job { Track* tr; uint32_t h; DevBuf buf; };
+    std::vector<Job> jobs;
     for (auto& kv : tracks_) {
         Track& tr = kv.second;
         if (!changed && tr.has_grey) continue;
         float up_ratio;
         if (set_.freq_scale == 1)
-            up_ratio = hz_to_mel((float)max_sr_ / 2.0f) / hz_to_mel((float)tr.sr / 2.0f);
+            up_ratio = hz_to_mel((float)max_sr / 2.0f) / hz_to_mel((float)tr.sr / 2.0f);
         else
-            up_ratio = (float)max_sr_ / (float)tr.sr;
-        float h = roundf((float)tr.bins * up_ratio);  // display.rs:45
-        tr.grey_h = h > 0.f ? (uint32_t)h : 0;
-        if (tr.grey_h < tr.bins) tr.grey_h = (uint32_t)tr.bins;
-        int rc = tr.grey.alloc((size_t)tr.grey_h * tr.T * sizeof(float));
+            up_ratio = (float)max_sr / (float)tr.sr;
+        const float h = roundf((float)tr.bins * up_ratio);  // display.rs:45
+        uint32_t gh = h > 0.f ? (uint32_t)h : 0;
+        if (gh < tr.bins) gh = (uint32_t)tr.bins;
+        jobs.push_back(Job{&tr, gh, DevBuf()});
+        int rc = jobs.back().buf.alloc(std::max<size_t>((size_t)gh * tr.T, 1) * sizeof(float));
         if (rc) return rc;
-        if (launch_spec_to_grey(tr.spec.as<float>(), (uint32_t)tr.T, (uint32_t)tr.bins, tr.grey_h,
-                                max_db_, min_db_, tr.grey.as<float>(), default_stream()))
+    }
+    max_db_ = max_db;
+    min_db_ = min_db;
+    max_sr_ = max_sr;
+    for (Job& j : jobs) {
+        if (launch_spec_to_grey(j.tr->spec(), (uint32_t)j.tr->T, (uint32_t)j.tr->bins, j.h, max_db_,
+                                min_db_, j.buf.as<float>(), default_stream()))
             return set_error(THESIA_ERR_DEVICE, "spec_to_grey launch failed");
-        tr.has_grey = true;
+        j.tr->grey = std::move(j.buf);
+        j.tr->grey_h = j.h;
+        j.tr->has_grey = true;
     }
     THESIA_HIP(hipStreamSynchronize(default_stream()));
     if (changed_out) *changed_out = changed ? 1 : 0;
@@ -221,39 +312,61 @@ const Track* MultiTrack::find(uint64_t id) const {
     return it == tracks_.end() ? nullptr : &it->second;
 }
 
-int MultiTrack::spec_image(uint64_t id, float px_per_sec, uint32_t nheight, std::vector<uint8_t>* out) {
+static uint32_t image_width(float px_per_sec, const Track& tr) {  // lib.rs:296, :309
+    const float wf = px_per_sec * (float)tr.n / (float)tr.sr;
+    return wf >= 4294967295.0f ? 4294967295u : (wf > 0.f ? (uint32_t)wf : 0u);
+}
+
+int MultiTrack::spec_image(uint64_t id, float px_per_sec, uint32_t nheight, uint8_t* out,
+                           size_t cap, size_t* needed) {
     const Track* tr = find(id);
     if (!tr) return set_error(THESIA_ERR_UNKNOWN_ID, "unknown track id");
-    const float wf = px_per_sec * (float)tr->n / (float)tr->sr;  // lib.rs:296
-    const uint32_t nwidth = wf >= 4294967295.0f ? 4294967295u : (wf > 0.f ? (uint32_t)wf : 0u);
-    out->assign((size_t)nwidth * nheight * 3, 0);
-    if (out->empty()) return THESIA_OK;
-    DevBuf rgb;
-    int rc = rgb.alloc(out->size());
+    const size_t bytes = (size_t)image_width(px_per_sec, *tr) * nheight * 3;
+    if (needed) *needed = bytes;
+    if (bytes == 0) return THESIA_OK;
+    if (!out || cap < bytes) return set_error(THESIA_ERR_BUFFER_TOO_SMALL, "output buffer too small");
+    if (img_.bytes < bytes) {
+        img_.release();
+        int rc = img_.alloc(bytes);
+        if (rc) return rc;
+    }
+    int rc = grey_to_rgb_device(tr->grey.as<float>(), (uint32_t)tr->T, tr->grey_h,
+                                image_width(px_per_sec, *tr), nheight, img_.as<uint8_t>(), default_stream());
     if (rc) return rc;
-    rc = grey_to_rgb_device(tr->grey.as<float>(), (uint32_t)tr->T, tr->grey_h, nwidth, nheight,
-                            rgb.as<uint8_t>(), default_stream());
-    if (rc) return rc;
-    THESIA_HIP(hipMemcpy(out->data(), rgb.p, out->size(), hipMemcpyDeviceToHost));
+    THESIA_HIP(hipMemcpy(out, img_.p, bytes, hipMemcpyDeviceToHost));
     return THESIA_OK;
 }
 
 int MultiTrack::wav_image(uint64_t id, float px_per_sec, uint32_t nheight, float amp_min,
-                          float amp_max, std::vector<uint8_t>* out) {
+                          float amp_max, uint8_t* out, size_t cap, size_t* needed) {
     const Track* tr = find(id);
     if (!tr) return set_error(THESIA_ERR_UNKNOWN_ID, "unknown track id");
-    const float wf = px_per_sec * (float)tr->n / (float)tr->sr;  // lib.rs:309
-    const uint32_t nwidth = wf >= 4294967295.0f ? 4294967295u : (wf > 0.f ? (uint32_t)wf : 0u);
-    out->assign((size_t)nwidth * nheight * 4, 0);
-    if (out->empty()) return THESIA_OK;
-    DevBuf img;
-    int rc = img.alloc(out->size());
-    if (rc) return rc;
+    const uint32_t nwidth = image_width(px_per_sec, *tr);
+    const size_t bytes = (size_t)nwidth * nheight * 4;
+    if (needed) *needed = bytes;
+    if (bytes == 0) return THESIA_OK;
+    if (!out || cap < bytes) return set_error(THESIA_ERR_BUFFER_TOO_SMALL, "output buffer too small");
+    if (img_.bytes < bytes) {
+        img_.release();
+        int rc = img_.alloc(bytes);
+        if (rc) return rc;
+    }
     int panicked = 0;
-    rc = wav_to_image_device(tr->wav.as<float>(), tr->n, nwidth, nheight, amp_min, amp_max,
-                             img.as<uint8_t>(), &panicked, default_stream());
+    int rc = wav_to_image_device(tr->wav(), tr->n, nwidth, nheight, amp_min, amp_max,
+                                 img_.as<uint8_t>(), &panicked, default_stream());
     if (rc) return rc;
-    THESIA_HIP(hipMemcpy(out->data(), img.p, out->size(), hipMemcpyDeviceToHost));
+    THESIA_HIP(hipMemcpy(out, img_.p, bytes, hipMemcpyDeviceToHost));
+    if (panicked)
+        return set_error(THESIA_ERR_PANIC, "the reference panics for these arguments (display.rs:95-108); "
+                                           "the image is written with the column clamped");
+    return THESIA_OK;
+}
+
+int MultiTrack::wav_host(uint64_t id, std::vector<float>* out) const {
+    const Track* tr = find(id);
+    if (!tr) return set_error(THESIA_ERR_UNKNOWN_ID, "unknown track id");
+    out->resize(tr->n);
+    if (tr->n) THESIA_HIP(hipMemcpy(out->data(), tr->wav(), tr->n * 4, hipMemcpyDeviceToHost));
     return THESIA_OK;
 }
 
@@ -270,7 +383,7 @@ int MultiTrack::spec_host(uint64_t id, std::vector<float>* out, size_t* T, size_
     const Track* tr = find(id);
     if (!tr) return set_error(THESIA_ERR_UNKNOWN_ID, "unknown track id");
     out->resize((size_t)tr->T * tr->bins);
-    THESIA_HIP(hipMemcpy(out->data(), tr->spec.p, out->size() * 4, hipMemcpyDeviceToHost));
+    THESIA_HIP(hipMemcpy(out->data(), tr->spec(), out->size() * 4, hipMemcpyDeviceToHost));
     *T = tr->T;
     *bins = tr->bins;
     return THESIA_OK;

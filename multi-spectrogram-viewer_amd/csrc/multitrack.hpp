@@ -3,6 +3,7 @@
 
 #include <cstdint>
 #include <map>
+#include <memory>
 #include <string>
 #include <vector>
 
@@ -15,18 +16,27 @@ struct Track {  // AudioTrack (lib.rs:30-37) + per-track caches (lib.rs:78-79)
     uint32_t sr = 0;
     uint64_t n = 0;  // samples after downmix
     size_t win = 0, hop = 0, n_fft = 0;
-    DevBuf wav;      // mono f32 [n]
-    DevBuf spec;     // dB [T, bins]
+    // the mono wav and the dB spectrogram live in buffers shared by the tracks of one
+    // add_tracks call and sample rate (one batched launch), freed with their last track
+    std::shared_ptr<DevBuf> wav_pool, spec_pool;
+    uint64_t wav_off = 0, spec_off = 0;  // float offsets into the pools
     size_t T = 0, bins = 0;
     float spec_max = -INFINITY, spec_min = INFINITY;
     DevBuf grey;     // [grey_h, T]
     uint32_t grey_h = 0;
     bool has_grey = false;
+    const float* wav() const { return wav_pool->as<float>() + wav_off; }
+    const float* spec() const { return spec_pool->as<float>() + spec_off; }
 };
 
+// One new track for add_tracks: interleaved samples [n_frames][channels] in their file
+// encoding (kind: wav.hpp PcmKind; f32 for the in-memory entry point), uploaded as they are
+// and converted + downmixed on the device.
 struct PcmIn {
-    const float* samples = nullptr;  // interleaved [n][ch]
-    uint64_t n_samples = 0;          // per channel
+    const void* data = nullptr;
+    int kind = 0;          // PCM_F32
+    float scale = 1.0f;    // integer divisor 2^(bits-1) (audio.rs:15-19)
+    uint64_t n_samples = 0;  // per channel
     uint32_t channels = 0, sr = 0;
     std::string path;
 };
@@ -44,9 +54,13 @@ class MultiTrack {
     int set_setting(float win_ms, size_t t_overlap, size_t f_overlap, int freq_scale, float db_range);
     int add_tracks(const std::vector<uint64_t>& ids, const std::vector<PcmIn>& pcm, int* changed);
     int remove_track(uint64_t id, int* changed);
-    int spec_image(uint64_t id, float px_per_sec, uint32_t nheight, std::vector<uint8_t>* out);
+    // images straight into the caller's buffer: *needed = bytes; THESIA_ERR_BUFFER_TOO_SMALL
+    // (nothing computed) when cap is short
+    int spec_image(uint64_t id, float px_per_sec, uint32_t nheight, uint8_t* out, size_t cap,
+                   size_t* needed);
     int wav_image(uint64_t id, float px_per_sec, uint32_t nheight, float amp_min, float amp_max,
-                  std::vector<uint8_t>* out);
+                  uint8_t* out, size_t cap, size_t* needed);
+    int wav_host(uint64_t id, std::vector<float>* out) const;
     int frequency_hz(uint64_t id, float rel, float* hz) const;
     int spec_host(uint64_t id, std::vector<float>* out, size_t* T, size_t* bins) const;
     int grey_host(uint64_t id, std::vector<float>* out, uint32_t* w, uint32_t* h) const;
@@ -58,8 +72,7 @@ class MultiTrack {
     size_t size() const { return tracks_.size(); }
 
   private:
-    int plan_for(uint32_t sr, const Track& tr, Plan** out);
-    int compute_spec(uint64_t id);
+    int make_plan(const Track& tr, Plan** out) const;
     int update_spec_greys(int* changed);
 
     Setting set_;
@@ -68,6 +81,7 @@ class MultiTrack {
     float max_db_ = -INFINITY, min_db_ = INFINITY, max_sec_ = 0.f;
     uint64_t id_max_sec_ = 0;
     uint32_t max_sr_ = 0;
+    DevBuf img_;  // image scratch (grow-only)
 };
 
 }  // namespace thesia

@@ -198,6 +198,120 @@ stftx_kernel(StftLaunch a) {
     }
 }
 
+// ------------------------------------------------------------------------------------
+// InvRealFFT (realfft.rs:167-241): spectrum of NC+1 bins -> 2*NC real samples, unnormalised
+// (the reference's complex_to_real test: 0.5 * Re(full inverse DFT)). Same structure as
+// stftx: one wave per frame; the realfft pre-twiddle (realfft.rs:210-219) written straight to
+// the prepare_radix4 positions, then rustfft 4.0 Radix4 with inverse = true: conjugated
+// twiddles (compute_twiddle(..).conj(), exact), rotate_90 by +i, and butterfly_4's inverse
+// output pair; the complex result is the real output, pairs interleaved (realfft.rs:225-230).
+// ------------------------------------------------------------------------------------
+namespace {
+__device__ __forceinline__ Cx xconj(Cx a) { return Cx{a.re, -a.im}; }
+__device__ __forceinline__ Cx xrot90i(Cx v) { return Cx{-v.im, v.re}; }  // inverse: * (+i)
+__device__ __forceinline__ void xbfly4i(Cx* buf) {
+    Cx v0 = buf[0], v1 = buf[1], v2 = buf[2], v3 = buf[3];
+    xbfly2(v0, v2);
+    xbfly2(v1, v3);
+    v3 = xrot90i(v3);
+    xbfly2(v0, v1);
+    xbfly2(v2, v3);
+    buf[0] = v0; buf[1] = v2; buf[2] = v1; buf[3] = v3;
+}
+__device__ __forceinline__ void xbfly8i(Cx* buf, Cx w1, Cx w3) {
+    Cx s[8] = {buf[0], buf[2], buf[4], buf[6], buf[1], buf[3], buf[5], buf[7]};
+    xbfly4i(s);
+    xbfly4i(s + 4);
+    s[5] = xmul(s[5], w1);
+    s[6] = xrot90i(s[6]);
+    s[7] = xmul(s[7], w3);
+    for (int i = 0; i < 4; ++i) xbfly2(s[i], s[i + 4]);
+    for (int i = 0; i < 8; ++i) buf[i] = s[i];
+}
+}  // namespace
+
+__global__ void __launch_bounds__(64 * kXWaves)
+irfftx_kernel(const float2* in, uint64_t n_frames, int NC, const int* xpos, const float2* tw1,
+              const float2* sincos, float4 w8, float* out) {
+    extern __shared__ __attribute__((aligned(16))) float xs[];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int bufl = (NC + 3) & ~3;
+    Cx* buf = reinterpret_cast<Cx*>(xs) + (size_t)wave * bufl;
+    const uint64_t g = (uint64_t)blockIdx.x * kXWaves + wave;
+    if (g >= n_frames) return;  // wave-uniform; no block barrier below
+    const float2* X = in + g * (uint64_t)(NC + 1);
+    // realfft.rs:210-219 (zip4 of input, input.rev(), sin_cos, buffer_in: k = 0 .. NC-1)
+    for (int k = lane; k < NC; k += 64) {
+        const float2 b = X[k], r = X[NC - k];
+        const float s = sincos[k].x, c = sincos[k].y;
+        const float xr = 0.5f * (((b.x + r.x) - c * (b.y + r.y)) - s * (b.x - r.x));
+        const float xi = 0.5f * (((b.y - r.y) + c * (b.x - r.x)) - s * (b.y + r.y));
+        buf[NC > 4 ? xpos[k] : k] = Cx{xr, xi};
+    }
+    wave_lds_sync();
+    if (NC == 2) {
+        if (lane == 0) xbfly2(buf[0], buf[1]);
+    } else if (NC == 4) {
+        if (lane == 0) xbfly4i(buf);
+    } else if (NC >= 8) {
+        const Cx* tw = reinterpret_cast<const Cx*>(tw1);  // forward twiddle(i, NC); conjugated below
+        int bits = 0;
+        while ((1 << bits) < NC) ++bits;
+        int cur;
+        if (bits % 2 == 0) {
+            for (int c = 4 * lane; c < NC; c += 256) xbfly4i(buf + c);
+            cur = 16;
+        } else {
+            const Cx w1 = xconj(Cx{w8.x, w8.y}), w3 = xconj(Cx{w8.z, w8.w});
+            for (int c = 8 * lane; c < NC; c += 512) xbfly8i(buf + c, w1, w3);
+            cur = 32;
+        }
+        for (; cur <= NC; cur *= 4) {
+            wave_lds_sync();
+            const int q = cur / 4, tstride = NC / cur;
+            for (int b = lane; b < NC / 4; b += 64) {
+                const int row = b / q, j = b - row * q;
+                Cx* d = buf + (size_t)row * cur;
+                // rustfft butterfly_4, inverse
+                const Cx s0 = xmul(d[j + q], xconj(tw[j * 1 * tstride]));
+                const Cx s1 = xmul(d[j + 2 * q], xconj(tw[j * 2 * tstride]));
+                const Cx s2 = xmul(d[j + 3 * q], xconj(tw[j * 3 * tstride]));
+                const Cx s5 = xsub(d[j], s1);
+                Cx d0 = xadd(d[j], s1);
+                const Cx s3 = xadd(s0, s2);
+                const Cx s4 = xsub(s0, s2);
+                d[j + 2 * q] = xsub(d0, s3);
+                d0 = xadd(d0, s3);
+                d[j] = d0;
+                d[j + q] = Cx{s5.re - s4.im, s5.im + s4.re};
+                d[j + 3 * q] = Cx{s5.re + s4.im, s5.im - s4.re};
+            }
+        }
+    }
+    wave_lds_sync();
+    float2* o = reinterpret_cast<float2*>(out + g * (uint64_t)(2 * NC));
+    for (int m = lane; m < NC; m += 64) o[m] = make_float2(buf[m].re, buf[m].im);
+}
+
+int launch_irfftx(const float* in, uint64_t n_frames, int length, const int* xpos, const float* tw1,
+                  const float* sincos, const float* xw8, float* out, hipStream_t s) {
+    if (length < 2 || (length & (length - 1))) return -2;
+    const int NC = length / 2;
+    const int lds = kXWaves * ((NC + 3) & ~3) * 8;
+    if (lds > 163840) return -2;
+    if (hipFuncSetAttribute(reinterpret_cast<const void*>(irfftx_kernel),
+                            hipFuncAttributeMaxDynamicSharedMemorySize, lds) != hipSuccess)
+        return -1;
+    if (n_frames == 0) return 0;
+    const uint64_t blocks = (n_frames + kXWaves - 1) / kXWaves;
+    if (blocks > 0x7fffffffULL) return -2;
+    hipLaunchKernelGGL(irfftx_kernel, dim3((unsigned)blocks), dim3(64 * kXWaves), lds, s,
+                       reinterpret_cast<const float2*>(in), n_frames, NC, xpos,
+                       reinterpret_cast<const float2*>(tw1), reinterpret_cast<const float2*>(sincos),
+                       make_float4(xw8[0], xw8[1], xw8[2], xw8[3]), out);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
 int stftx_lds_bytes(int n_fft) {
     const int NC = n_fft / 2, F = NC + 1;
     const int bufl = (NC + 1 + 3) & ~3;

@@ -1,7 +1,8 @@
-// wav.cpp -- WAV decoding with hound 3.4 semantics (audio.rs:9-37): integer PCM becomes
-// (x as f32) / 2^(bits-1), float PCM is taken as is, samples stay channel-interleaved.
-// The reference's rodio fallback (FLAC / Vorbis, audio.rs:21-31) is out of scope: such
-// files return THESIA_ERR_UNSUPPORTED.
+// wav.cpp -- WAV parsing with hound 3.4 semantics (audio.rs:9-37): integer PCM converts as
+// (x as f32) / 2^(bits-1) (8-bit WAV unsigned, x - 128), float PCM is taken as is, samples stay
+// channel-interleaved. Parsing keeps the file's sample bytes (the device converts them);
+// decode_pcm_f32 is the host conversion. The reference's rodio fallback (FLAC / Vorbis,
+// audio.rs:21-31) is out of scope: such files return THESIA_ERR_UNSUPPORTED.
 #include "wav.hpp"
 
 #include <algorithm>
@@ -16,6 +17,27 @@ namespace thesia {
 static uint32_t rd32(const uint8_t* p) { return p[0] | (p[1] << 8) | (p[2] << 16) | ((uint32_t)p[3] << 24); }
 static uint16_t rd16(const uint8_t* p) { return (uint16_t)(p[0] | (p[1] << 8)); }
 
+float pcm_scale(int kind, uint32_t bits) {
+    return kind == PCM_F32 ? 1.0f : (float)(1ull << (bits - 1));
+}
+
+void decode_pcm_f32(const uint8_t* raw, int kind, float scale, uint64_t n, float* out) {
+    const int bps = pcm_bytes(kind);
+    for (uint64_t i = 0; i < n; ++i) {
+        const uint8_t* p = raw + i * bps;
+        if (kind == PCM_F32) {
+            std::memcpy(&out[i], p, 4);
+            continue;
+        }
+        int32_t v;
+        if (kind == PCM_U8) v = (int32_t)p[0] - 128;
+        else if (kind == PCM_S16) v = (int16_t)rd16(p);
+        else if (kind == PCM_S24) v = (int32_t)((uint32_t)p[0] << 8 | (uint32_t)p[1] << 16 | (uint32_t)p[2] << 24) >> 8;
+        else v = (int32_t)rd32(p);
+        out[i] = (float)v / scale;
+    }
+}
+
 int read_wav(const std::string& path, WavData* out, std::string* err) {
     FILE* f = std::fopen(path.c_str(), "rb");
     if (!f) {
@@ -24,6 +46,11 @@ int read_wav(const std::string& path, WavData* out, std::string* err) {
         return THESIA_ERR_IO;
     }
     std::vector<uint8_t> buf;
+    if (std::fseek(f, 0, SEEK_END) == 0) {
+        const long sz = std::ftell(f);
+        if (sz > 0) buf.reserve((size_t)sz);
+        std::fseek(f, 0, SEEK_SET);
+    }
     {
         uint8_t tmp[1 << 16];
         size_t n;
@@ -65,38 +92,31 @@ int read_wav(const std::string& path, WavData* out, std::string* err) {
         *err = "malformed WAV file (missing fmt or data chunk)";
         return THESIA_ERR_IO;
     }
-    const size_t bps = block_align / channels;  // bytes per sample
-    const size_t n_samp = data_len / bps;
-    out->sr = sr;
-    out->channels = channels;
-    out->samples.resize(n_samp);
-    if (fmt_tag == 3) {  // IEEE float
+    const size_t bps = block_align / channels;  // bytes per sample (container)
+    int kind;
+    if (fmt_tag == 3) {  // IEEE float: hound reads f32 only
         if (bits != 32 || bps != 4) {
             *err = "unsupported float WAV bit depth";
             return THESIA_ERR_UNSUPPORTED;
         }
-        std::memcpy(out->samples.data(), data, n_samp * 4);
-    } else if (fmt_tag == 1) {  // integer PCM: (x as f32) / 2^(bits-1), audio.rs:15-19
-        if (bits == 0 || bits > 32 || bps > 4 || bps * 8 < bits) {
+        kind = PCM_F32;
+    } else if (fmt_tag == 1) {
+        if (bits == 0 || bits > 32 || bps == 0 || bps > 4 || bps * 8 < bits) {
             *err = "unsupported integer WAV bit depth";
             return THESIA_ERR_UNSUPPORTED;
         }
-        const float scale = (float)(1u << (bits - 1));
-        for (size_t i = 0; i < n_samp; ++i) {
-            const uint8_t* p = data + i * bps;
-            int32_t v;
-            if (bps == 1) v = (int32_t)p[0] - 128;  // 8-bit WAV is unsigned
-            else if (bps == 2) v = (int16_t)rd16(p);
-            else if (bps == 3) v = (int32_t)((uint32_t)p[0] << 8 | (uint32_t)p[1] << 16 | (uint32_t)p[2] << 24) >> 8;
-            else v = (int32_t)rd32(p);
-            out->samples[i] = (float)v / scale;
-        }
+        kind = bps == 1 ? PCM_U8 : bps == 2 ? PCM_S16 : bps == 3 ? PCM_S24 : PCM_S32;
     } else {
         *err = "unsupported WAV format tag " + std::to_string(fmt_tag);
         return THESIA_ERR_UNSUPPORTED;
     }
+    out->sr = sr;
+    out->channels = channels;
+    out->bits = bits;
+    out->kind = kind;
     // audio.rs:32-34: truncate to whole frames
-    out->samples.resize((out->samples.size() / channels) * channels);
+    out->n_frames = (data_len / bps) / channels;
+    out->raw.assign(data, data + out->n_frames * channels * bps);
     return THESIA_OK;
 }
 

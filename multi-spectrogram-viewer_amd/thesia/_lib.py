@@ -101,6 +101,10 @@ _SIGS = {
     "thesia_render_rgb_multi": (_i, [_sz, C.POINTER(C.c_void_p), C.POINTER(_u64p), C.POINTER(_sz),
                                      C.POINTER(_sz), _fp, C.POINTER(C.c_uint32), _u32, _f, _f, C.c_void_p,
                                      _u64p]),
+    "thesia_mt_get_wav": (_i, [_vp, _u64, _fp, _sz, C.POINTER(_sz)]),
+    "thesia_inv_real_fft": (_i, [_fp, _sz, _sz, _fp]),
+    "thesia_inv_real_fft_device": (_i, [C.c_void_p, _sz, _sz, C.c_void_p]),
+    "thesia_open_audio_file": (_i, [C.c_char_p, _fp, _sz, C.POINTER(_sz), C.POINTER(_u32), C.POINTER(_u32)]),
     "thesia_mt_create": (_i, [C.POINTER(_vp)]),
     "thesia_mt_destroy": (None, [_vp]),
     "thesia_mt_set_setting": (_i, [_vp, _f, _sz, _sz, _i, _f]),
@@ -139,6 +143,8 @@ ERR_TOO_SHORT = -4
 ERR_UNSUPPORTED = -5
 ERR_DEVICE = -6
 ERR_BUFFER_TOO_SMALL = -7
+ERR_NEGATIVE = -8
+ERR_PANIC = -9  # the reference panics for these arguments (the output is still written)
 
 
 class ThesiaError(RuntimeError):

@@ -7,7 +7,7 @@ from typing import Optional, Sequence
 
 import numpy as np
 
-from ._lib import lib, check, _fp, _u8p, _u64p
+from ._lib import lib, check, _fp, _u8p, _u64p, ERR_BUFFER_TOO_SMALL, ERR_PANIC
 
 
 class FreqScale(enum.IntEnum):  # lib.rs:25-28
@@ -38,6 +38,16 @@ def perform_stft(input, win_length: int, hop_length: int, n_fft: int, window=Non
                                   window.ctypes.data_as(_fp) if window is not None else None,
                                   out.ctypes.data_as(_fp), out.shape[0], C.byref(nf)))
     return out[: nf.value]
+
+
+def open_audio_file(path: str):
+    """audio.rs:9-37 (WAV, hound semantics): (wav [channels, n] f32, sr)."""
+    n, sr, ch = C.c_size_t(), C.c_uint32(), C.c_uint32()
+    check(lib.thesia_open_audio_file(path.encode(), None, 0, C.byref(n), C.byref(sr), C.byref(ch)))
+    buf = np.empty(n.value, np.float32)
+    check(lib.thesia_open_audio_file(path.encode(), buf.ctypes.data_as(_fp), buf.size, C.byref(n),
+                                     C.byref(sr), C.byref(ch)))
+    return buf.reshape(-1, ch.value).T, sr.value
 
 
 class MultiTrack:
@@ -101,9 +111,29 @@ class MultiTrack:
         """lib.rs:294-298: RGB bytes, row-major [nheight][nwidth][3]."""
         return self._bytes(lib.thesia_mt_get_spec_image, id, px_per_sec, nheight)
 
-    def get_wav_image(self, id: int, px_per_sec: float, nheight: int, amp_min: float, amp_max: float) -> bytes:
-        """lib.rs:300-313: RGBA bytes."""
-        return self._bytes(lib.thesia_mt_get_wav_image, id, px_per_sec, nheight, amp_min, amp_max)
+    def get_wav_image(self, id: int, px_per_sec: float, nheight: int, amp_min: float, amp_max: float,
+                      allow_panic: bool = False) -> bytes:
+        """lib.rs:300-313: RGBA bytes. Where the reference panics (display.rs:95-108) this
+        raises ThesiaError(ERR_PANIC) unless allow_panic (then the clamped image is returned)."""
+        need = C.c_size_t()
+        rc = lib.thesia_mt_get_wav_image(self.h, id, px_per_sec, nheight, amp_min, amp_max, None, 0,
+                                         C.byref(need))
+        if rc not in (0, ERR_BUFFER_TOO_SMALL):
+            check(rc)
+        buf = (C.c_uint8 * max(need.value, 1))()
+        rc = lib.thesia_mt_get_wav_image(self.h, id, px_per_sec, nheight, amp_min, amp_max, buf,
+                                         need.value, C.byref(need))
+        if not (allow_panic and rc == ERR_PANIC):
+            check(rc)
+        return bytes(buf)[: need.value]
+
+    def get_wav(self, id: int) -> np.ndarray:
+        """The track's mono wav as held on the device (audio.rs:9-37 decode + lib.rs:42 sum)."""
+        n = C.c_size_t()
+        check(lib.thesia_mt_get_wav(self.h, id, None, 0, C.byref(n)))
+        out = np.empty(n.value, np.float32)
+        check(lib.thesia_mt_get_wav(self.h, id, out.ctypes.data_as(_fp), out.size, C.byref(n)))
+        return out
 
     def get_frequency_hz(self, id: int, relative_freq: float) -> float:
         out = C.c_float()

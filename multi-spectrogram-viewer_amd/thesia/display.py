@@ -3,7 +3,7 @@ import ctypes as C
 
 import numpy as np
 
-from ._lib import lib, check, _fp, _u8p
+from ._lib import lib, check, _fp, _u8p, ERR_PANIC
 
 COLORMAP = np.array([[0, 0, 4], [27, 12, 65], [74, 12, 107], [120, 28, 109], [165, 44, 96],
                      [207, 68, 70], [237, 105, 37], [251, 155, 6], [247, 209, 61],
@@ -33,11 +33,16 @@ def grey_to_rgb(grey: np.ndarray, nwidth: int, nheight: int) -> np.ndarray:
     return out
 
 
-def wav_to_image(wav: np.ndarray, nwidth: int, nheight: int, amp_range) -> np.ndarray:
-    """display.rs:63-115: min/max envelope in WAVECOLOR -> RGBA u8 [nheight, nwidth, 4]."""
+def wav_to_image(wav: np.ndarray, nwidth: int, nheight: int, amp_range, return_panic: bool = False):
+    """display.rs:63-115: min/max envelope in WAVECOLOR -> RGBA u8 [nheight, nwidth, 4]. Where
+    the reference panics (display.rs:95-108) this raises ThesiaError(ERR_PANIC); with
+    return_panic it returns (image, panicked) instead."""
     wav = np.ascontiguousarray(wav, np.float32)
     out = np.empty((nheight, nwidth, 4), np.uint8)
-    check(lib.thesia_wav_to_image(wav.ctypes.data_as(_fp), wav.size, nwidth, nheight,
-                                  float(amp_range[0]), float(amp_range[1]),
-                                  out.ctypes.data_as(_u8p), out.size))
-    return out
+    rc = lib.thesia_wav_to_image(wav.ctypes.data_as(_fp), wav.size, nwidth, nheight,
+                                 float(amp_range[0]), float(amp_range[1]),
+                                 out.ctypes.data_as(_u8p), out.size)
+    if return_panic and rc == ERR_PANIC:
+        return out, True
+    check(rc)
+    return (out, False) if return_panic else out

@@ -210,6 +210,72 @@ int or_pad_reflect_f32(const float* x, size_t n, size_t left, size_t right, floa
         }                                                                                    \
         o[half].re = buf[0].re - buf[0].im; o[half].im = (T)0; /* realfft.rs:157 */          \
     }                                                                                        \
+    /* rustfft 4.0 Radix4 with inverse = true: twiddles compute_twiddle(..).conj(),          \
+     * rotate_90 by +i, butterfly_4's inverse output pair (same passes as cfft_tab) */      \
+    static inline cx_##SUF rot90i_##SUF(cx_##SUF v) { cx_##SUF r = {-v.im, v.re}; return r; } \
+    static inline cx_##SUF conj_##SUF(cx_##SUF v) { cx_##SUF r = {v.re, -v.im}; return r; } \
+    static void bfly4i_##SUF(cx_##SUF* buf) {                                                \
+        cx_##SUF v0 = buf[0], v1 = buf[1], v2 = buf[2], v3 = buf[3];                         \
+        bfly2_##SUF(&v0, &v2); bfly2_##SUF(&v1, &v3);                                        \
+        v3 = rot90i_##SUF(v3);                                                               \
+        bfly2_##SUF(&v0, &v1); bfly2_##SUF(&v2, &v3);                                        \
+        buf[0] = v0; buf[1] = v2; buf[2] = v1; buf[3] = v3; }                                \
+    static void bfly8i_##SUF(cx_##SUF* buf, cx_##SUF w1, cx_##SUF w3) {                      \
+        cx_##SUF s[8] = {buf[0], buf[2], buf[4], buf[6], buf[1], buf[3], buf[5], buf[7]};    \
+        bfly4i_##SUF(s); bfly4i_##SUF(s + 4);                                                \
+        s[5] = cmul_##SUF(s[5], w1); s[6] = rot90i_##SUF(s[6]); s[7] = cmul_##SUF(s[7], w3); \
+        for (int i = 0; i < 4; ++i) bfly2_##SUF(&s[i], &s[i + 4]);                           \
+        for (int i = 0; i < 8; ++i) buf[i] = s[i]; }                                         \
+    static void cifft_tab_##SUF(const cx_##SUF* in, size_t len, cx_##SUF* out,               \
+                                const cx_##SUF* tw, const cx_##SUF* w8) {                    \
+        if (len == 1) { out[0] = in[0]; return; }                                            \
+        if (len == 2) { out[0] = in[0]; out[1] = in[1]; bfly2_##SUF(&out[0], &out[1]); return; } \
+        if (len == 4) { memcpy(out, in, 4 * sizeof(cx_##SUF)); bfly4i_##SUF(out); return; }  \
+        prepare_radix4_##SUF(len, in, out, 1);                                               \
+        unsigned bits = 0; while (((size_t)1 << bits) < len) ++bits;                         \
+        size_t cur;                                                                          \
+        if (bits % 2 == 0) { for (size_t c = 0; c < len; c += 4) bfly4i_##SUF(out + c); cur = 16; } \
+        else {                                                                               \
+            const cx_##SUF w1 = conj_##SUF(w8[0]), w3 = conj_##SUF(w8[1]);                   \
+            for (size_t c = 0; c < len; c += 8) bfly8i_##SUF(out + c, w1, w3);               \
+            cur = 32;                                                                        \
+        }                                                                                    \
+        for (; cur <= len; cur *= 4) {                                                       \
+            size_t q = cur / 4, tstride = len / cur;                                         \
+            for (size_t row = 0; row < len / cur; ++row) {                                   \
+                cx_##SUF* d = out + row * cur;                                               \
+                for (size_t j = 0; j < q; ++j) { /* rustfft butterfly_4, inverse */          \
+                    cx_##SUF s0 = cmul_##SUF(d[j + q], conj_##SUF(tw[j * 1 * tstride]));     \
+                    cx_##SUF s1 = cmul_##SUF(d[j + 2 * q], conj_##SUF(tw[j * 2 * tstride])); \
+                    cx_##SUF s2 = cmul_##SUF(d[j + 3 * q], conj_##SUF(tw[j * 3 * tstride])); \
+                    cx_##SUF s5 = csub_##SUF(d[j], s1);                                      \
+                    d[j] = cadd_##SUF(d[j], s1);                                             \
+                    cx_##SUF s3 = cadd_##SUF(s0, s2);                                        \
+                    cx_##SUF s4 = csub_##SUF(s0, s2);                                        \
+                    d[j + 2 * q] = csub_##SUF(d[j], s3);                                     \
+                    d[j] = cadd_##SUF(d[j], s3);                                             \
+                    d[j + q].re = s5.re - s4.im; d[j + q].im = s5.im + s4.re;                \
+                    d[j + 3 * q].re = s5.re + s4.im; d[j + 3 * q].im = s5.im - s4.re;        \
+                }                                                                            \
+            }                                                                                \
+        }                                                                                    \
+    }                                                                                        \
+    /* realfft.rs:167-241 InvRealFFT::new + process: in [n/2+1] complex, out [n] real */    \
+    int or_irfft_##SUF(const T* in, size_t n, T* out) {                                      \
+        plan_##SUF* p = plan_new_##SUF(n);                                                   \
+        if (!p) return -1;                                                                   \
+        const size_t half = p->half;                                                         \
+        const cx_##SUF* X = (const cx_##SUF*)in;                                             \
+        for (size_t k = 0; k < half; ++k) { /* realfft.rs:210-219 (zip4 over rev) */         \
+            T s = p->sn[k], c = p->cs[k];                                                    \
+            cx_##SUF b = X[k], r = X[half - k];                                              \
+            p->buf[k].re = (T)0.5 * (((b.re + r.re) - c * (b.im + r.im)) - s * (b.re - r.re)); \
+            p->buf[k].im = (T)0.5 * (((b.im - r.im) + c * (b.re - r.re)) - s * (b.im + r.im)); \
+        }                                                                                    \
+        cifft_tab_##SUF(p->buf, half, (cx_##SUF*)out, p->tw, p->w8); /* realfft.rs:225-230 */ \
+        plan_free_##SUF(p);                                                                  \
+        return 0;                                                                            \
+    }                                                                                        \
     /* one RealFFT::new per call (the reference's per-frame re-plan, lib.rs:455) */          \
     int or_rfft_##SUF(const T* in, size_t n, T* out) {                                       \
         plan_##SUF* p = plan_new_##SUF(n);                                                   \

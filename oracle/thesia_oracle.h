@@ -44,6 +44,8 @@ int or_cfft_radix4_f64(const double* in, size_t len, double* out);
 /* RealFFT::process (realfft.rs:105-159). in: n reals (n even), out: (n/2+1) complex. */
 int or_rfft_f32(const float* in, size_t n, float* out);
 int or_rfft_f64(const double* in, size_t n, double* out);
+int or_irfft_f32(const float* in, size_t n, float* out);   /* realfft.rs:167-241 InvRealFFT */
+int or_irfft_f64(const double* in, size_t n, double* out);
 /* RealFFT::new sin_cos table (realfft.rs:85-93): out[2k]=sin, out[2k+1]=cos, k<n/2. */
 void or_rfft_sin_cos_f32(size_t n, float* out);
 

@@ -37,6 +37,8 @@ def lib():
             "or_cfft_radix4_f64": (C.c_int, [_f64p, _sz, _f64p]),
             "or_rfft_f32": (C.c_int, [_f32p, _sz, _f32p]),
             "or_rfft_f64": (C.c_int, [_f64p, _sz, _f64p]),
+            "or_irfft_f32": (C.c_int, [_f32p, _sz, _f32p]),
+            "or_irfft_f64": (C.c_int, [_f64p, _sz, _f64p]),
             "or_rfft_sin_cos_f32": (None, [_sz, _f32p]),
             "or_stft_n_frames": (_sz, [_sz, _sz, _sz]),
             "or_perform_stft_f32": (_sz, [_f32p, _sz, _sz, _sz, _sz, C.c_void_p, _f32p]),
@@ -133,6 +135,21 @@ def rfft(x, dtype=np.float32):
     if lib().or_rfft_f32(xin, n, out) != 0:
         raise ValueError("RealFFT length error")
     return out.view(np.complex64)
+
+
+def irfft(X, n, dtype=np.float32):
+    """InvRealFFT (realfft.rs:167-241): X [n/2+1] complex -> [n] real, unnormalised."""
+    if dtype == np.float64:
+        xin = np.ascontiguousarray(np.asarray(X, np.complex128)).view(np.float64)
+        out = np.empty(n, np.float64)
+        if lib().or_irfft_f64(xin, n, out) != 0:
+            raise ValueError("InvRealFFT length error")
+        return out
+    xin = np.ascontiguousarray(np.asarray(X, np.complex64)).view(np.float32)
+    out = np.empty(n, np.float32)
+    if lib().or_irfft_f32(xin, n, out) != 0:
+        raise ValueError("InvRealFFT length error")
+    return out
 
 
 def rfft_sin_cos(n):
