@@ -213,7 +213,7 @@ int thesia_grey_to_rgb(const float* grey, uint32_t width, uint32_t height, uint3
  * spectra of length/2+1 complex values (re, im interleaved f32) -> n_frames rows of `length`
  * reals, unnormalised (0.5 * Re of the full inverse DFT, the reference's complex_to_real test),
  * in the reference's operation order (rustfft 4.0 Radix4, inverse). length even
- * (THESIA_ERR_INVALID_ARG otherwise, "Length must be even") and a power of two <= 16384
+ * (THESIA_ERR_INVALID_ARG otherwise, "Length must be even") and a power of two <= 4096
  * (THESIA_ERR_UNSUPPORTED: Radix4 panics on other sizes). _device: HBM buffers, stream-ordered. */
 int thesia_inv_real_fft_device(const float* d_in, size_t n_frames, size_t length, float* d_out);
 int thesia_inv_real_fft(const float* in, size_t n_frames, size_t length, float* out);

@@ -960,7 +960,7 @@ int inv_real_fft_device(const float* d_in, size_t n_frames, size_t length, float
     if (length % 2) return set_error(THESIA_ERR_INVALID_ARG, "Length must be even (realfft.rs:171)");
     if (length < 2 || (length & (length - 1)))
         return set_error(THESIA_ERR_UNSUPPORTED, "Radix4 needs a power-of-two length/2 (the reference panics)");
-    if (length > (1u << 14)) return set_error(THESIA_ERR_UNSUPPORTED, "length above 16384");
+    if (length > 4096) return set_error(THESIA_ERR_UNSUPPORTED, "length above 4096 (the engine's n_fft range)");
     static std::mutex mu;
     static auto& plans = *new std::map<std::pair<int, size_t>, Plan*>();  // leaked, see dev_taps
     int dev = 0;

@@ -47,9 +47,13 @@ def test_resize_then_colormap_matches_reference_formula():
 
 @pytest.mark.parametrize("n,nw,nh,rng_amp", [(44100, 441, 200, (-1.0, 1.0)), (1000, 3000, 50, (-1.5, 1.5)),
                                              (48000 * 3, 300, 500, (-0.5, 0.5)), (777, 100, 64, (-2, 2))])
-def test_wav_to_image_exact_where_reference_does_not_panic(n, nw, nh, rng_amp):
+def test_wav_to_image_exact_and_panics_reported(n, nw, nh, rng_amp):
     rng = np.random.default_rng(n)
     wav = (np.sin(np.arange(n) * 0.01) * 0.4 + rng.normal(0, 0.05, n)).astype(np.float32)
-    got = display.wav_to_image(wav, nw, nh, rng_amp)
+    got, got_panic = display.wav_to_image(wav, nw, nh, rng_amp, return_panic=True)
     ref, panicked = O.wav_to_image(wav, nw, nh, *rng_amp)
+    assert got_panic == panicked  # THESIA_ERR_PANIC exactly where the reference panics
     assert np.array_equal(got, ref), int((got != ref).sum())
+    if panicked:
+        with pytest.raises(thesia.ThesiaError):
+            display.wav_to_image(wav, nw, nh, rng_amp)

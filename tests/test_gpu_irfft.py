@@ -11,7 +11,7 @@ from thesia.realfft import InvRealFFT
 pytestmark = pytest.mark.gpu
 
 
-@pytest.mark.parametrize("n", [2 ** k for k in range(1, 15)])
+@pytest.mark.parametrize("n", [2 ** k for k in range(1, 13)])
 def test_inv_real_fft_bit_exact(n):
     rng = np.random.default_rng(3 * n)
     frames = max(1, min(64, (1 << 16) // n))
@@ -39,3 +39,5 @@ def test_length_errors():
         InvRealFFT(12).process(np.zeros(7, np.complex64))
     with pytest.raises(ValueError):
         InvRealFFT(8).process(np.zeros(4, np.complex64))
+    with pytest.raises(thesia.ThesiaError):
+        InvRealFFT(8192).process(np.zeros(4097, np.complex64))  # beyond the engine's n_fft range
