@@ -171,21 +171,24 @@ class RenderPipeline:
         return out
 
     def display_bytes(self) -> dict:
-        """Algorithmic HBM bytes of one display pass (DESIGN.md §4 'Display roofline'): the dB
-        spectrogram read once (the per-track range + grey/vertical pass), the vertical pass's
-        f32 intermediate [T, nheight] written and read once, the RGB bytes written once."""
+        """HBM bytes of one display pass (DESIGN.md §4 'Display roofline'). `total` is the
+        algorithmic minimum: the dB spectrogram read once and the RGB bytes written once. The
+        separable resize's f32 intermediate [nheight, T] (image 0.23's vertical-then-horizontal
+        order) is an implementation's choice, reported apart as an upper bound (the fused path
+        neither forms nor reads the rows whose taps reach only the zero fill)."""
         spec = tmp = rgb = 0
         for i, t in enumerate(self.tracks):
             _, _, T, bins = self.where[i]
             spec += T * bins * 4
             tmp += T * self.nheight * 4
             rgb += self._geo[i] * self.nheight * 3
-        return {"spec_read": spec, "tmp_write_read": 2 * tmp, "rgb_write": rgb,
-                "total": spec + 2 * tmp + rgb}
+        return {"spec_read": spec, "rgb_write": rgb, "total": spec + rgb,
+                "intermediate_write_read_upper_bound": 2 * tmp}
 
     def display_timed(self, iters: int = 3) -> dict:
         """Device time of the display path (range + grey + Lanczos3 + colormap, no host copy),
-        HIP events on the library stream, and its HBM-roofline fraction."""
+        HIP events on the library stream, and its HBM-roofline fraction on the algorithmic
+        bytes (spectrogram read + RGB written once)."""
         engine.synchronize()
         self.render(want_rgb=False)  # warm (workspaces, tap tables)
         with engine.EventTimer() as tm:
@@ -195,7 +198,8 @@ class RenderPipeline:
         b = self.display_bytes()
         ach = b["total"] / (ms * 1e-3) / 1e9
         return {"bound": "hbm", "achieved": ach, "peak": 8000.0, "unit": "GB/s", "frac": ach / 8000.0,
-                "traffic": None, "display_ms": ms, "algorithmic_bytes": b,
+                "traffic": None, "traffic_note": "PMC per step in profiles/r02_display (FETCH/WRITE_SIZE)",
+                "display_ms": ms, "algorithmic_bytes": b,
                 "kernel": "per-track range + grey/vertical Lanczos3 + horizontal Lanczos3 + colormap"}
 
     def _pinned_host(self, g: int, total: int) -> np.ndarray:
