@@ -150,6 +150,14 @@ int launch_render_batch2(const float* spec, uint32_t bins, float max, float min,
                          uint32_t nw_max, uint32_t nh, int h_taps, int h_span, uint32_t v_band,
                          int v_rows, int v_kv, float* tmp, const uint8_t* cmap, uint8_t* rgb,
                          hipStream_t s);
+// The fully fused display (grey + vertical + horizontal Lanczos3 + colormap, the intermediate in
+// LDS only): a block = R output rows x 64 columns of one track; kt register taps (16/32/48) for
+// the horizontal pass, kv padded vertical taps, s_cap / g_cap the largest frame span / grey-row
+// span of a tile in the launch (host-computed). Same bytes as launch_render_batch2.
+int render_fused_lds_bytes(int R, int kv, int s_cap, int g_cap, int kt);
+int launch_render_fused(const float* spec, uint32_t bins, float max, float min, const RenderDesc* d_desc,
+                        uint32_t n, uint32_t nw_max, uint32_t nh, int kt, int R, int kv, int s_cap,
+                        int g_cap, const uint8_t* cmap, uint8_t* rgb, hipStream_t s);
 int launch_spec_to_grey(const float* spec, uint32_t T, uint32_t bins, uint32_t H, float max,
                         float min, float* grey, hipStream_t s);
 int launch_resize_v(const float* in, uint32_t w, uint32_t h, uint32_t nh, const int32_t* left,
