@@ -53,6 +53,7 @@ def parse():
     p.add_argument("--n-mels", type=int, default=128)
     p.add_argument("--output", choices=["mel_db", "amp_db", "power_db", "complex"], default="mel_db")
     p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--no-e2e", action="store_true", help="skip the PCIe-inclusive end-to-end sample")
     p.add_argument("--no-rfft-roofline", action="store_true",
                    help="skip the extra complex-output (window+rFFT kernel) roofline measurement")
     p.add_argument("--no-c1", action="store_true", help="skip the C1 (48 kHz sample, 1024/256) line")
@@ -414,6 +415,52 @@ def main_c5(args, ws, rank, pg, device):
     p.close()
 
 
+def end_to_end(args, plan, kind):
+    """PCIe-inclusive rate of the C4 path (H2D int16 + D2H), reported beside the
+    value, never as it: a sample of the shard's geometry as int16 PCM (the WAV encoding, 2 B per
+    sample) in page-locked host memory -> device -> the same fused kernel (s16 input) -> rows
+    back into page-locked host memory, timed over 3 passes after one warm pass."""
+    import ctypes as C
+    import numpy as np
+    from thesia import engine
+    from thesia._lib import lib, check
+    n_tr = min(100, args.tracks)
+    n_samples = int(round(args.seconds * args.sr))
+    host = np.empty(n_tr * n_samples * args.channels, np.int16)
+    for t in range(n_tr):
+        host[t * n_samples * args.channels:(t + 1) * n_samples * args.channels] = \
+            engine.synth_pcm_host(args.channels, t, n_samples, args.sr).reshape(-1)
+    offs = np.arange(n_tr, dtype=np.uint64) * (n_samples * args.channels)
+    lens = np.full(n_tr, n_samples, np.uint64)
+    frames = engine.Batch.frames_for(plan, lens)
+    out = np.empty(frames * plan.row_bins * (8 if kind == engine.OUT_COMPLEX else 4), np.uint8)
+    for a in (host, out):
+        check(lib.thesia_host_register(a.ctypes.data_as(C.c_void_p), a.nbytes))
+    din = engine.DeviceBuffer(host.nbytes)
+    dout = engine.DeviceBuffer(out.nbytes)
+    b = engine.Batch(plan, din, offs, lens, dout, input_format=engine.IN_S16, channels=args.channels)
+
+    def one():
+        check(lib.thesia_memcpy_h2d(din.ptr, host.ctypes.data_as(C.c_void_p), host.nbytes))
+        b.run()
+        check(lib.thesia_memcpy_d2h(out.ctypes.data_as(C.c_void_p), dout.ptr, out.nbytes))
+
+    one()
+    engine.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(3):
+        one()
+    engine.synchronize()
+    dt = (time.perf_counter() - t0) / 3
+    b.close()
+    for a in (host, out):
+        lib.thesia_host_unregister(a.ctypes.data_as(C.c_void_p))
+    return {"frames_per_s": frames / dt, "ms_per_pass": dt * 1e3, "frames": frames,
+            "h2d_bytes": host.nbytes, "d2h_bytes": out.nbytes,
+            "sample": f"{n_tr} tracks of the shard geometry, int16 PCM in page-locked host memory "
+                      f"(H2D {host.nbytes / 1e9:.2f} GB + kernel + D2H {out.nbytes / 1e9:.2f} GB)"}
+
+
 def main_worker(args):
     ws, rank, local, pg = dist_setup()
     if args.selftest:
@@ -553,6 +600,8 @@ def main_worker(args):
             result["cpu_baseline"] = cpu_baseline(args, n_samples)
         if ws == 1 and not args.no_c1:
             result["c1"] = c1_line(args)
+        if ws == 1 and not args.no_e2e:
+            result["end_to_end_pcie"] = end_to_end(args, plan, kind)
         print(json.dumps(result), flush=True)
     batch.close()
     if pg is not None:

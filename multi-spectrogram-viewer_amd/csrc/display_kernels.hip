@@ -30,6 +30,9 @@
 #ifndef THESIA_HKT_MAX
 #define THESIA_HKT_MAX 48  // horizontal pass: most taps held in registers
 #endif
+#ifndef THESIA_H_DIRECT
+#define THESIA_H_DIRECT 1  // horizontal pass: RGB bytes stored lane by lane (no LDS assembly)
+#endif
 #ifndef THESIA_H_2ROW
 #define THESIA_H_2ROW 1  // horizontal pass: two rows per block step
 #endif
@@ -538,7 +541,9 @@ __global__ void __launch_bounds__(256) resize_h_rgb_batch_kernel(uint32_t nh, co
         // two rows per step (y and y + G): two independent sum chains per column over the
         // same weights, both rows' spans prefetched a step ahead
         float* rin1 = reinterpret_cast<float*>(cm + 32);
+#if !THESIA_H_DIRECT
         uint8_t* seg1 = reinterpret_cast<uint8_t*>(rin1 + span_cap + KT);
+#endif
         for (int k = tid; k < span_cap + KT; k += 256) rin1[k] = 0.0f;
         const uint32_t G = gridDim.y;
         float nx1[kHPf];
@@ -581,13 +586,29 @@ __global__ void __launch_bounds__(256) resize_h_rgb_batch_kernel(uint32_t nh, co
                         t1 += rin1[base + i] * wi;
                     }
                 }
+#if THESIA_H_DIRECT
+                // RGB bytes straight to HBM (three byte stores per pixel: a wave's 192 bytes are
+                // contiguous, L2 merges them), no LDS assembly and one barrier less per step
+                uint8_t px[6];
+                colormap_px(t0, cm, px);
+                colormap_px(t1, cm, px + 3);
+                uint8_t* g0 = rgb + r.rgb_off + ((uint64_t)y * r.nw + ox) * 3;
+                g0[0] = px[0]; g0[1] = px[1]; g0[2] = px[2];
+                if (two) {
+                    uint8_t* g1 = g0 + (uint64_t)G * r.nw * 3;
+                    g1[0] = px[3]; g1[1] = px[4]; g1[2] = px[5];
+                }
+#else
                 colormap_px(t0, cm, seg + 3 * tid);
                 colormap_px(t1, cm, seg1 + 3 * tid);
+#endif
             }
             __syncthreads();
+#if !THESIA_H_DIRECT
             store_row(y, seg);
             if (two) store_row(y + G, seg1);
             __syncthreads();
+#endif
         }
         return;
     }
