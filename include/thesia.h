@@ -188,9 +188,18 @@ typedef enum {
     /* 1 = the other output-row store method of the streaming kernel (LDS-staged 16-byte stores
      * for complex rows / lane-wise stores for linear rows; stft3_kernel at n_fft 2048 stereo
      * f32 only) */
-    THESIA_BATCH_OPT_ROW_STORE = 3
+    THESIA_BATCH_OPT_ROW_STORE = 3,
+    /* a device buffer of 3 int32 per track (value = its address, 0 = off): every run also
+     * leaves each track's max / min over its output rows and a NaN flag there (the per-track
+     * reduction of update_spec_greys, lib.rs:194-207), folded into the streaming kernel's row
+     * epilogue for the linear kinds, else one pass over the rows; read with
+     * thesia_batch_ranges_read. Real output kinds only. */
+    THESIA_BATCH_OPT_RANGE = 4
 } thesia_batch_option;
 int thesia_batch_set_option(thesia_batch* batch, int option, int64_t value);
+/* Decode n tracks' range slots (THESIA_BATCH_OPT_RANGE buffer, device) after the runs that
+ * wrote them: max / min per track (ndarray-stats: -inf / +inf for an empty track), has_nan. */
+int thesia_batch_ranges_read(const void* d_range, size_t n, float* max, float* min, int* has_nan);
 
 /* Deterministic synthetic PCM (int16-quantised chirp + noise) written on the device, and
  * its bit-identical host twin. format: thesia_input_format. Layout [track][sample][ch]. */

@@ -444,6 +444,13 @@ int thesia_render_rgb_batch_device(const float* d_spec, const uint64_t* row0, si
     GUARD_END
 }
 
+int thesia_batch_ranges_read(const void* d_range, size_t n, float* max, float* min, int* has_nan) {
+    GUARD_BEGIN
+    if (n && (!d_range || !max || !min || !has_nan)) return set_error(THESIA_ERR_INVALID_ARG, "null pointer");
+    return ranges_read(static_cast<const int*>(d_range), n, max, min, has_nan, default_stream());
+    GUARD_END
+}
+
 int thesia_minmax_segments_multi(size_t n_groups, const float* const* d_specs,
                                  const uint64_t* const* row0s, const size_t* bins, const size_t* ns,
                                  float* max, float* min, int* has_nan) {

@@ -144,6 +144,57 @@ int launch_decode_downmix(const void* raw, int kind, float scale, int channels, 
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
+// per-track output ranges for Batch::range (the kernels without the in-epilogue accumulation)
+__global__ void range_init_kernel(int* r, uint64_t n) {
+    const uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
+    if (i < n) {
+        r[3 * i] = range_ord(-INFINITY);
+        r[3 * i + 1] = range_ord(INFINITY);
+        r[3 * i + 2] = 0;
+    }
+}
+
+int launch_range_init(int* range, uint64_t n_tracks, hipStream_t s) {
+    if (n_tracks == 0) return 0;
+    hipLaunchKernelGGL(range_init_kernel, dim3((unsigned)((n_tracks + 255) / 256)), dim3(256), 0, s, range,
+                       n_tracks);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+__global__ void __launch_bounds__(256) range_rows_kernel(const float* out, const uint64_t* frame0,
+                                                         uint32_t row_floats, int* range) {
+    const uint64_t t = blockIdx.y;
+    const uint64_t beg = frame0[t] * row_floats, end = frame0[t + 1] * row_floats;
+    float mx = -INFINITY, mn = INFINITY;
+    int nan = 0;
+    for (uint64_t i = beg + blockIdx.x * 256ull + threadIdx.x; i < end; i += gridDim.x * 256ull) {
+        const float v = out[i];
+        mx = fmaxf(mx, v);
+        mn = fminf(mn, v);
+        nan |= v != v;
+    }
+#pragma unroll
+    for (int m = 32; m >= 1; m >>= 1) {
+        mx = fmaxf(mx, __shfl_xor(mx, m));
+        mn = fminf(mn, __shfl_xor(mn, m));
+        nan |= __shfl_xor(nan, m);
+    }
+    if ((threadIdx.x & 63) == 0) {
+        atomicMax(range + 3 * t, range_ord(mx));
+        atomicMin(range + 3 * t + 1, range_ord(mn));
+        if (nan) atomicOr(range + 3 * t + 2, 1);
+    }
+}
+
+int launch_range_rows(const float* out, const uint64_t* d_frame0, uint64_t n_tracks, uint32_t row_floats,
+                      int* range, hipStream_t s) {
+    if (n_tracks == 0) return 0;
+    if (n_tracks > 65535) return -2;
+    hipLaunchKernelGGL(range_rows_kernel, dim3(32, (unsigned)n_tracks), dim3(256), 0, s, out, d_frame0,
+                       row_floats, range);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
 // ------------------------------------------------------------------------------------
 // K3 per-track max/min (NaN -> flag)
 // ------------------------------------------------------------------------------------

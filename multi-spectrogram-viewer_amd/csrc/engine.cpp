@@ -543,6 +543,11 @@ int batch_set_option(Batch* b, int option, int64_t value) {
             b->launch.stamps = reinterpret_cast<unsigned long long*>(value);
             return THESIA_OK;
 #endif
+        case THESIA_BATCH_OPT_RANGE:
+            if (value != 0 && b->launch.out_kind == OUT_COMPLEX)
+                return set_error(THESIA_ERR_INVALID_ARG, "ranges need real output rows");
+            b->range = reinterpret_cast<int*>(value);
+            return THESIA_OK;
         case THESIA_BATCH_OPT_ROW_STORE:
             if (value < 0 || value > 1) return set_error(THESIA_ERR_INVALID_ARG, "row_store must be 0 or 1");
             b->launch.row_alt = (int)value;
@@ -554,19 +559,51 @@ int batch_set_option(Batch* b, int option, int64_t value) {
 
 int batch_run(Batch* b, hipStream_t s) {
     if (!s) s = default_stream();
+    // per-track output ranges: folded into stft3's staged-row epilogue (linear kinds), else one
+    // reduction pass over the rows after the spectrogram launch
+    const uint64_t n_tr = b->frame0.empty() ? 0 : b->frame0.size() - 1;
+    const bool lin = b->launch.out_kind != OUT_COMPLEX && b->launch.out_kind != OUT_MEL &&
+                     b->launch.out_kind != OUT_MEL_AMP_DB;
+    bool in_kernel = false;
+    if (b->range && launch_range_init(b->range, n_tr, s))
+        return set_error(THESIA_ERR_DEVICE, "range init launch failed");
     int rc = -2;
     if (b->kernel == 9) {
         rc = launch_stftx(b->launch, s);
         if (rc) return set_error(rc == -2 ? THESIA_ERR_UNSUPPORTED : THESIA_ERR_DEVICE, "stftx launch failed");
-        return THESIA_OK;
+    } else {
+        if (b->kernel == 5) rc = launch_stft5(b->launch, s);
+        if (rc == -2 && b->kernel >= 3) {
+            const bool fold = b->range && lin && b->launch.row_alt == 0;
+            b->launch.trk_range = fold ? b->range : nullptr;
+            rc = launch_stft3(b->launch, s);
+            in_kernel = fold && rc == 0;
+            b->launch.trk_range = nullptr;
+        }
+        if (rc == -2 && b->kernel >= 2) rc = launch_stft2(b->launch, s);
+        if (rc == -2) rc = launch_stft(b->launch, s);
+        if (rc == -2) return set_error(THESIA_ERR_UNSUPPORTED, "unsupported n_fft");
+        if (rc) return set_error(THESIA_ERR_DEVICE, std::string("stft launch failed: ") +
+                                                        hipGetErrorString(hipGetLastError()));
     }
-    if (b->kernel == 5) rc = launch_stft5(b->launch, s);
-    if (rc == -2 && b->kernel >= 3) rc = launch_stft3(b->launch, s);
-    if (rc == -2 && b->kernel >= 2) rc = launch_stft2(b->launch, s);
-    if (rc == -2) rc = launch_stft(b->launch, s);
-    if (rc == -2) return set_error(THESIA_ERR_UNSUPPORTED, "unsupported n_fft");
-    if (rc) return set_error(THESIA_ERR_DEVICE, std::string("stft launch failed: ") +
-                                                    hipGetErrorString(hipGetLastError()));
+    if (b->range && !in_kernel &&
+        launch_range_rows(static_cast<const float*>(b->desc.d_output), b->d_frame0.as<uint64_t>(), n_tr,
+                          (uint32_t)b->plan->row_bins(), b->range, s))
+        return set_error(THESIA_ERR_DEVICE, "range launch failed");
+    return THESIA_OK;
+}
+
+// host side of Batch::range: {ord max, ord min, NaN} -> (max, min, NaN) per track
+int ranges_read(const int* d_range, size_t n, float* mx, float* mn, int* nan, hipStream_t s) {
+    if (n == 0) return THESIA_OK;
+    std::vector<int> h(3 * n);
+    THESIA_HIP(hipMemcpyAsync(h.data(), d_range, h.size() * sizeof(int), hipMemcpyDeviceToHost, s));
+    THESIA_HIP(hipStreamSynchronize(s));
+    for (size_t i = 0; i < n; ++i) {
+        mx[i] = range_unord(h[3 * i]);
+        mn[i] = range_unord(h[3 * i + 1]);
+        nan[i] = h[3 * i + 2];
+    }
     return THESIA_OK;
 }
 

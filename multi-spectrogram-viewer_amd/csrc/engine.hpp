@@ -95,11 +95,13 @@ struct Batch {
         return k5_ok && mel ? 5 : k3_ok ? 3 : plan->use_v2 ? 2 : 1;
     }
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
+    int* range = nullptr;  // THESIA_BATCH_OPT_RANGE: per-track {ord max, ord min, NaN} on the device
     ~Batch();
 };
 int batch_create(Plan* plan, const thesia_batch_desc& d, Batch** out);
 int batch_run(Batch* b, hipStream_t s);
 int batch_set_option(Batch* b, int option, int64_t value);  // thesia_batch_set_option
+int ranges_read(const int* d_range, size_t n, float* mx, float* mn, int* nan, hipStream_t s);
 
 // display path selection (thesia_set_render_path): 0 fused batched launches (grey + vertical
 // in one pass, then horizontal + colormap), 1 per-track launches, 2 three-stage batched

@@ -82,7 +82,26 @@ struct StftLaunch {
     const float* xmel_w = nullptr;
     // diagnostic builds only (-DTHESIA_STAMPS, scripts/stamps.py): per-wave phase cycle sums
     unsigned long long* stamps = nullptr;
+    // per-track range of the output rows (update_spec_greys' max / min, lib.rs:194-207),
+    // accumulated in the epilogue of the kernels that support it: 3 ints per track
+    // {ordered max, ordered min, NaN seen} (range_ord below); null = off
+    int* trk_range = nullptr;
 };
+
+// f32 <-> int32 with the order of the floats (max / min by integer atomics); NaN excluded
+__host__ __device__ inline int range_ord(float x) {
+    const int b = __builtin_bit_cast(int, x);
+    return b >= 0 ? b : b ^ 0x7FFFFFFF;
+}
+__host__ __device__ inline float range_unord(int o) {
+    return __builtin_bit_cast(float, o >= 0 ? o : o ^ 0x7FFFFFFF);
+}
+// trk_range slots set to {ord(-inf), ord(+inf), 0}
+int launch_range_init(int* range, uint64_t n_tracks, hipStream_t s);
+// the range of each track's rows [frame0[t] * row_floats, frame0[t+1] * row_floats) of `out`
+// (for the kernels without the in-epilogue accumulation)
+int launch_range_rows(const float* out, const uint64_t* d_frame0, uint64_t n_tracks, uint32_t row_floats,
+                      int* range, hipStream_t s);
 
 // Returns 0 on success, -2 for an unsupported n_fft.
 int launch_stft(const StftLaunch& a, hipStream_t stream);

@@ -98,6 +98,27 @@ stft3_kernel(StftLaunch a, uint64_t fps) {
     // the stream's current track, cached across frames (looked up again only past its end)
     uint64_t g_beg = 1, g_end = 0, base = 0;
     int64_t n = 0;
+    // per-track range of the rows this stream writes (a.trk_range: linear kinds, staged rows),
+    // committed with one atomic triple per track the stream leaves
+    float r_max = -INFINITY, r_min = INFINITY;
+    int r_nan = 0, r_trk = -1;
+    auto r_flush = [&]() {
+#pragma unroll
+        for (int m = L / 2; m >= 1; m >>= 1) {  // the frame's L lanes (xor stays inside the group)
+            r_max = fmaxf(r_max, __shfl_xor(r_max, m));
+            r_min = fminf(r_min, __shfl_xor(r_min, m));
+            r_nan |= __shfl_xor(r_nan, m);
+        }
+        if (j == 0) {
+            int* rp = a.trk_range + 3 * r_trk;
+            atomicMax(rp, range_ord(r_max));
+            atomicMin(rp + 1, range_ord(r_min));
+            if (r_nan) atomicOr(rp + 2, 1);
+        }
+        r_max = -INFINITY;
+        r_min = INFINITY;
+        r_nan = 0;
+    };
     for (uint64_t it = 0; it < fps; ++it) {  // wave-uniform trip count
         MARK(top);
         // wave priority phases (measured): loads / window / FFT at priority 0,
@@ -239,12 +260,25 @@ stft3_kernel(StftLaunch a, uint64_t fps) {
             float* frow = static_cast<float*>(a.out) + g * F;
             const int sh = (int)((reinterpret_cast<uintptr_t>(frow) >> 2) & 3);
             float* st = region + sh;
+            const bool rng = a.trk_range != nullptr;  // uniform
+            if (rng) {
+                const int t = valid ? hint : -1;
+                if (t != r_trk) {  // uniform over the frame's lanes
+                    if (r_trk >= 0) r_flush();
+                    r_trk = t;
+                }
+            }
             untangle2<NC, kBatch>(v, j, partner, ub, [&](int k, float xr, float xi) {
                 const float p2 = __builtin_fmaf(xr, xr, xi * xi);
                 float val = power ? p2 : __builtin_amdgcn_sqrtf(p2);
                 if (db) val = power ? db_of(val, a.log_amin, 1e-36f, 10.0f)
                                     : db_of(val, a.log_amin, 1e-18f, 20.0f);
                 st[k] = val;
+                if (rng) {
+                    r_max = fmaxf(r_max, val);
+                    r_min = fminf(r_min, val);
+                    r_nan |= val != val;
+                }
             });
             wave_lds_sync();
             if (valid) store_row_b128<L>(frow, sh, region, F, j);
@@ -268,6 +302,7 @@ stft3_kernel(StftLaunch a, uint64_t fps) {
             }
         }
     }
+    if (r_trk >= 0) r_flush();  // (a.trk_range set: the stream's last track)
 }
 
 // --------------------------------------------------------------------------------------

@@ -88,6 +88,7 @@ _SIGS = {
     "thesia_wav_to_image": (_i, [_fp, _sz, _u32, _u32, _f, _f, _u8p, _sz]),
     "thesia_batch_kernel": (_i, [_vp, C.POINTER(C.c_int)]),
     "thesia_batch_set_option": (_i, [_vp, _i, C.c_int64]),
+    "thesia_batch_ranges_read": (_i, [C.c_void_p, _sz, _fp, _fp, C.POINTER(C.c_int)]),
     "thesia_set_render_path": (_i, [_i]),
     "thesia_minmax_device": (_i, [C.c_void_p, C.c_uint64, C.POINTER(C.c_float), C.POINTER(C.c_float),
                                   C.POINTER(C.c_int)]),

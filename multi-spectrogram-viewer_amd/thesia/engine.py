@@ -11,7 +11,7 @@ from ._lib import lib, check, PlanDesc, BatchDesc, _fp, _u64p
 
 OUT_COMPLEX, OUT_MAG, OUT_POWER, OUT_AMP_DB, OUT_POWER_DB, OUT_MEL, OUT_MEL_AMP_DB = range(7)
 IN_F32, IN_S16 = 0, 1
-OPT_KERNEL, OPT_MAX_BLOCKS, OPT_ROW_STORE = 1, 2, 3
+OPT_KERNEL, OPT_MAX_BLOCKS, OPT_ROW_STORE, OPT_RANGE = 1, 2, 3, 4
 
 
 def device_count() -> int:
@@ -215,6 +215,18 @@ class Batch:
             self.close()
         except Exception:
             pass
+
+
+def ranges_read(d_range: "DeviceBuffer", n: int, offset_tracks: int = 0):
+    """THESIA_BATCH_OPT_RANGE slots of n tracks -> (max, min, has_nan) arrays (one readback)."""
+    mx = np.empty(n, np.float32)
+    mn = np.empty(n, np.float32)
+    nan = np.empty(n, np.int32)
+    check(lib.thesia_batch_ranges_read(C.c_void_p(d_range.ptr.value + 12 * offset_tracks), n,
+                                       mx.ctypes.data_as(C.POINTER(C.c_float)),
+                                       mn.ctypes.data_as(C.POINTER(C.c_float)),
+                                       nan.ctypes.data_as(C.POINTER(C.c_int))))
+    return mx, mn, nan
 
 
 def set_render_path(path: int) -> None:

@@ -104,6 +104,13 @@ class RenderPipeline:
         self._off = np.concatenate([[0], np.cumsum(self._sizes)[:-1]]).astype(np.uint64)
         self._rgb_total = int(self._sizes.sum())
         self._rgb = engine.DeviceBuffer(max(self._rgb_total, 1))
+        # per-track dB ranges left by the spectrogram launches themselves (Batch range option,
+        # folded into the streaming kernel's row epilogue): 3 int32 per track, call order
+        self._d_range = engine.DeviceBuffer(12 * max(len(self._order), 1))
+        t0 = 0
+        for (_, _, _, b), ntr in zip(self.groups, self._c_ns):
+            b.set_option(engine.OPT_RANGE, self._d_range.ptr.value + 12 * t0)
+            t0 += ntr
         self._up = {}  # max_sr -> up_ratio per track (call order)
         self._max_sr = max((t.sr for t in self.tracks), default=0)
 
@@ -118,15 +125,9 @@ class RenderPipeline:
 
     def _range_arrays(self):
         """(max, min) dB per track in call order (group order), NaN-holding tracks as -inf /
-        +inf (ndarray-stats max/min error on NaN -> unwrap_or, lib.rs:198-199): one segmented
-        reduction over every group in one library call (one synchronisation)."""
-        n = len(self._order)
-        mx = np.empty(n, np.float32)
-        mn = np.empty(n, np.float32)
-        nan = np.empty(n, np.int32)
-        check(lib.thesia_minmax_segments_multi(len(self.groups), self._c_specs, self._c_row0, self._c_bins,
-                                               self._c_ns, mx.ctypes.data_as(_fp), mn.ctypes.data_as(_fp),
-                                               nan.ctypes.data_as(C.POINTER(C.c_int))))
+        +inf (ndarray-stats max/min error on NaN -> unwrap_or, lib.rs:198-199): the ranges the
+        last run_spectrograms() left (one readback)."""
+        mx, mn, nan = engine.ranges_read(self._d_range, len(self._order))
         bad = nan != 0
         return np.where(bad, -np.inf, mx.astype(np.float64)), np.where(bad, np.inf, mn.astype(np.float64))
 
@@ -223,6 +224,7 @@ class RenderPipeline:
             plan.close()
         self.groups = []
         self._rgb.close()
+        self._d_range.close()
 
 
 def render_tracks(tracks: Sequence[Track], px_per_sec: float = 100.0, nheight: int = 500,

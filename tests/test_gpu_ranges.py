@@ -1,0 +1,50 @@
+"""Batch range option (THESIA_BATCH_OPT_RANGE): per-track max / min of the output rows
+(update_spec_greys' reduction, lib.rs:194-207) left by the spectrogram launch itself -- folded
+into stft3's staged-row epilogue for the linear kinds, one pass over the rows otherwise -- must
+equal numpy's max / min of the rows the same launch wrote, for ragged tracks, every kernel and
+several frame-stream splits (max_blocks: streams crossing track boundaries)."""
+import numpy as np
+import pytest
+
+from thesia import engine
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.mark.parametrize("kind", [engine.OUT_AMP_DB, engine.OUT_POWER_DB, engine.OUT_MAG, engine.OUT_MEL_AMP_DB])
+@pytest.mark.parametrize("n_fft", [256, 1024, 2048])
+@pytest.mark.parametrize("kernel,max_blocks", [(0, 0), (0, 3), (1, 0), (2, 0)])
+def test_batch_ranges_equal_row_reduction(kind, n_fft, kernel, max_blocks):
+    rng = np.random.default_rng(n_fft + kind)
+    lens = [n_fft * 3 + 17, n_fft * 40 + 5, n_fft + 1, n_fft * 11 + 300, n_fft * 2]
+    ch = 2
+    tracks = [(rng.standard_normal((n, ch)) * np.float32(10.0) ** rng.uniform(-5, 0)).astype(np.float32)
+              for n in lens]
+    flat = np.concatenate([t.reshape(-1) for t in tracks])
+    offs = np.cumsum([0] + [t.size for t in tracks[:-1]]).astype(np.uint64)
+    plan = engine.Plan(n_fft, n_fft, n_fft // 4, kind, sr=48000, n_mels=64 if kind == engine.OUT_MEL_AMP_DB else 0)
+    T = engine.Batch.frames_for(plan, lens)
+    din = engine.DeviceBuffer.from_host(flat)
+    dout = engine.DeviceBuffer(T * plan.row_bins * 4)
+    b = engine.Batch(plan, din, offs, lens, dout, input_format=engine.IN_F32, channels=ch, fold_mono=True,
+                     kernel=kernel, max_blocks=max_blocks)
+    drange = engine.DeviceBuffer(12 * len(lens))
+    b.set_option(engine.OPT_RANGE, drange.ptr.value)
+    for _ in range(2):  # the slots are re-initialised by every run
+        b.run()
+    engine.synchronize()
+    mx, mn, nan = engine.ranges_read(drange, len(lens))
+    rows = dout.to_host(np.float32, (T, plan.row_bins))
+    for i in range(len(lens)):
+        r = rows[int(b.frame0[i]):int(b.frame0[i + 1])]
+        assert not nan[i]
+        assert mx[i] == r.max() and mn[i] == r.min(), (i, kernel, mx[i], r.max(), mn[i], r.min())
+
+
+def test_range_option_rejects_complex_rows():
+    plan = engine.Plan(512, 512, 128, engine.OUT_COMPLEX, sr=48000)
+    din = engine.DeviceBuffer(4 * 4096)
+    dout = engine.DeviceBuffer(8 * 257 * 64)
+    b = engine.Batch(plan, din, np.zeros(1, np.uint64), [4096], dout)
+    with pytest.raises(Exception):
+        b.set_option(engine.OPT_RANGE, 1 << 20)
