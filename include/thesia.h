@@ -265,6 +265,9 @@ int thesia_render_rgb_batch_device(const float* d_spec, const uint64_t* row0, si
                                    uint32_t nheight, float max, float min, uint8_t* d_rgb,
                                    const uint64_t* rgb_off);
 
+/* The _device display entries are stream-ordered on the library stream: they return once
+ * their launches are enqueued, and every later library call (thesia_memcpy_d2h included) sees
+ * their results. thesia_memcpy_h2d / _d2h are blocking and ordered after all enqueued work. */
 /* Several geometry groups in one call (group k: spectrogram buffer d_specs[k] of bins[k]
  * floats per row, ns[k] tracks with row table row0s[k] of ns[k]+1 entries); the per-track
  * arrays (max/min/has_nan out; up_ratio, nwidth, rgb_off in) are concatenated in group order.

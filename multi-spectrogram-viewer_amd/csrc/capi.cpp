@@ -67,11 +67,11 @@ int thesia_device_free(void* ptr) {
     return THESIA_OK;
 }
 int thesia_memcpy_h2d(void* dst, const void* src, size_t bytes) {
-    THESIA_HIP(hipMemcpy(dst, src, bytes, hipMemcpyHostToDevice));
+    THESIA_HIP(copy_ordered(dst, src, bytes, hipMemcpyHostToDevice));
     return THESIA_OK;
 }
 int thesia_memcpy_d2h(void* dst, const void* src, size_t bytes) {
-    THESIA_HIP(hipMemcpy(dst, src, bytes, hipMemcpyDeviceToHost));
+    THESIA_HIP(copy_ordered(dst, src, bytes, hipMemcpyDeviceToHost));
     return THESIA_OK;
 }
 int thesia_host_register(void* host, size_t bytes) {
@@ -215,7 +215,7 @@ int thesia_perform_stft(const float* input, size_t n, size_t win, size_t hop, si
     if (!rc) rc = batch_run(b, default_stream());
     if (!rc) {
         hipError_t e = hipStreamSynchronize(default_stream());
-        if (e == hipSuccess) e = hipMemcpy(out, dout.p, (size_t)T * F * 8, hipMemcpyDeviceToHost);
+        if (e == hipSuccess) e = copy_ordered(out, dout.p, (size_t)T * F * 8, hipMemcpyDeviceToHost);
         if (e != hipSuccess) rc = set_error(THESIA_ERR_DEVICE, hipGetErrorString(e));
     }
     delete b;
@@ -368,7 +368,7 @@ int thesia_spec_to_grey(const float* spec, size_t T, size_t bins, float up_ratio
     if (launch_spec_to_grey(ds.as<float>(), (uint32_t)T, (uint32_t)bins, H, max, min, dg.as<float>(), default_stream()))
         return set_error(THESIA_ERR_DEVICE, "spec_to_grey launch failed");
     THESIA_HIP(hipStreamSynchronize(default_stream()));
-    THESIA_HIP(hipMemcpy(grey, dg.p, (size_t)H * T * sizeof(float), hipMemcpyDeviceToHost));
+    THESIA_HIP(copy_ordered(grey, dg.p, (size_t)H * T * sizeof(float), hipMemcpyDeviceToHost));
     return THESIA_OK;
     GUARD_END
 }
@@ -384,7 +384,7 @@ int thesia_grey_to_rgb(const float* grey, uint32_t w, uint32_t h, uint32_t nw, u
     if (!rc) rc = drgb.alloc(bytes);
     if (!rc) rc = grey_to_rgb_device(dg.as<float>(), w, h, nw, nh, drgb.as<uint8_t>(), default_stream());
     if (rc) return rc;
-    THESIA_HIP(hipMemcpy(out, drgb.p, bytes, hipMemcpyDeviceToHost));
+    THESIA_HIP(copy_ordered(out, drgb.p, bytes, hipMemcpyDeviceToHost));
     return THESIA_OK;
     GUARD_END
 }
@@ -508,7 +508,7 @@ int thesia_inv_real_fft(const float* in, size_t n_frames, size_t length, float* 
     if (!rc) rc = inv_real_fft_device(din.as<float>(), n_frames, length, dout.as<float>(), default_stream());
     if (rc) return rc;
     THESIA_HIP(hipStreamSynchronize(default_stream()));
-    THESIA_HIP(hipMemcpy(out, dout.p, n_frames * length * sizeof(float), hipMemcpyDeviceToHost));
+    THESIA_HIP(copy_ordered(out, dout.p, n_frames * length * sizeof(float), hipMemcpyDeviceToHost));
     return THESIA_OK;
     GUARD_END
 }
@@ -526,7 +526,7 @@ int thesia_wav_to_image(const float* wav, size_t n, uint32_t nwidth, uint32_t nh
     if (!rc) rc = wav_to_image_device(dw.as<float>(), n, nwidth, nheight, amp_min, amp_max,
                                       dimg.as<uint8_t>(), &panicked, default_stream());
     if (rc) return rc;
-    THESIA_HIP(hipMemcpy(out, dimg.p, bytes, hipMemcpyDeviceToHost));
+    THESIA_HIP(copy_ordered(out, dimg.p, bytes, hipMemcpyDeviceToHost));
     if (panicked)
         return set_error(THESIA_ERR_PANIC, "the reference panics for these arguments (display.rs:95-108); "
                                            "the image is written with the column clamped");

@@ -49,8 +49,17 @@ int DevBuf::alloc(size_t n) {
 int DevBuf::upload(const void* host, size_t n) {
     int rc = alloc(n);
     if (rc) return rc;
-    if (n && host) THESIA_HIP(hipMemcpy(p, host, n, hipMemcpyHostToDevice));
+    if (n && host) THESIA_HIP(copy_ordered(p, host, n, hipMemcpyHostToDevice));
     return THESIA_OK;
+}
+
+// A blocking copy ordered after everything already enqueued on the library stream (a plain
+// hipMemcpy runs on the null stream, which does not wait for the non-blocking library stream)
+hipError_t copy_ordered(void* dst, const void* src, size_t bytes, hipMemcpyKind kind) {
+    hipStream_t s = default_stream();
+    hipError_t e = hipMemcpyAsync(dst, src, bytes, kind, s);
+    if (e == hipSuccess) e = hipStreamSynchronize(s);
+    return e;
 }
 
 hipStream_t default_stream() {
@@ -1012,7 +1021,7 @@ int render_rgb_fused(size_t n_groups, const float* const* d_specs, const uint64_
         if (!rc) rc = grow(ws.desc, std::max<size_t>(desc.size(), 1) * sizeof(RenderDesc));
         if (rc) return rc;
         if (!desc.empty())
-            THESIA_HIP(hipMemcpy(ws.desc.p, desc.data(), desc.size() * sizeof(RenderDesc), hipMemcpyHostToDevice));
+            THESIA_HIP(copy_ordered(ws.desc.p, desc.data(), desc.size() * sizeof(RenderDesc), hipMemcpyHostToDevice));
         ws.groups = std::move(groups);
         ws.key = std::move(key);
     }
@@ -1032,7 +1041,7 @@ int render_rgb_fused(size_t n_groups, const float* const* d_specs, const uint64_
                                      g.v_rows, g.v_kv, ws.tmp.as<float>(), cmap_ptr, d_rgb, s))
                 return set_error(THESIA_ERR_DEVICE, "render batch launch failed");
         }
-    THESIA_HIP(hipStreamSynchronize(s));
+    // stream-ordered: the images are complete for every later library call (copies included)
     return THESIA_OK;
 }
 

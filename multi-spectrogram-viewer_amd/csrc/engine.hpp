@@ -47,6 +47,7 @@ struct DevBuf {
 };
 
 hipStream_t default_stream();  // library stream of the current device
+hipError_t copy_ordered(void* dst, const void* src, size_t bytes, hipMemcpyKind kind);
 
 // ---- plan ----
 struct Plan {

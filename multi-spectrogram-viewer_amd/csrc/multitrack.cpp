@@ -333,7 +333,7 @@ int MultiTrack::spec_image(uint64_t id, float px_per_sec, uint32_t nheight, uint
     int rc = grey_to_rgb_device(tr->grey.as<float>(), (uint32_t)tr->T, tr->grey_h,
                                 image_width(px_per_sec, *tr), nheight, img_.as<uint8_t>(), default_stream());
     if (rc) return rc;
-    THESIA_HIP(hipMemcpy(out, img_.p, bytes, hipMemcpyDeviceToHost));
+    THESIA_HIP(copy_ordered(out, img_.p, bytes, hipMemcpyDeviceToHost));
     return THESIA_OK;
 }
 
@@ -355,7 +355,7 @@ int MultiTrack::wav_image(uint64_t id, float px_per_sec, uint32_t nheight, float
     int rc = wav_to_image_device(tr->wav(), tr->n, nwidth, nheight, amp_min, amp_max,
                                  img_.as<uint8_t>(), &panicked, default_stream());
     if (rc) return rc;
-    THESIA_HIP(hipMemcpy(out, img_.p, bytes, hipMemcpyDeviceToHost));
+    THESIA_HIP(copy_ordered(out, img_.p, bytes, hipMemcpyDeviceToHost));
     if (panicked)
         return set_error(THESIA_ERR_PANIC, "the reference panics for these arguments (display.rs:95-108); "
                                            "the image is written with the column clamped");
@@ -366,7 +366,7 @@ int MultiTrack::wav_host(uint64_t id, std::vector<float>* out) const {
     const Track* tr = find(id);
     if (!tr) return set_error(THESIA_ERR_UNKNOWN_ID, "unknown track id");
     out->resize(tr->n);
-    if (tr->n) THESIA_HIP(hipMemcpy(out->data(), tr->wav(), tr->n * 4, hipMemcpyDeviceToHost));
+    if (tr->n) THESIA_HIP(copy_ordered(out->data(), tr->wav(), tr->n * 4, hipMemcpyDeviceToHost));
     return THESIA_OK;
 }
 
@@ -383,7 +383,7 @@ int MultiTrack::spec_host(uint64_t id, std::vector<float>* out, size_t* T, size_
     const Track* tr = find(id);
     if (!tr) return set_error(THESIA_ERR_UNKNOWN_ID, "unknown track id");
     out->resize((size_t)tr->T * tr->bins);
-    THESIA_HIP(hipMemcpy(out->data(), tr->spec(), out->size() * 4, hipMemcpyDeviceToHost));
+    THESIA_HIP(copy_ordered(out->data(), tr->spec(), out->size() * 4, hipMemcpyDeviceToHost));
     *T = tr->T;
     *bins = tr->bins;
     return THESIA_OK;
@@ -393,7 +393,7 @@ int MultiTrack::grey_host(uint64_t id, std::vector<float>* out, uint32_t* w, uin
     const Track* tr = find(id);
     if (!tr) return set_error(THESIA_ERR_UNKNOWN_ID, "unknown track id");
     out->resize((size_t)tr->T * tr->grey_h);
-    THESIA_HIP(hipMemcpy(out->data(), tr->grey.p, out->size() * 4, hipMemcpyDeviceToHost));
+    THESIA_HIP(copy_ordered(out->data(), tr->grey.p, out->size() * 4, hipMemcpyDeviceToHost));
     *w = (uint32_t)tr->T;
     *h = tr->grey_h;
     return THESIA_OK;
