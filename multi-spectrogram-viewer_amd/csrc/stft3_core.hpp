@@ -111,7 +111,8 @@ __device__ __attribute__((noinline)) void fill_raw_half(const void* in, float* r
 template <int NC, int INF>
 __device__ __forceinline__ void load_raw_generic_ool(const StftLaunch& a, float* region, int j,
                                                      int64_t start, int64_t n, uint64_t base, int C,
-                                                     bool fold, float2 (&raw)[Geo2<NC>::P]) {
+                                                     bool fold, float2 (&raw)[Geo2<NC>::P], int rot = 0) {
+    // rot: the ring's slot map (stft5 THESIA_RING5): slot n1 holds point (n1 - rot) mod P
     constexpr int L = Geo2<NC>::L, P = Geo2<NC>::P;
 #pragma unroll
     for (int e = 0; e < 2; ++e) {
@@ -120,7 +121,7 @@ __device__ __forceinline__ void load_raw_generic_ool(const StftLaunch& a, float*
         wave_lds_sync();
         static_for<0, P>([&](auto ic) {
             constexpr int n1 = decltype(ic)::value;
-            const float r = region[L * n1 + j];
+            const float r = region[L * ((n1 + P - rot) & (P - 1)) + j];
             if (e == 0) raw[n1].x = r; else raw[n1].y = r;
         });
     }
