@@ -30,6 +30,9 @@
 #ifndef THESIA_HKT_MAX
 #define THESIA_HKT_MAX 48  // horizontal pass: most taps held in registers
 #endif
+#ifndef THESIA_H_ABL
+#define THESIA_H_ABL 0
+#endif
 #ifndef THESIA_H_DIRECT
 #define THESIA_H_DIRECT 1  // horizontal pass: RGB bytes stored lane by lane (no LDS assembly)
 #endif
@@ -476,7 +479,7 @@ __global__ void resize_v_batch_kernel(uint32_t nh, const RenderDesc* d, const fl
 #pragma unroll
         for (int i = 0; i < 16; ++i)
             if (i < n) t += v[i] * wr[i];
-        tmp[r.tmp_off + (uint64_t)oy * r.T + x] = t;
+        tmp[r.tmp_off + (uint64_t)oy * r.ts + x] = t;
     }
 }
 
@@ -558,7 +561,7 @@ __global__ void __launch_bounds__(256) resize_h_rgb_batch_kernel(uint32_t nh, co
     const bool pf = staged && span <= kHPf * 256;
     float nx[kHPf];
     auto load_row = [&](uint32_t yy) {
-        const float* src = tmp + r.tmp_off + (uint64_t)yy * r.T + lb;
+        const float* src = tmp + r.tmp_off + (uint64_t)yy * r.ts + lb;
 #pragma unroll
         for (int p = 0; p < kHPf; ++p) {
             const int32_t k = tid + 256 * p;
@@ -599,7 +602,7 @@ __global__ void __launch_bounds__(256) resize_h_rgb_batch_kernel(uint32_t nh, co
         const uint32_t G = gridDim.y;
         float nx1[kHPf];
         auto load_row1 = [&](uint32_t yy) {
-            const float* src = tmp + r.tmp_off + (uint64_t)yy * r.T + lb;
+            const float* src = tmp + r.tmp_off + (uint64_t)yy * r.ts + lb;
 #pragma unroll
             for (int p = 0; p < kHPf; ++p) {
                 const int32_t k = tid + 256 * p;
@@ -619,12 +622,15 @@ __global__ void __launch_bounds__(256) resize_h_rgb_batch_kernel(uint32_t nh, co
                 }
             }
             __syncthreads();
+#if !(THESIA_H_ABL & 4)  // ablation (timing only): no span loads
             if (y + 2 * G < nh) load_row(y + 2 * G);
             if (y + 3 * G < nh) load_row1(y + 3 * G);
+#endif
             if (act) {
                 float t0 = 0.0f, t1 = 0.0f;
                 const int base = l - lb;
-                if (n <= KT) {
+                if (THESIA_H_ABL & 1) {  // ablation (timing only): no sums
+                } else if (n <= KT) {
 #pragma unroll
                     for (int i = 0; i < KT; ++i) {
                         t0 += rin[base + i] * w[i];
@@ -644,8 +650,12 @@ __global__ void __launch_bounds__(256) resize_h_rgb_batch_kernel(uint32_t nh, co
                 colormap_px(t0, cm, px);
                 colormap_px(t1, cm, px + 3);
                 uint8_t* g0 = rgb + r.rgb_off + ((uint64_t)y * r.nw + ox) * 3;
+                if (THESIA_H_ABL & 2) {  // ablation (timing only): no stores
+                    if (px[0] == 255 && px[1] == 1 && px[2] == 254) g0[0] = 7;
+                } else {
                 g0[0] = px[0]; g0[1] = px[1]; g0[2] = px[2];
-                if (two) {
+                }
+                if (two && !(THESIA_H_ABL & 2)) {
                     uint8_t* g1 = g0 + (uint64_t)G * r.nw * 3;
                     g1[0] = px[3]; g1[1] = px[4]; g1[2] = px[5];
                 }
@@ -675,7 +685,7 @@ __global__ void __launch_bounds__(256) resize_h_rgb_batch_kernel(uint32_t nh, co
             __syncthreads();
             if (y + gridDim.y < nh) load_row(y + gridDim.y);
         } else if (staged) {
-            const float* src = tmp + r.tmp_off + (uint64_t)y * r.T + lb;
+            const float* src = tmp + r.tmp_off + (uint64_t)y * r.ts + lb;
             if (!(abl & 4))  // ablation (timing only): no row loads
                 for (int32_t k = tid; k < span; k += 256) rin[k] = src[k];
             __syncthreads();
@@ -691,7 +701,7 @@ __global__ void __launch_bounds__(256) resize_h_rgb_batch_kernel(uint32_t nh, co
                     for (int i = 0; i < n; ++i) t += rin[base + i] * wl[i * 256 + tid];
                 }
             } else {
-                const float* row = tmp + r.tmp_off + (uint64_t)y * r.T + l;
+                const float* row = tmp + r.tmp_off + (uint64_t)y * r.ts + l;
                 for (int32_t i = 0; i < n; ++i) t += row[i] * wr[i];
             }
             if (abl & 1) {  // ablation (timing only): no colormap
@@ -859,7 +869,7 @@ __global__ void __launch_bounds__(256) grey_vert_kernel(const float* spec, uint3
 #if THESIA_V_ABL & 1  // ablation (timing only): no tmp stores
                 if (t[q] == 1.2345e-30f)
 #endif
-                    out[(uint64_t)(oy + 4 * q) * r.T] = t[q];
+                    out[(uint64_t)(oy + 4 * q) * r.ts] = t[q];
             }
         }
         for (; oy < oy1; oy += 4) {
@@ -875,7 +885,7 @@ __global__ void __launch_bounds__(256) grey_vert_kernel(const float* spec, uint3
                 t += c[2 * TS] * w.z;
                 t += c[3 * TS] * w.w;
             }
-            out[(uint64_t)oy * r.T] = t;
+            out[(uint64_t)oy * r.ts] = t;
         }
         return;
     }
@@ -889,7 +899,7 @@ __global__ void __launch_bounds__(256) grey_vert_kernel(const float* spec, uint3
             const int32_t y = l + i;
             t += (y >= top ? grey_of(srow[H - 1 - y], max, min) : 0.0f) * wr[i];
         }
-        out[(uint64_t)oy * r.T] = t;
+        out[(uint64_t)oy * r.ts] = t;
     }
 }
 

@@ -880,6 +880,7 @@ int plan_fused_group(const float* d_spec, const uint64_t* row0, size_t bins, siz
         RenderDesc r{};
         r.spec_off = row0[i] * bins;
         r.tmp_off = g.tmp_tot;
+        r.ts = (T + 15) & ~15u;  // 64-byte aligned intermediate rows
         r.rgb_off = rgb_off[i];
         r.T = T;
         r.H = H;
@@ -894,7 +895,7 @@ int plan_fused_group(const float* d_spec, const uint64_t* row0, size_t bins, siz
         while (oz < nheight && vt->h_left[oz] + vt->h_count[oz] <= top) ++oz;
         r.oz = oz;
         if (std::find(vts.begin(), vts.end(), std::make_pair(vt, oz)) == vts.end()) vts.emplace_back(vt, oz);
-        g.tmp_tot += (uint64_t)T * nheight;
+        g.tmp_tot += (uint64_t)r.ts * nheight;
         g.h_taps = std::max(g.h_taps, ht->max_taps);
         g.h_span = std::max<int>(g.h_span, (int)((256.0 * T + nwidth[i] - 1) / nwidth[i]) + ht->max_taps + 8);
         g.T_max = std::max(g.T_max, T);
@@ -1124,6 +1125,7 @@ int render_rgb_batch_device(const float* d_spec, const uint64_t* row0, size_t bi
             r.spec_off = row0[i] * bins;
             r.grey_off = grey_tot;
             r.tmp_off = tmp_tot;
+            r.ts = T;
             r.rgb_off = rgb_off[i];
             r.T = T;
             r.H = H[i];

@@ -149,6 +149,7 @@ struct RenderDesc {
     // band (display.rs:44-54). Their sums are +0 exactly (t = +0; t += 0 * w stays +0), so the
     // fused path neither forms nor reads them: colormap(+0) rows. 0 = no shortcut.
     uint32_t oz;
+    uint32_t ts, pad_;  // row stride of the f32 intermediate (>= T; the fused path pads to 16)
 
     const int32_t *vl, *vc, *vo;
     const float* vw;
