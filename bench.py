@@ -64,6 +64,8 @@ def parse():
     p.add_argument("--kernel", type=int, default=0, help="force a fused kernel (1/2/3/5; 0 = automatic)")
     p.add_argument("--kernels", default="", help="A/B of named kernels on the product library: comma list "
                    "of kernel ids (interleaved rounds, one process), e.g. 3,5")
+    p.add_argument("--mel-paths", default="", help="A/B of stft5's mel projections (THESIA_BATCH_OPT_MEL_PATH): "
+                   "comma list, e.g. 1,2,3 (interleaved rounds, one process)")
     p.add_argument("--selftest", action="store_true",
                    help="launcher / reduction plumbing only: no GPU, no thesia (CPU tests)")
     p.add_argument("--selftest-fail-rank", type=int, default=-1, help=argparse.SUPPRESS)
@@ -542,6 +544,19 @@ def main_worker(args):
         if rank == 0:
             print(json.dumps({"kernels_ms": {str(k): {"median": float(np.median(t)), "min": float(min(t))}
                                              for k, t in res.items()}}), flush=True)
+
+    if args.mel_paths:
+        ps = [int(v) for v in args.mel_paths.split(",")]
+        res = {q: [] for q in ps}
+        for _ in range(5):  # interleaved rounds
+            for q in ps:
+                batch.set_option(engine.OPT_MEL_PATH, q)
+                batch.run_timed(1)
+                res[q].append(batch.run_timed(3) / 3)
+        batch.set_option(engine.OPT_MEL_PATH, 0)
+        if rank == 0:
+            print(json.dumps({"mel_paths_ms": {str(q): {"median": float(np.median(t)), "min": float(min(t))}
+                                               for q, t in res.items()}}), flush=True)
 
     # kernel duration from HIP events on the launch stream (roofline numerator / denominator)
     kms = batch.run_timed(max(args.steps, 5)) / max(args.steps, 5)

@@ -194,7 +194,12 @@ typedef enum {
      * reduction of update_spec_greys, lib.rs:194-207), folded into the streaming kernel's row
      * epilogue for the linear kinds, else one pass over the rows; read with
      * thesia_batch_ranges_read. Real output kinds only. */
-    THESIA_BATCH_OPT_RANGE = 4
+    THESIA_BATCH_OPT_RANGE = 4,
+    /* mel projection of stft5_kernel (the mel kinds at n_fft 2048): 0 = automatic, 1 = the
+     * filter rounds as one chunk stream, 2 / 3 = the packed stream (filters dealt to lanes by
+     * load) with 2 / 3 float4 steps per chunk. Every path is the same k-ascending fma chain
+     * per mel (identical bits). */
+    THESIA_BATCH_OPT_MEL_PATH = 5
 } thesia_batch_option;
 int thesia_batch_set_option(thesia_batch* batch, int option, int64_t value);
 /* Decode n tracks' range slots (THESIA_BATCH_OPT_RANGE buffer, device) after the runs that

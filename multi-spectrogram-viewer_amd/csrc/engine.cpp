@@ -277,6 +277,175 @@ static int build_mel4(Plan* p) {
     return rc;
 }
 
+// stft5's packed mel stream (kernels.hpp melp_*), S float4 steps per chunk. Every filter is
+// padded to whole chunks: its first chunk starts at a multiple of 4 bins at or before its band
+// and the weights outside the band are zero, so the lane's k-ascending fma chain adds only +0
+// terms around the band and each mel is the same chain as mel4's (bit-exact with it). The
+// filters are dealt to the 32 lanes largest first onto the least loaded lane (LPT) and a lane
+// runs its filters back to back: a frame costs the largest lane load in chunks (mel-128 @ 48 kHz
+// / 2048: 11 chunks of 2 steps, where the rounds pad every lane to the round's widest band and
+// take 32 steps). Placement: which lane runs which filter sequence, the order of a lane's
+// filters and each filter's start within its slack are searched (seeded random restarts +
+// coordinate descent) for the fewest LDS cycles of the |X| reads (a ds_read_b128 is served in
+// build_mel4's 16-lane groups; per group, the lanes of one 16-byte slot mod 16 cost one cycle
+// per distinct address).
+static const int kLdsG[2][16] = {{0, 1, 2, 3, 12, 13, 14, 15, 20, 21, 22, 23, 24, 25, 26, 27},
+                                 {4, 5, 6, 7, 8, 9, 10, 11, 16, 17, 18, 19, 28, 29, 30, 31}};
+
+static int build_melp(Plan* p, int S, Plan::Melp& out) {
+    out.chunks = 0;
+    out.steps = S;
+    constexpr int L = 32;
+    const long F = (long)p->NC + 1, F4 = (F + 3) / 4 * 4;
+    const int M = (int)p->n_mels;
+    if (p->NC != 1024 || F4 != kMelpOut || M <= 0 || kMelpOut + M + kMelpDummies > kStft5Region)
+        return THESIA_OK;  // not stft5's geometry / the mel slots do not fit the region
+    struct Flt { long kmin, kmax; int ch; };
+    std::vector<Flt> fl(M);
+    for (int m = 0; m < M; ++m) {
+        long lo = -1, hi = -1;
+        for (long k = 0; k < F; ++k)
+            if (p->mel_fb[(size_t)k * M + m] != 0.0f) {
+                if (lo < 0) lo = k;
+                hi = k + 1;
+            }
+        if (lo < 0) lo = hi = 0;  // empty filter: one chunk of zero weights (its mel is +0)
+        const long lo4 = lo / 4 * 4;
+        const int ch = (int)((std::max(1L, (hi - lo4 + 3) / 4) + S - 1) / S);
+        const long span = 4L * S * ch;
+        if (span > F4) return THESIA_OK;
+        fl[m] = Flt{std::max(0L, (hi - span + 3) / 4 * 4), std::min(lo4, F4 - span), ch};
+    }
+    std::vector<int> order(M);
+    for (int m = 0; m < M; ++m) order[m] = m;
+    std::stable_sort(order.begin(), order.end(), [&](int a, int b) { return fl[a].ch > fl[b].ch; });
+    std::vector<std::vector<int>> seq(L);
+    std::vector<int> load(L, 0);
+    for (int f : order) {
+        const int j = (int)(std::min_element(load.begin(), load.end()) - load.begin());
+        seq[j].push_back(f);
+        load[j] += fl[f].ch;
+    }
+    const int C = *std::max_element(load.begin(), load.end());
+    if (C > 64) return THESIA_OK;
+
+    int grp[L];
+    for (int g = 0; g < 2; ++g)
+        for (int i = 0; i < 16; ++i) grp[kLdsG[g][i]] = g;
+    std::vector<long> offs((size_t)L * C);  // |X| float offset per (lane, chunk); -1 = idle
+    auto cell = [&](int c, int g) {
+        long seen[16][16];
+        int cnt[16] = {0}, worst = 0;
+        for (int i = 0; i < 16; ++i) {
+            const long o = offs[(size_t)kLdsG[g][i] * C + c];
+            if (o < 0) continue;
+            const int s = (int)((o / 4) & 15);
+            bool dup = false;
+            for (int t = 0; t < cnt[s]; ++t) dup = dup || seen[s][t] == o;
+            if (!dup) seen[s][cnt[s]++] = o;
+            worst = std::max(worst, cnt[s]);
+        }
+        return worst;
+    };
+    std::vector<int> lane_of(M), c0_of(M), best_lane, best_c0;
+    std::vector<long> k0(M), best_k0;
+    long best = -1;
+    uint64_t rs = 0x9E3779B97F4A7C15ull;  // fixed seed: the plan's tables are deterministic
+    auto rnd = [&](uint64_t n) {
+        rs ^= rs << 13; rs ^= rs >> 7; rs ^= rs << 17;
+        return (int)(rs % n);
+    };
+    std::vector<int> perm(L);
+    for (int trial = 0; trial < 48; ++trial) {
+        for (int s = 0; s < L; ++s) perm[s] = s;
+        auto sq = seq;
+        if (trial > 0) {
+            for (int s = L - 1; s > 0; --s) std::swap(perm[s], perm[rnd(s + 1)]);
+            for (auto& q : sq)
+                for (int t = (int)q.size() - 1; t > 0; --t) std::swap(q[t], q[rnd(t + 1)]);
+        }
+        std::fill(offs.begin(), offs.end(), -1L);
+        for (int s = 0; s < L; ++s) {
+            int c = 0;
+            for (int f : sq[s]) {
+                lane_of[f] = perm[s];
+                c0_of[f] = c;
+                k0[f] = fl[f].kmax;
+                for (int i = 0; i < fl[f].ch; ++i) offs[(size_t)perm[s] * C + c + i] = k0[f] + 4L * S * i;
+                c += fl[f].ch;
+            }
+        }
+        for (int pass = 0; pass < 2; ++pass)
+            for (int f = 0; f < M; ++f) {
+                const int j = lane_of[f], g = grp[j];
+                long bk = k0[f];
+                int bc = 1 << 30;
+                for (long k = fl[f].kmax; k >= fl[f].kmin; k -= 4) {
+                    for (int i = 0; i < fl[f].ch; ++i) offs[(size_t)j * C + c0_of[f] + i] = k + 4L * S * i;
+                    int cost = 0;
+                    for (int i = 0; i < fl[f].ch; ++i) cost += cell(c0_of[f] + i, g);
+                    if (cost < bc) { bc = cost; bk = k; }
+                }
+                k0[f] = bk;
+                for (int i = 0; i < fl[f].ch; ++i) offs[(size_t)j * C + c0_of[f] + i] = bk + 4L * S * i;
+            }
+        long total = 0;
+        for (int c = 0; c < C; ++c) total += cell(c, 0) + cell(c, 1);
+        if (best < 0 || total < best) {
+            best = total;
+            best_lane = lane_of;
+            best_c0 = c0_of;
+            best_k0 = k0;
+        }
+    }
+    // tables: meta rows r = 0 .. C + 1 ({woff(r-1), keep(r-1), xoff(r), 0}); weight rows of
+    // chunks 0 .. C (chunk C: the pipeline's read-ahead padding, zero weights)
+    std::fill(offs.begin(), offs.end(), -1L);
+    std::vector<int> woff((size_t)(C + 1) * L), keep((size_t)(C + 1) * L, -1);
+    for (int j = 0; j < L; ++j)
+        for (int c = 0; c <= C; ++c) woff[(size_t)c * L + j] = (kMelpOut + M + (j & (kMelpDummies - 1))) * 4;
+    std::vector<float> wt((size_t)(C + 1) * S * L * 4, 0.0f);
+    for (int f = 0; f < M; ++f) {
+        const int j = best_lane[f];
+        for (int i = 0; i < fl[f].ch; ++i) {
+            const int c = best_c0[f] + i;
+            offs[(size_t)j * C + c] = best_k0[f] + 4L * S * i;
+            for (int u = 0; u < S; ++u)
+                for (int e = 0; e < 4; ++e) {
+                    const long k = best_k0[f] + 4L * (S * i + u) + e;
+                    wt[(((size_t)c * S + u) * L + j) * 4 + e] = k < F ? p->mel_fb[(size_t)k * M + f] : 0.0f;
+                }
+        }
+        const int cl = best_c0[f] + fl[f].ch - 1;
+        woff[(size_t)cl * L + j] = (kMelpOut + f) * 4;
+        keep[(size_t)cl * L + j] = 0;
+    }
+    // idle chunks read an address another lane of their group reads (a broadcast: no cycle)
+    std::vector<int> xoff((size_t)(C + 1) * L, 0);
+    for (int c = 0; c < C; ++c)
+        for (int g = 0; g < 2; ++g) {
+            long any = 0;
+            for (int i = 0; i < 16; ++i)
+                if (offs[(size_t)kLdsG[g][i] * C + c] >= 0) { any = offs[(size_t)kLdsG[g][i] * C + c]; break; }
+            for (int i = 0; i < 16; ++i) {
+                const int j = kLdsG[g][i];
+                const long o = offs[(size_t)j * C + c];
+                xoff[(size_t)c * L + j] = (int)((o >= 0 ? o : any) * 4);
+            }
+        }
+    std::vector<int4> meta((size_t)(C + 2) * L);
+    for (int r = 0; r <= C + 1; ++r)
+        for (int j = 0; j < L; ++j) {
+            const int c = r - 1;
+            meta[(size_t)r * L + j] = int4{c >= 0 ? woff[(size_t)c * L + j] : 0, c >= 0 ? keep[(size_t)c * L + j] : -1,
+                                           r <= C ? xoff[(size_t)r * L + j] : 0, 0};
+        }
+    int rc = out.meta.upload(meta.data(), meta.size() * sizeof(int4));
+    if (!rc) rc = out.wt.upload(wt.data(), wt.size() * sizeof(float));
+    if (!rc) out.chunks = C;
+    return rc;
+}
+
 // rustfft's prepare_radix4 (oracle cfft_tab): spec[j] = sig[...] in the digit order the
 // radix-4 passes expect; run on indices it gives the source of every position
 static void prepare_radix4_order(size_t size, const int* sig, int* spec, size_t stride) {
@@ -398,6 +567,15 @@ int plan_create(const thesia_plan_desc& d, Plan** out) {
         }
         if (!rc) rc = build_mel(p);
         if (!rc) rc = build_mel4(p);
+        for (int i = 0; i < 2 && !rc; ++i) rc = build_melp(p, 2 + i, p->melp[i]);
+        if (!rc) {  // default: the fewest estimated instructions per chunk stream (5 + 6 S each)
+            long bc = -1;
+            for (int i = 0; i < 2; ++i)
+                if (p->melp[i].chunks > 0) {
+                    const long c = (long)p->melp[i].chunks * (5 + 6 * p->melp[i].steps);
+                    if (bc < 0 || c < bc) { bc = c; p->melp_best = i; }
+                }
+        }
         if (!rc) {  // the reference-order kernel: each mel's nonzero band, weights flat
             const size_t M = p->n_mels;
             std::vector<int4> band(std::max<size_t>(M, 1), int4{0, 0, 0, 0});
@@ -514,14 +692,19 @@ int batch_create(Plan* plan, const thesia_batch_desc& d, Batch** out) {
     L.mel_chunks = plan->mel_chunks;
     L.mel_xo = plan->mel_xo.as<int>();
     L.out = d.d_output;
+    b->apply_mel_path();
     // kernel choice: the streaming kernel for its geometry, else the 4-waves/SIMD kernel for
     // its sizes, else the general one (thesia_batch_set_option can force another one)
     b->k3_ok = plan->use_v2 && stft3_supports((int)plan->n_fft, (int)plan->win, (int)plan->hop,
                                               d.input_format, (int)d.channels) &&
                stft3_lds_bytes(L) <= 163840;  // the mel weights must fit LDS (else stft2)
-    b->k5_ok = b->k3_ok && stft5_supports((int)plan->n_fft, (int)plan->win, (int)plan->hop,
-                                          d.input_format, (int)d.channels) &&
-               stft5_lds_bytes(L) <= 163840;
+    const bool k5_geo = b->k3_ok && stft5_supports((int)plan->n_fft, (int)plan->win, (int)plan->hop,
+                                                   d.input_format, (int)d.channels);
+    if (k5_geo && L.melp_chunks && stft5_lds_bytes(L) > 163840) {  // packed stream too big: rounds
+        b->mel_path = 1;
+        b->apply_mel_path();
+    }
+    b->k5_ok = k5_geo && stft5_lds_bytes(L) <= 163840;
     b->kernel = b->auto_kernel();
     if (hipEventCreate(&b->ev0) != hipSuccess || hipEventCreate(&b->ev1) != hipSuccess) {
         delete b;
@@ -529,6 +712,22 @@ int batch_create(Plan* plan, const thesia_batch_desc& d, Batch** out) {
     }
     *out = b;
     return THESIA_OK;
+}
+
+void Batch::apply_mel_path() {
+    StftLaunch& L = launch;
+    L.melp_chunks = L.melp_steps = L.melp_v4 = 0;
+    L.melp_meta = nullptr;
+    L.melp_wt = nullptr;
+    const int idx = mel_path == 0 ? plan->melp_best : mel_path >= 2 ? mel_path - 2 : -1;
+    if (idx < 0 || plan->melp[idx].chunks == 0) return;
+    const Plan::Melp& m = plan->melp[idx];
+    L.melp_chunks = m.chunks;
+    L.melp_steps = m.steps;
+    L.melp_meta = m.meta.as<int4>();
+    L.melp_wt = m.wt.as<float4>();
+    L.melp_v4 = plan->n_mels % 4 == 0 && plan->n_mels <= 128 &&
+                (reinterpret_cast<uintptr_t>(L.out) & 15) == 0;
 }
 
 int batch_set_option(Batch* b, int option, int64_t value) {
@@ -557,6 +756,20 @@ int batch_set_option(Batch* b, int option, int64_t value) {
                 return set_error(THESIA_ERR_INVALID_ARG, "ranges need real output rows");
             b->range = reinterpret_cast<int*>(value);
             return THESIA_OK;
+        case THESIA_BATCH_OPT_MEL_PATH: {
+            if (value < 0 || value > 3) return set_error(THESIA_ERR_INVALID_ARG, "mel_path must be 0..3");
+            if (value >= 2 && b->plan->melp[value - 2].chunks == 0)
+                return set_error(THESIA_ERR_UNSUPPORTED, "no packed mel stream for this plan");
+            const int prev = b->mel_path;
+            b->mel_path = (int)value;
+            b->apply_mel_path();
+            if (b->k5_ok && stft5_lds_bytes(b->launch) > 163840) {
+                b->mel_path = prev;
+                b->apply_mel_path();
+                return set_error(THESIA_ERR_UNSUPPORTED, "the mel tables of that path do not fit LDS");
+            }
+            return THESIA_OK;
+        }
         case THESIA_BATCH_OPT_ROW_STORE:
             if (value < 0 || value > 1) return set_error(THESIA_ERR_INVALID_ARG, "row_store must be 0 or 1");
             b->launch.row_alt = (int)value;

@@ -69,6 +69,13 @@ struct Plan {
     float xw8[4] = {0.f, 0.f, 0.f, 0.f};
     int mel_chunks = 0;
     size_t mel4_wt_rows = 0;
+    // stft5's packed mel stream, built for 2 and 3 float4 steps per chunk (build_melp)
+    struct Melp {
+        DevBuf meta, wt;
+        int chunks = 0;  // 0: not available for this filterbank
+        int steps = 0;
+    } melp[2];
+    int melp_best = -1;  // index into melp of the default (fewest estimated instructions), -1 none
     bool use_v2 = false;  // stft2_kernel runs this plan (n_fft 256..2048)
     size_t row_bins() const;
     size_t out_elem_bytes() const { return out_kind == OUT_COMPLEX ? 8 : 4; }
@@ -95,6 +102,10 @@ struct Batch {
         const bool mel = launch.out_kind == OUT_MEL || launch.out_kind == OUT_MEL_AMP_DB;
         return k5_ok && mel ? 5 : k3_ok ? 3 : plan->use_v2 ? 2 : 1;
     }
+    // mel projection of stft5 (THESIA_BATCH_OPT_MEL_PATH): 0 automatic, 1 the rounds' chunk
+    // stream (mel4p), 2 / 3 the packed stream with 2 / 3 float4 steps per chunk
+    int mel_path = 0;
+    void apply_mel_path();
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     int* range = nullptr;  // THESIA_BATCH_OPT_RANGE: per-track {ord max, ord min, NaN} on the device
     ~Batch();

@@ -68,6 +68,20 @@ struct StftLaunch {
     // last chunk of its round. 0 chunks when the plan does not fit (<= 8 chunks).
     int mel_chunks = 0;
     const int* mel_xo = nullptr;
+    // stft5's packed mel stream (engine.cpp build_melp): every lane runs its own sequence of
+    // whole filters, each padded to chunks of melp_steps float4 steps (lanes load-balanced, so
+    // a frame runs melp_chunks chunks instead of the rounds' widest bands). Chunk c of lane j:
+    // weights melp_wt[(c * melp_steps + u) * L + j], u < melp_steps; its |X| floats start at
+    // byte xoff(c) of the stream's LDS region; after its fma chain the running sum is stored
+    // at byte woff(c) of the region (the mel's slot behind the |X| row, kMelpOut, or a dummy
+    // slot) and ANDed with keep(c) (0: the chunk ends a filter, the next starts from +0).
+    // melp_meta[(c + 1) * L + j] = {woff(c), keep(c), xoff(c + 1), 0}, c = -1 .. melp_chunks - 1
+    // (one zero chunk of padding at the end: the pipeline reads one chunk ahead).
+    int melp_chunks = 0;
+    int melp_steps = 0;
+    int melp_v4 = 0;  // n_mels % 4 == 0 and 16-byte aligned rows: float4 row stores
+    const int4* melp_meta = nullptr;
+    const float4* melp_wt = nullptr;
     // output
     void* out = nullptr;  // packed rows: frame g at out + g * row_elems
     // scheduling / named alternatives (thesia_batch_set_option)
@@ -87,6 +101,10 @@ struct StftLaunch {
     // {ordered max, ordered min, NaN seen} (range_ord below); null = off
     int* trk_range = nullptr;
 };
+
+// stft5 stream region (floats) and where the packed mel stream stages a frame's mels in it:
+// behind the |X| row of F4 = 1028 floats; dummy slots follow the n_mels slots
+constexpr int kStft5Region = 1184, kMelpOut = 1028, kMelpDummies = 16;
 
 // f32 <-> int32 with the order of the floats (max / min by integer atomics); NaN excluded
 __host__ __device__ inline int range_ord(float x) {

@@ -76,7 +76,11 @@ struct Geo5 {
     static constexpr int TAB_FLOATS = WL_FLOATS + TW_FLOATS;
     static constexpr int TWC = THESIA_TWC5;  // stage-1 twiddle float4 reads per batch
     static constexpr int BH = THESIA_BH5;    // parts the partner row B is read in
+#ifdef THESIA_PF5
+    static constexpr int PF_POS = THESIA_PF5;  // where the next hop's loads issue (3: after the mel)
+#else
     static constexpr int PF_POS = WV == 8 ? 0 : 2;  // where the next hop's loads issue
+#endif
     static_assert(RS_MIN >= P * S && RS_MIN >= F + 6 && RS_MIN % 4 == 0 && RS % 4 == 0, "region");
 };
 
@@ -153,6 +157,89 @@ __device__ __forceinline__ void untangle5(const float2 (&v)[32], bool lane0, con
     });
 }
 
+// The packed mel stream (engine.cpp build_melp, kernels.hpp melp_*): the chunks of the lane's
+// filters back to back, software-pipelined one chunk ahead (chunk c + 1's meta, weight and |X|
+// reads are issued before chunk c's fma chain; chunk c + 1's |X| offset came with chunk c's
+// meta). A chunk ends by storing its running sum at woff(c) of the region (the mel's slot, or a
+// dummy slot while the filter continues) and ANDing it with keep(c): +0 after a filter's last
+// chunk. The chain of each mel is mel4's k-ascending fma chain (identical bits). The frame's
+// mels then leave as dB rows: one 16-byte store per lane for n_mels % 4 == 0.
+static_assert(Geo5::RS == kStft5Region && Geo2<Geo5::NC>::F4 == kMelpOut, "melp region layout");
+template <int S>
+__device__ __forceinline__ void melp5(const StftLaunch& a, float* region, const int4* meta,
+                                      const float4* wt, int j, uint64_t g, bool valid) {
+    constexpr int L = Geo5::L;
+    const int C = a.melp_chunks;
+    char* rb = reinterpret_cast<char*>(region);
+    const int4* mp = meta + j;
+    const float4* wp = wt + j;
+    struct Buf {
+        float4 w[S], x[S];
+        int4 m;
+    };
+    auto issue = [&](int c, int xoff, Buf& b) {
+        b.m = mp[(c + 1) * L];
+#pragma unroll
+        for (int u = 0; u < S; ++u) b.w[u] = wp[(c * S + u) * L];
+        const float4* xp = reinterpret_cast<const float4*>(rb + xoff);
+#pragma unroll
+        for (int u = 0; u < S; ++u) b.x[u] = xp[u];
+        // keep the reads ahead of the previous chunk's chain
+        __builtin_amdgcn_sched_barrier(0);
+    };
+    float acc = 0.0f;
+    auto chain = [&](const Buf& b) {
+#pragma unroll
+        for (int u = 0; u < S; ++u) {
+            acc = __builtin_fmaf(b.x[u].x, b.w[u].x, acc);
+            acc = __builtin_fmaf(b.x[u].y, b.w[u].y, acc);
+            acc = __builtin_fmaf(b.x[u].z, b.w[u].z, acc);
+            acc = __builtin_fmaf(b.x[u].w, b.w[u].w, acc);
+        }
+        *reinterpret_cast<float*>(rb + b.m.x) = acc;
+        acc = __builtin_bit_cast(float, __builtin_bit_cast(int, acc) & b.m.y);
+    };
+    Buf A, B;
+    int c = 0;
+    const int x0 = mp[0].z;
+    if (C & 1) {
+        issue(0, x0, B);
+        issue(1, B.m.z, A);
+        chain(B);
+        c = 1;
+    } else {
+        issue(0, x0, A);
+    }
+    for (; c < C; c += 2) {  // C - c even; chunk C is the tables' zero padding (read, not used)
+        issue(c + 1, A.m.z, B);
+        chain(A);
+        issue(c + 2, B.m.z, A);
+        chain(B);
+    }
+    wave_lds_sync();
+    const int n_mels = a.n_mels;
+    const bool db = a.out_kind == OUT_MEL_AMP_DB;
+    float* out = static_cast<float*>(a.out) + g * (uint64_t)n_mels;
+    const float* mo = region + kMelpOut;
+    if (a.melp_v4) {
+        if (4 * j < n_mels) {
+            float4 r = *reinterpret_cast<const float4*>(mo + 4 * j);
+            if (db) {
+                r.x = db_of(r.x, a.log_amin, 1e-18f, 20.0f);
+                r.y = db_of(r.y, a.log_amin, 1e-18f, 20.0f);
+                r.z = db_of(r.z, a.log_amin, 1e-18f, 20.0f);
+                r.w = db_of(r.w, a.log_amin, 1e-18f, 20.0f);
+            }
+            if (valid) *reinterpret_cast<float4*>(out + 4 * j) = r;
+        }
+    } else {
+        for (int m = j; m < n_mels; m += L) {
+            const float v = mo[m];
+            if (valid) st_out(out + m, db ? db_of(v, a.log_amin, 1e-18f, 20.0f) : v);
+        }
+    }
+}
+
 // OK: 0 complex, 1 linear kinds, 2 mel kinds. C: 1 mono, 2 stereo (interleaved); INF: f32 / s16.
 template <int OK, int C, int INF>
 __global__ void __launch_bounds__(Geo5::BLOCK, Geo5::WV / 4)
@@ -169,10 +256,14 @@ stft5_kernel(StftLaunch a, uint64_t fps, int rs) {
     float* wtl = lds;
     float2* twtab = reinterpret_cast<float2*>(lds + G::WL_FLOATS);
     float* work = lds + G::WL_FLOATS + G::TW_FLOATS;
+    // mel tables: the packed stream (meta rows, then weight rows) or the rounds' chunk stream
+    const bool packed = OK == 2 && a.melp_chunks > 0;
     float4* mel_lds = reinterpret_cast<float4*>(lds + G::TAB_FLOATS + G::STREAMS * rs);
-    int* k0_lds = reinterpret_cast<int*>(mel_lds + (OK == 2 ? a.mel4_rows * L : 0));
-    int2* rd_lds = reinterpret_cast<int2*>(k0_lds + (OK == 2 ? a.mel4_rounds * L : 0));
-    int* xo_lds = reinterpret_cast<int*>(rd_lds + (OK == 2 ? a.mel4_rounds : 0));
+    int4* pm_lds = reinterpret_cast<int4*>(mel_lds);
+    float4* pw_lds = mel_lds + (packed ? (a.melp_chunks + 2) * L : 0);
+    int* k0_lds = reinterpret_cast<int*>(mel_lds + (OK == 2 && !packed ? a.mel4_rows * L : 0));
+    int2* rd_lds = reinterpret_cast<int2*>(k0_lds + (OK == 2 && !packed ? a.mel4_rounds * L : 0));
+    int* xo_lds = reinterpret_cast<int*>(rd_lds + (OK == 2 && !packed ? a.mel4_rounds : 0));
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int slot = lane / L, j = lane % L;
     const bool lane0 = j == 0;
@@ -182,7 +273,11 @@ stft5_kernel(StftLaunch a, uint64_t fps, int rs) {
         const int m = i >> 1, jj = m % L, n1 = m / L;
         wtl[jj * G::WL_STRIDE + 2 * n1 + (i & 1)] = a.wpad[i] * 0.5f;
     }
-    if constexpr (OK == 2) {
+    if (packed) {
+        for (int i = threadIdx.x; i < (a.melp_chunks + 2) * L; i += kBlock) pm_lds[i] = a.melp_meta[i];
+        const int nw = (a.melp_chunks + 1) * a.melp_steps * L;
+        for (int i = threadIdx.x; i < nw; i += kBlock) pw_lds[i] = a.melp_wt[i];
+    } else if constexpr (OK == 2) {
         const int nw = a.mel4_rows * L;
         for (int i = threadIdx.x; i < nw; i += kBlock) mel_lds[i] = a.mel4_wt[i];
         for (int i = threadIdx.x; i < a.mel4_rounds * L; i += kBlock) k0_lds[i] = a.mel4_k0[i];
@@ -461,9 +556,16 @@ stft5_kernel(StftLaunch a, uint64_t fps, int rs) {
             wave_lds_sync();
             if constexpr (G::PF_POS == 2) prefetch();
             MARK5(untangled, 6);
-            if (a.mel_chunks == 8) mel4p<NC, 8>(a, region, mel_lds, xo_lds, j, g, valid);
+            if (packed) {
+                if (a.melp_steps == 2) melp5<2>(a, region, pm_lds, pw_lds, j, g, valid);
+                else melp5<3>(a, region, pm_lds, pw_lds, j, g, valid);
+            }
+#ifndef THESIA_MELP_ONLY
+            else if (a.mel_chunks == 8) mel4p<NC, 8>(a, region, mel_lds, xo_lds, j, g, valid);
             else if (a.mel_chunks == 4) mel4p<NC, 4>(a, region, mel_lds, xo_lds, j, g, valid);
             else mel4<NC, 8, 1>(a, region, mel_lds, rd_lds, k0_lds, j, g, valid);
+#endif
+            if constexpr (G::PF_POS == 3) prefetch();
         } else if constexpr (OK == 0) {  // lane-wise 8-byte stores
             if constexpr (G::PF_POS == 2) prefetch();
             float2* crow = reinterpret_cast<float2*>(a.out) + g * F;
@@ -522,11 +624,15 @@ stft5_kernel(StftLaunch a, uint64_t fps, int rs) {
 // --------------------------------------------------------------------------------------
 template <int OK>
 static int lds5_bytes(const StftLaunch& a, int rs) {
-    return (Geo5::TAB_FLOATS + Geo5::STREAMS * rs +
-            (OK == 2 ? (a.mel4_rows * 4 + a.mel4_rounds + a.mel_chunks) * Geo5::L + 2 * a.mel4_rounds : 0)) * 4;
+    const int mel = OK != 2 ? 0
+                    : a.melp_chunks > 0 ? ((a.melp_chunks + 2) + (a.melp_chunks + 1) * a.melp_steps) * Geo5::L * 4
+                    : (a.mel4_rows * 4 + a.mel4_rounds + a.mel_chunks) * Geo5::L + 2 * a.mel4_rounds;
+    return (Geo5::TAB_FLOATS + Geo5::STREAMS * rs + mel) * 4;
 }
 template <int OK>
 static int region_stride5(const StftLaunch& a) {
+    // the packed mel stream stages the frame's mels behind the |X| row: full regions only
+    if (OK == 2 && a.melp_chunks > 0) return Geo5::RS;
     return lds5_bytes<OK>(a, Geo5::RS) <= 163840 ? Geo5::RS : Geo5::RS_MIN;
 }
 

@@ -11,7 +11,7 @@ from ._lib import lib, check, PlanDesc, BatchDesc, _fp, _u64p
 
 OUT_COMPLEX, OUT_MAG, OUT_POWER, OUT_AMP_DB, OUT_POWER_DB, OUT_MEL, OUT_MEL_AMP_DB = range(7)
 IN_F32, IN_S16 = 0, 1
-OPT_KERNEL, OPT_MAX_BLOCKS, OPT_ROW_STORE, OPT_RANGE = 1, 2, 3, 4
+OPT_KERNEL, OPT_MAX_BLOCKS, OPT_ROW_STORE, OPT_RANGE, OPT_MEL_PATH = 1, 2, 3, 4, 5
 
 
 def device_count() -> int:
@@ -155,8 +155,8 @@ class Batch:
 
     def __init__(self, plan: Plan, d_input: DeviceBuffer, track_offset, track_len, d_output,
                  input_format: int = IN_F32, channels: int = 1, fold_mono: bool = False,
-                 kernel: int = 0, max_blocks: int = 0, row_store: int = 0):
-        """kernel / max_blocks / row_store: thesia_batch_set_option (0 = defaults)."""
+                 kernel: int = 0, max_blocks: int = 0, row_store: int = 0, mel_path: int = 0):
+        """kernel / max_blocks / row_store / mel_path: thesia_batch_set_option (0 = defaults)."""
         self.plan = plan
         self._off = np.ascontiguousarray(track_offset, np.uint64)
         self._len = np.ascontiguousarray(track_len, np.uint64)
@@ -174,7 +174,8 @@ class Batch:
         check(lib.thesia_batch_frames(self.handle, C.byref(tot), f0.ctypes.data_as(_u64p)))
         self.total_frames = tot.value
         self.frame0 = f0
-        for opt, v in ((OPT_KERNEL, kernel), (OPT_MAX_BLOCKS, max_blocks), (OPT_ROW_STORE, row_store)):
+        for opt, v in ((OPT_KERNEL, kernel), (OPT_MAX_BLOCKS, max_blocks), (OPT_ROW_STORE, row_store),
+                       (OPT_MEL_PATH, mel_path)):
             if v:
                 self.set_option(opt, v)
 

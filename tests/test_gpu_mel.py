@@ -10,6 +10,7 @@ import pytest
 
 import oracle_ffi as O
 from thesia import engine
+from thesia._lib import ThesiaError
 from tolerances import DB_MAX, DB_P9999, db_clamped_err
 
 pytestmark = pytest.mark.gpu
@@ -19,7 +20,7 @@ _LAST = {}
 
 
 def _run(kind, tracks, channels, fmt, n_mels=0, sr=48000, kernel=3, gap=0, mel_fb=None,
-         max_blocks=0):
+         max_blocks=0, mel_path=0, out_shift=0):
     parts, offs, off = [], [], 0
     for t in tracks:
         offs.append(off)
@@ -33,15 +34,20 @@ def _run(kind, tracks, channels, fmt, n_mels=0, sr=48000, kernel=3, gap=0, mel_f
     din = engine.DeviceBuffer.from_host(flat)
     T = engine.Batch.frames_for(plan, lens)
     esz = 8 if kind == engine.OUT_COMPLEX else 4
-    dout = engine.DeviceBuffer(T * plan.row_bins * esz)
-    b = engine.Batch(plan, din, offs, lens, dout, input_format=fmt, channels=channels,
-                     kernel=kernel, max_blocks=max_blocks)
+    dout = engine.DeviceBuffer(T * plan.row_bins * esz + out_shift)
+    b = engine.Batch(plan, din, offs, lens, dout.ptr.value + out_shift, input_format=fmt, channels=channels,
+                     kernel=kernel, max_blocks=max_blocks, mel_path=mel_path)
     if kernel:
         assert b.kernel == kernel
     _LAST["kernel"] = b.kernel
     b.run()
     engine.synchronize()
-    out = dout.to_host(np.complex64 if esz == 8 else np.float32, (T, plan.row_bins))
+    dt = np.complex64 if esz == 8 else np.float32
+    if out_shift:
+        raw = dout.to_host(np.uint8, (T * plan.row_bins * esz + out_shift,))
+        out = raw[out_shift:].view(dt).reshape(T, plan.row_bins)
+    else:
+        out = dout.to_host(dt, (T, plan.row_bins))
     return out, plan
 
 
@@ -67,6 +73,32 @@ def test_mel_is_the_dot_of_the_kernels_own_magnitude(kernel, n_mels, sr, channel
     fb = O.calc_mel_fb(sr, 2048, n_mels) if n_mels else O.calc_mel_fb_default(sr, 2048)
     assert plan.row_bins == fb.shape[1]
     np.testing.assert_array_equal(mel, O.dot(mag, fb))
+
+
+@pytest.mark.parametrize("mel_path,out_shift", [(1, 0), (2, 0), (3, 0), (2, 4), (3, 8)])
+@pytest.mark.parametrize("n_mels,sr", [(128, 48000), (40, 48000), (80, 16000), (130, 44100), (10, 48000)])
+def test_stft5_mel_paths_are_the_same_chain(mel_path, out_shift, n_mels, sr):
+    """stft5's mel projections (THESIA_BATCH_OPT_MEL_PATH): the rounds' chunk stream and the
+    packed streams with 2 / 3 float4 steps per chunk (filters dealt to lanes by load, mels staged
+    behind the |X| row; 16-byte row stores when n_mels % 4 == 0 and the rows are aligned, lane-wise
+    stores otherwise -- out_shift misaligns the output) are all the k-ascending fma chain of
+    O.dot over the kernel's own |X|, bit for bit; the dB rows follow from the same values."""
+    rng = np.random.default_rng(n_mels + 3 * mel_path + out_shift + sr)
+    tracks = _tracks(rng, 2, engine.IN_F32, [2048 * 7 + 5, 512 * 33 + 1, 30011])
+    mag, _ = _run(engine.OUT_MAG, tracks, 2, engine.IN_F32, kernel=5, max_blocks=3)
+    fb = O.calc_mel_fb(sr, 2048, n_mels)
+    try:
+        mel, plan = _run(engine.OUT_MEL, tracks, 2, engine.IN_F32, n_mels=n_mels, sr=sr, kernel=5,
+                         max_blocks=3, mel_path=mel_path, out_shift=out_shift)
+    except ThesiaError as e:  # the packed stream does not cover this filterbank
+        assert mel_path >= 2 and ("packed" in str(e) or "fit" in str(e)), e
+        pytest.skip(str(e))
+    np.testing.assert_array_equal(mel, O.dot(mag, fb))
+    db, _ = _run(engine.OUT_MEL_AMP_DB, tracks, 2, engine.IN_F32, n_mels=n_mels, sr=sr, kernel=5,
+                 max_blocks=3, mel_path=mel_path, out_shift=out_shift)
+    ref, _ = _run(engine.OUT_MEL_AMP_DB, tracks, 2, engine.IN_F32, n_mels=n_mels, sr=sr, kernel=5,
+                  max_blocks=3, mel_path=1)
+    np.testing.assert_array_equal(db, ref)
 
 
 @pytest.mark.parametrize("which", ["dense", "two_wide_bands", "slaney_like"])
