@@ -61,6 +61,14 @@ namespace thesia {
 #ifndef THESIA_TWC5
 #define THESIA_TWC5 8
 #endif
+// the next hop's samples by LDS-DMA (global_load_lds_dwordx4, no VGPRs) into the wave's two
+// stream regions after the mel, stereo f32 only (experiment: three waves per SIMD)
+#ifndef THESIA_DMA5
+#define THESIA_DMA5 0
+#endif
+#ifndef THESIA_S32
+#define THESIA_S32 0
+#endif
 struct Geo5 {
     static constexpr int NC = 1024, L = 32, P = 32, FPW = 2, F = NC + 1, SH = P / 4;
     static constexpr int S = L + 4;       // transpose row stride (16 lanes of a b128 read: distinct banks)
@@ -73,10 +81,13 @@ struct Geo5 {
     static constexpr int RS = 1184, RS_MIN = 1152;
     static constexpr int WL_STRIDE = 2 * P + 4, WL_FLOATS = L * WL_STRIDE;
     static constexpr int TW_FLOATS = 2 * P * L;
-    static constexpr int TAB_FLOATS = WL_FLOATS + TW_FLOATS;
+    static constexpr int SCT_FLOATS = THESIA_SC5 == 2 ? 16 * L * 2 : 0;  // rotation table (SC5 == 2)
+    static constexpr int TAB_FLOATS = WL_FLOATS + TW_FLOATS + SCT_FLOATS;
     static constexpr int TWC = THESIA_TWC5;  // stage-1 twiddle float4 reads per batch
     static constexpr int BH = THESIA_BH5;    // parts the partner row B is read in
-#ifdef THESIA_PF5
+#if THESIA_DMA5
+    static constexpr int PF_POS = 3;  // the DMA lands in the stream regions: after the mel
+#elif defined(THESIA_PF5)
     static constexpr int PF_POS = THESIA_PF5;  // where the next hop's loads issue (3: after the mel)
 #else
     static constexpr int PF_POS = WV == 8 ? 0 : 2;  // where the next hop's loads issue
@@ -113,6 +124,16 @@ struct RotTable {
     const float2 (&t)[16];
     template <int I>
     __device__ __forceinline__ void get(float& s, float& co) const { s = t[I].x; co = t[I].y; }
+};
+// the same values from an LDS table [16][L] (THESIA_SC5 == 2: no registers held across frames)
+struct RotLds {
+    const float2* t;  // + lane j
+    template <int I>
+    __device__ __forceinline__ void get(float& s, float& co) const {
+        const float2 v = t[I * Geo5::L];
+        s = v.x;
+        co = v.y;
+    }
 };
 
 template <int I0, int I1, class Rot, class Epi>
@@ -171,8 +192,12 @@ __device__ __forceinline__ void melp5(const StftLaunch& a, float* region, const 
     constexpr int L = Geo5::L;
     const int C = a.melp_chunks;
     char* rb = reinterpret_cast<char*>(region);
-    const int4* mp = meta + j;
-    const float4* wp = wt + j;
+    // opaque lane index: the table addresses are formed per frame, not hoisted out of the
+    // frame loop into registers held across it
+    int lj = j;
+    asm volatile("" : "+v"(lj));
+    const int4* mp = meta + lj;
+    const float4* wp = wt + lj;
     struct Buf {
         float4 w[S], x[S];
         int4 m;
@@ -222,18 +247,18 @@ __device__ __forceinline__ void melp5(const StftLaunch& a, float* region, const 
     float* out = static_cast<float*>(a.out) + g * (uint64_t)n_mels;
     const float* mo = region + kMelpOut;
     if (a.melp_v4) {
-        if (4 * j < n_mels) {
-            float4 r = *reinterpret_cast<const float4*>(mo + 4 * j);
+        if (4 * lj < n_mels) {
+            float4 r = *reinterpret_cast<const float4*>(mo + 4 * lj);
             if (db) {
                 r.x = db_of(r.x, a.log_amin, 1e-18f, 20.0f);
                 r.y = db_of(r.y, a.log_amin, 1e-18f, 20.0f);
                 r.z = db_of(r.z, a.log_amin, 1e-18f, 20.0f);
                 r.w = db_of(r.w, a.log_amin, 1e-18f, 20.0f);
             }
-            if (valid) *reinterpret_cast<float4*>(out + 4 * j) = r;
+            if (valid) *reinterpret_cast<float4*>(out + 4 * lj) = r;
         }
     } else {
-        for (int m = j; m < n_mels; m += L) {
+        for (int m = lj; m < n_mels; m += L) {
             const float v = mo[m];
             if (valid) st_out(out + m, db ? db_of(v, a.log_amin, 1e-18f, 20.0f) : v);
         }
@@ -255,7 +280,7 @@ stft5_kernel(StftLaunch a, uint64_t fps, int rs) {
     extern __shared__ __attribute__((aligned(16))) float lds[];
     float* wtl = lds;
     float2* twtab = reinterpret_cast<float2*>(lds + G::WL_FLOATS);
-    float* work = lds + G::WL_FLOATS + G::TW_FLOATS;
+    float* work = lds + G::TAB_FLOATS;
     // mel tables: the packed stream (meta rows, then weight rows) or the rounds' chunk stream
     const bool packed = OK == 2 && a.melp_chunks > 0;
     float4* mel_lds = reinterpret_cast<float4*>(lds + G::TAB_FLOATS + G::STREAMS * rs);
@@ -264,6 +289,9 @@ stft5_kernel(StftLaunch a, uint64_t fps, int rs) {
     int* k0_lds = reinterpret_cast<int*>(mel_lds + (OK == 2 && !packed ? a.mel4_rows * L : 0));
     int2* rd_lds = reinterpret_cast<int2*>(k0_lds + (OK == 2 && !packed ? a.mel4_rounds * L : 0));
     int* xo_lds = reinterpret_cast<int*>(rd_lds + (OK == 2 && !packed ? a.mel4_rounds : 0));
+#if THESIA_SC5 == 2
+    float2* sct_lds = reinterpret_cast<float2*>(lds + G::WL_FLOATS + G::TW_FLOATS);
+#endif
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int slot = lane / L, j = lane % L;
     const bool lane0 = j == 0;
@@ -291,7 +319,16 @@ stft5_kernel(StftLaunch a, uint64_t fps, int rs) {
     }
     // untangle bases: slots 0..7 start at bin kb_lo (lane 0: 32), slots 8..15 at bin j
     float2 ub_lo = a.sincos[lane0 ? 32 : j], ub_hi = a.sincos[j];
-#if THESIA_SC5
+#if THESIA_SC5 == 2
+    if (threadIdx.x < L)
+        static_for<0, 16>([&](auto ic) {
+            constexpr int i = decltype(ic)::value;
+            float sv, cv;
+            rot16<i>(i < 8 ? ub_lo : ub_hi, sv, cv);
+            sct_lds[i * L + j] = make_float2(sv, cv);
+        });
+    const RotLds rot{sct_lds + j};
+#elif THESIA_SC5
     float2 sct[16];
     static_for<0, 16>([&](auto ic) {
         constexpr int i = decltype(ic)::value;
@@ -304,18 +341,28 @@ stft5_kernel(StftLaunch a, uint64_t fps, int rs) {
 
     const uint64_t total = a.total_frames;
     const uint64_t stream = ((uint64_t)blockIdx.x * G::WV + wave) * FPW + slot;
-    const uint64_t g0 = stream * fps;
-    const uint64_t g1 = g0 + fps < total ? g0 + fps : total;
+#if THESIA_S32  // 32-bit frame / sample words (total frames < 2^32, tracks < 2^31 samples)
+    using FI = uint32_t;
+    using SI = int32_t;
+#else
+    using FI = uint64_t;
+    using SI = int64_t;
+#endif
+    const FI g0 = (FI)(stream * fps);
+    const FI g1 = (FI)(stream * fps + fps < total ? stream * fps + fps : total);
     const int hop = a.hop;
     float* region = work + (wave * FPW + slot) * rs;
     const ET* in = static_cast<const ET*>(a.in);
 
     float2 raw[P];
     CT pre[SH];
+    constexpr bool kDma = THESIA_DMA5 && C == 2 && INF == IN_F32;
+    float* wave_area = work + wave * FPW * rs;  // the wave's two stream regions, contiguous
     bool pre_ok = false;
     int hint = -1;
-    uint64_t g_beg = 1, g_end = 0, base = 0;
-    int64_t n = 0;
+    FI g_beg = 1, g_end = 0;
+    uint64_t base = 0;
+    SI n = 0;
 #ifdef THESIA_STAMPS
     unsigned long long st_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     unsigned long long st_last;
@@ -326,7 +373,7 @@ stft5_kernel(StftLaunch a, uint64_t fps, int rs) {
         // / mel / stores at 2
         __builtin_amdgcn_s_setprio(0);
         MARK5(top, 7);
-        const uint64_t g = g0 + it;
+        const FI g = g0 + (FI)it;
         const bool valid = g < g1;
 #if !THESIA_SC5
         asm volatile("" : "+v"(ub_lo.x), "+v"(ub_lo.y), "+v"(ub_hi.x), "+v"(ub_hi.y));
@@ -337,23 +384,39 @@ stft5_kernel(StftLaunch a, uint64_t fps, int rs) {
         int wj = j, wjb = jb, wkb = kb_lo;
         asm volatile("" : "+v"(wj), "+v"(wjb), "+v"(wkb));
         const float4* wrow = reinterpret_cast<const float4*>(wtl + wj * G::WL_STRIDE);
-        int64_t start = 0;
+        SI start = 0;
         if (valid) {
             if (g >= g_end || g < g_beg) {
                 hint = find_track(a.trk_frame0, a.n_tracks, g, hint);
-                g_beg = a.trk_frame0[hint];
-                g_end = a.trk_frame0[hint + 1];
-                n = (int64_t)a.trk_len[hint];
+                g_beg = (FI)a.trk_frame0[hint];
+                g_end = (FI)a.trk_frame0[hint + 1];
+                n = (SI)a.trk_len[hint];
                 base = a.trk_in_off[hint];
             }
-            start = (int64_t)(g - g_beg) * hop - NC;  // half_win = NC, pad_left = 0
+            start = (SI)(g - g_beg) * hop - NC;  // half_win = NC, pad_left = 0
         }
         // ---- the frame's raw samples: shift by SH points + the prefetched hop ----
+        if constexpr (kDma) {  // the hop landed in the wave's regions by LDS-DMA: into the ring first
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            if (pre_ok) {
+#pragma unroll
+                for (int q = 0; q < SH; ++q) pre[q] = reinterpret_cast<const CT*>(wave_area + q * 256)[lane];
+#pragma unroll
+                for (int n1 = 0; n1 < P - SH; ++n1) raw[n1] = raw[n1 + SH];
+#pragma unroll
+                for (int q = 0; q < SH; ++q) raw[P - SH + q] = CK::mix(pre[q]);
+            }
+            // the other stream's lanes may refill their region below (generic loads): their
+            // writes must not pass these reads (a cross-lane hazard the per-thread model misses)
+            wave_lds_sync();
+        }
         if (pre_ok) {
+            if constexpr (!kDma) {
 #pragma unroll
-            for (int n1 = 0; n1 < P - SH; ++n1) raw[n1] = raw[n1 + SH];
+                for (int n1 = 0; n1 < P - SH; ++n1) raw[n1] = raw[n1 + SH];
 #pragma unroll
-            for (int q = 0; q < SH; ++q) raw[P - SH + q] = CK::mix(pre[q]);
+                for (int q = 0; q < SH; ++q) raw[P - SH + q] = CK::mix(pre[q]);
+            }
         } else if (valid && start >= 0 && start + 2 * NC <= n && ((base + (uint64_t)start * C) % (2 * C)) == 0) {
             const CT* src = reinterpret_cast<const CT*>(in + base + (uint64_t)start * C) + j;
             static_for<0, P / 8>([&](auto gc) {
@@ -375,14 +438,25 @@ stft5_kernel(StftLaunch a, uint64_t fps, int rs) {
         // after the window at 2 waves/SIMD (a whole frame to land, as stft3), after the
         // untangle at 3 (register budget) ----
         auto prefetch = [&]() {
-            const int64_t nstart = start + hop;
+            const SI nstart = start + hop;
             const bool nxt = valid && g + 1 < g1 && g + 1 < g_end && nstart + 2 * NC <= n &&
                              nstart + 2 * L * (P - SH) >= 0 &&
                              ((base + (uint64_t)(nstart + 2 * L * (P - SH)) * C) % (2 * C)) == 0;
             if (nxt) {
                 const CT* src = reinterpret_cast<const CT*>(in + base + (uint64_t)(nstart + 2 * L * (P - SH)) * C) + j;
+                if constexpr (kDma) {
+                    // lane l of the wave lands at byte 16 l of each 1 KiB block: stream s's 32
+                    // lanes fill bytes [512 s, 512 s + 512); the regions' last reads are done
+                    wave_lds_sync();
 #pragma unroll
-                for (int q = 0; q < SH; ++q) pre[q] = src[L * q];
+                    for (int q = 0; q < SH; ++q)
+                        __builtin_amdgcn_global_load_lds(
+                            (__attribute__((address_space(1))) void*)(src + L * q),
+                            (__attribute__((address_space(3))) void*)(wave_area + q * 256), 16, 0, 0);
+                } else {
+#pragma unroll
+                    for (int q = 0; q < SH; ++q) pre[q] = src[L * q];
+                }
             }
             pre_ok = nxt;
         };
