@@ -66,6 +66,8 @@ def parse():
                    "of kernel ids (interleaved rounds, one process), e.g. 3,5")
     p.add_argument("--mel-paths", default="", help="A/B of stft5's mel projections (THESIA_BATCH_OPT_MEL_PATH): "
                    "comma list, e.g. 1,2,3 (interleaved rounds, one process)")
+    p.add_argument("--render-paths", default="", help="c5: A/B of the display launch structures "
+                   "(thesia_set_render_path), comma list, interleaved rounds")
     p.add_argument("--selftest", action="store_true",
                    help="launcher / reduction plumbing only: no GPU, no thesia (CPU tests)")
     p.add_argument("--selftest-fail-rank", type=int, default=-1, help=argparse.SUPPRESS)
@@ -388,6 +390,18 @@ def main_c5(args, ws, rank, pg, device):
     # spectrogram kernels alone (HIP events per group launch)
     kms = sum(b.run_timed(3) / 3 for _, _, _, b in p.groups)
     disp = p.display_timed(3)
+    if args.render_paths:
+        import numpy as np
+        rp = [int(v) for v in args.render_paths.split(",")]
+        res = {q: [] for q in rp}
+        for _ in range(5):  # interleaved rounds
+            for q in rp:
+                engine.set_render_path(q)
+                res[q].append(p.display_timed(3)["display_ms"])
+        engine.set_render_path(0)
+        if rank == 0:
+            print(json.dumps({"render_paths_ms": {str(q): {"median": float(np.median(t)), "min": float(min(t))}
+                                                  for q, t in res.items()}}), flush=True)
     in_bytes = sum(t.pcm.nbytes for t in tracks)
     out_bytes = sum(b.total_frames * pl.row_bins * 4 for pl, _, _, b in p.groups)
     achieved = (in_bytes + out_bytes) / (kms * 1e-3) / 1e9

@@ -924,8 +924,11 @@ int launch_render_batch2(const float* spec, uint32_t bins, float max, float min,
     hipLaunchKernelGGL(grey_vert_kernel, g1, dim3(256), lds1, s, spec, bins, max, min, nh, d_desc, tmp,
                        tile_cap, kv, v_band);
     // K5h + K6: the three-stage path's horizontal pass (same intermediate layout [nh][T])
-    const uint32_t ry_h = THESIA_RYH;
-    dim3 g3((nw_max + 255) / 256, nh < ry_h ? nh : ry_h, n);
+    // row blocks per image: THESIA_RYH, more when few images would leave CUs idle
+    uint32_t ry_h = THESIA_RYH;
+    const uint32_t nxb = (nw_max + 255) / 256;
+    while (ry_h < 128 && (uint64_t)nxb * ry_h * n < 4096) ry_h *= 2;
+    dim3 g3(nxb, nh < ry_h ? nh : ry_h, n);
     // register weights up to THESIA_HKT_MAX taps (a downsampling group's 20-48 taps as an LDS
     // weight table took 44 KiB per block: two blocks per CU); more taps: the LDS table
     const int kt = h_taps <= 16 ? 16 : h_taps <= 32 && THESIA_HKT_MAX >= 32 ? 32
