@@ -259,11 +259,13 @@ int thesia_minmax_segments_device(const float* d_spec, const uint64_t* row0, siz
                                   size_t n, float* max, float* min, int* has_nan);
 /* Process-wide choice of the batched display path's launch structure (all byte-identical):
  * 0 = the fused path (default): per geometry group one kernel for grey + vertical Lanczos3 in
- * one pass over the spectrogram, then one for horizontal Lanczos3 + colormap, every track of a
- * call in each launch; 1 = per-track launches (the reference's one image at a time structure);
- * 2 = every track in one launch per stage: grey, vertical, horizontal + colormap; 3 = one
- * kernel per group for the whole display (the intermediate in LDS) where the group's tiles
- * fit, else as 0 (measured slower on C5: kept selectable and parity-tested). */
+ * one pass over the spectrogram, then one for horizontal Lanczos3 + colormap (row spans staged
+ * by LDS-DMA), every track of a call in each launch; 1 = per-track launches (the reference's one
+ * image at a time structure); 2 = every track in one launch per stage: grey, vertical,
+ * horizontal + colormap; 3 = one kernel per group for the whole display (the intermediate in
+ * LDS) where the group's tiles fit, else as 0; 4 = as 0 with the previous register-staged
+ * horizontal pass (3 and 4 measured slower on C5: kept selectable and parity-tested,
+ * DESIGN.md §4). */
 int thesia_set_render_path(int path);
 int thesia_render_rgb_batch_device(const float* d_spec, const uint64_t* row0, size_t bins,
                                    size_t n, const float* up_ratio, const uint32_t* nwidth,

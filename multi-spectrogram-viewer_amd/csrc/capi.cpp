@@ -475,7 +475,7 @@ int thesia_render_rgb_multi(size_t n_groups, const float* const* d_specs, const 
         tot += ns[k];
     }
     if (tot && (!up_ratio || !nwidth || !d_rgb || !rgb_off)) return set_error(THESIA_ERR_INVALID_ARG, "null pointer");
-    if (render_path() == 0 || render_path() == 3)
+    if (render_path() == 0 || render_path() >= 3)
         return render_rgb_fused(n_groups, d_specs, row0s, bins, ns, up_ratio, nwidth, nheight, max, min,
                                 d_rgb, rgb_off, default_stream());
     size_t t0 = 0;

@@ -903,6 +903,128 @@ __global__ void __launch_bounds__(256) grey_vert_kernel(const float* spec, uint3
     }
 }
 
+// The horizontal pass with its row spans staged by LDS-DMA (global_load_lds_dwordx4, no VGPRs):
+// NB row buffers per block, NB - 1 rows in flight while a row is summed, one barrier per row.
+// A block owns 256 output columns of one image (thread = column, <= KT zero-padded register
+// weights: n <= KT for every column of the launch) and walks its rows (blockIdx.y-strided). Row
+// k's span [lb4, lb4 + span4) (16-byte aligned) lands in buffer k % NB: wave w issues the chunks
+// (m * 4 + w) * 64 + lane, m < K; chunks past the span re-read the span's last chunk (finite
+// values in the buffer's tail, summed with zero weights: bits unchanged, as in the staged pass;
+// the intermediate's row padding is zeroed when its workspace is allocated). Each wave waits for
+// its own chunks of row k (a counted vmcnt: the only vector-memory ops after them are the next
+// NB - 2 rows' K chunks and this wave's byte stores, which only add to the count), then the
+// barrier makes the whole row visible and frees the buffer of row k - 1 for row k + NB - 1.
+// Same sums and colormap as resize_h_rgb_batch_kernel (identical bytes).
+template <int N>
+__device__ __forceinline__ void wait_vm() {
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+template <int KT, int K, int NB>
+__global__ void __launch_bounds__(256) resize_h_dma_kernel(uint32_t nh, const RenderDesc* d, const float* tmp,
+                                                           const uint8_t* cmap, uint8_t* rgb) {
+    extern __shared__ __attribute__((aligned(16))) float hsm[];
+    constexpr int BUF = K * 1024;  // floats per row buffer: K chunks of 64 lanes x 16 B per wave
+    uint8_t* cm = reinterpret_cast<uint8_t*>(hsm + NB * BUF);
+    const RenderDesc r = d[blockIdx.z];
+    const uint32_t ox0 = blockIdx.x * 256;
+    if (ox0 >= r.nw) return;  // block-uniform
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    if (tid < 30) cm[tid] = cmap[tid];
+    const uint32_t ox = ox0 + tid;
+    const bool act = ox < r.nw;
+    int32_t l = 0, n = 0;
+    const float* wr = r.hw;
+    if (act) {
+        l = r.hl[ox];
+        n = r.hc[ox];
+        wr = r.hw + r.ho[ox];
+    }
+    float w[KT];
+#pragma unroll
+    for (int i = 0; i < KT; ++i) w[i] = i < n ? wr[i] : 0.0f;
+    const uint32_t npx = r.nw - ox0 < 256u ? r.nw - ox0 : 256u;
+    const int32_t lb4 = r.hl[ox0] & ~3;
+    const uint32_t last = ox0 + npx - 1;
+    const int32_t span4 = (r.hl[last] + r.hc[last] - lb4 + 3) & ~3;  // <= BUF - KT (host)
+    const int nchunk = span4 > 0 ? span4 >> 2 : 1;
+    const int base = l - lb4;
+    uint8_t* orgb = rgb + r.rgb_off + (uint64_t)ox * 3;
+    __syncthreads();  // colormap bytes
+    // rows below oz: their intermediate rows are +0 (never formed) -> colormap(+0)
+    const uint32_t G = gridDim.y;
+    uint32_t y0 = blockIdx.y;
+    if (r.oz > y0) {
+        uint8_t px[3];
+        colormap_px(0.0f, cm, px);
+        for (; y0 < r.oz && y0 < nh; y0 += G)
+            if (act) {
+                uint8_t* o = orgb + (uint64_t)y0 * r.nw * 3;
+                o[0] = px[0]; o[1] = px[1]; o[2] = px[2];
+            }
+    }
+    const int nrows = y0 < nh ? (int)((nh - 1 - y0) / G) + 1 : 0;
+    const float* rows0 = tmp + r.tmp_off + lb4;
+    auto dma = [&](int k) {
+        const float* row = rows0 + (uint64_t)(y0 + G * (uint32_t)k) * r.ts;
+        float* buf = hsm + (k % NB) * BUF;
+#pragma unroll
+        for (int m = 0; m < K; ++m) {
+            const int c = (m * 4 + wave) * 64 + lane;
+            const int cc = c < nchunk ? c : nchunk - 1;
+            __builtin_amdgcn_global_load_lds((__attribute__((address_space(1))) void*)(row + 4 * cc),
+                                             (__attribute__((address_space(3))) void*)(buf + (m * 4 + wave) * 256),
+                                             16, 0, 0);
+        }
+    };
+    for (int k = 0; k < NB - 1 && k < nrows; ++k) dma(k);
+    for (int k = 0; k < nrows; ++k) {
+        if (k + NB - 2 < nrows) wait_vm<(NB - 2) * K>();
+        else wait_vm<0>();
+        __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");
+        if (k + NB - 1 < nrows) dma(k + NB - 1);
+        if (act) {
+            const float* rin = hsm + (k % NB) * BUF + base;
+            float t = 0.0f;
+#pragma unroll
+            for (int i = 0; i < KT; ++i) t += rin[i] * w[i];
+            uint8_t px[3];
+            colormap_px(t, cm, px);
+            uint8_t* o = orgb + (uint64_t)(y0 + G * (uint32_t)k) * r.nw * 3;
+            o[0] = px[0]; o[1] = px[1]; o[2] = px[2];
+        }
+    }
+}
+
+extern int g_h_dma;
+// the LDS-DMA horizontal pass for a launch (h_taps <= 48, span + taps <= 4 096 floats), else -2
+static int launch_resize_h_dma(uint32_t nh, const RenderDesc* d_desc, uint32_t n, uint32_t nw_max, int h_taps,
+                               int h_span, const float* tmp, const uint8_t* cmap, uint8_t* rgb, dim3 g3,
+                               hipStream_t s) {
+    const int kt = h_taps <= 16 ? 16 : h_taps <= 32 ? 32 : h_taps <= 48 ? 48 : 0;
+    if (!kt) return -2;
+    const int need = h_span + 4 + kt;
+    const int K = need <= 1024 ? 1 : need <= 2048 ? 2 : need <= 4096 ? 4 : 0;
+    if (!K) return -2;
+    constexpr int NB = 4;  // row buffers (3 and 6 measured slower: 3.40 / 3.42 vs 3.36 ms per C5 step)
+    const int lds = NB * K * 1024 * 4 + 32;
+    const void* kern = nullptr;
+#define THESIA_HDMA(KT_, K_) \
+    if (kt == KT_ && K == K_) kern = reinterpret_cast<const void*>(resize_h_dma_kernel<KT_, K_, NB>);
+    THESIA_HDMA(16, 1) THESIA_HDMA(16, 2) THESIA_HDMA(16, 4)
+    THESIA_HDMA(32, 1) THESIA_HDMA(32, 2) THESIA_HDMA(32, 4)
+    THESIA_HDMA(48, 1) THESIA_HDMA(48, 2) THESIA_HDMA(48, 4)
+#undef THESIA_HDMA
+    if (hipFuncSetAttribute(kern, hipFuncAttributeMaxDynamicSharedMemorySize, lds) != hipSuccess) return -1;
+    void* args[] = {&nh, &d_desc, &tmp, &cmap, &rgb};
+    if (hipLaunchKernel(kern, g3, dim3(256), args, lds, s) != hipSuccess) return -1;
+    (void)n;
+    (void)nw_max;
+    return 0;
+}
+
+int g_h_dma = 1;  // the LDS-DMA horizontal pass: 0 off (render path 4)
+
 int launch_render_batch2(const float* spec, uint32_t bins, float max, float min,
                          const RenderDesc* d_desc, uint32_t n, uint32_t T_max, uint32_t H_max,
                          uint32_t nw_max, uint32_t nh, int h_taps, int h_span, uint32_t v_band,
@@ -925,12 +1047,16 @@ int launch_render_batch2(const float* spec, uint32_t bins, float max, float min,
                        tile_cap, kv, v_band);
     // K5h + K6: the three-stage path's horizontal pass (same intermediate layout [nh][T])
     // row blocks per image: THESIA_RYH, more when few images would leave CUs idle
-    uint32_t ry_h = THESIA_RYH;
+    uint32_t ry_h = THESIA_RYH;  // (8 rows blocks: same time with the LDS-DMA pass; 32: +4 %)
     const uint32_t nxb = (nw_max + 255) / 256;
     while (ry_h < 128 && (uint64_t)nxb * ry_h * n < 4096) ry_h *= 2;
     dim3 g3(nxb, nh < ry_h ? nh : ry_h, n);
     // register weights up to THESIA_HKT_MAX taps (a downsampling group's 20-48 taps as an LDS
     // weight table took 44 KiB per block: two blocks per CU); more taps: the LDS table
+    if (g_h_dma) {
+        const int rc = launch_resize_h_dma(nh, d_desc, n, nw_max, h_taps, h_span, tmp, cmap, rgb, g3, s);
+        if (rc != -2) return rc;
+    }
     const int kt = h_taps <= 16 ? 16 : h_taps <= 32 && THESIA_HKT_MAX >= 32 ? 32
                  : h_taps <= 48 && THESIA_HKT_MAX >= 48 ? 48 : 16;
     int taps = h_taps > kt ? h_taps : 0;

@@ -866,7 +866,7 @@ int minmax_device(const float* d_x, uint64_t n, float* mx, float* mn, bool* nan,
 static int g_render_path = 0;  // thesia_set_render_path
 int render_path() { return __atomic_load_n(&g_render_path, __ATOMIC_RELAXED); }
 int set_render_path(int path) {
-    if (path < 0 || path > 3) return set_error(THESIA_ERR_INVALID_ARG, "render path must be 0, 1, 2 or 3");
+    if (path < 0 || path > 4) return set_error(THESIA_ERR_INVALID_ARG, "render path must be 0 .. 4");
     __atomic_store_n(&g_render_path, path, __ATOMIC_RELAXED);
     return THESIA_OK;
 }
@@ -1170,6 +1170,7 @@ int plan_fused_group(const float* d_spec, const uint64_t* row0, size_t bins, siz
 
 }  // namespace
 
+extern int g_h_dma;
 int render_rgb_fused(size_t n_groups, const float* const* d_specs, const uint64_t* const* row0s,
                      const size_t* bins, const size_t* ns, const float* up_ratio,
                      const uint32_t* nwidth, uint32_t nheight, float max, float min, uint8_t* d_rgb,
@@ -1231,15 +1232,22 @@ int render_rgb_fused(size_t n_groups, const float* const* d_specs, const uint64_
             b.release();
             return b.alloc(bytes + bytes / 8);
         };
+        const void* tmp_before = ws.tmp.p;
         rc = grow(ws.tmp, tmp_max * sizeof(float));
         if (!rc) rc = grow(ws.desc, std::max<size_t>(desc.size(), 1) * sizeof(RenderDesc));
         if (rc) return rc;
+        // the intermediate rows' padding [T, ts) is never written by the vertical pass: zero it
+        // once per allocation, so every float a horizontal pass may stage is finite
+        if (ws.tmp.p != tmp_before) THESIA_HIP(hipMemsetAsync(ws.tmp.p, 0, ws.tmp.bytes, s));
         if (!desc.empty())
             THESIA_HIP(copy_ordered(ws.desc.p, desc.data(), desc.size() * sizeof(RenderDesc), hipMemcpyHostToDevice));
         ws.groups = std::move(groups);
         ws.key = std::move(key);
     }
     const std::vector<FusedGroup>& groups = ws.groups;
+    // the horizontal pass: LDS-DMA row staging (display_kernels.hip resize_h_dma_kernel); path 4
+    // = the register-staged pass it replaced (kept for A/B, byte-identical)
+    g_h_dma = rpath == 4 ? 0 : 1;
     for (const FusedGroup& g : groups)
         for (size_t b = 0; b < g.ndesc; b += 65535) {  // grid.z limit
             const uint32_t nb = (uint32_t)std::min<size_t>(65535, g.ndesc - b);
@@ -1314,7 +1322,7 @@ int render_rgb_batch_device(const float* d_spec, const uint64_t* row0, size_t bi
     int crc = 0;
     const uint8_t* cmap_ptr = colormap_device(&crc);
     if (crc) return crc;
-    if (render_path() == 0 || render_path() == 3) {
+    if (render_path() == 0 || render_path() >= 3) {
         const size_t ns[1] = {n};
         const size_t bs[1] = {bins};
         return render_rgb_fused(1, &d_spec, &row0, bs, ns, up_ratio, nwidth, nheight, max, min, d_rgb,
