@@ -164,6 +164,12 @@ int thesia_batch_output_bytes(const thesia_batch* batch, uint64_t* bytes);
 /* One pass of the hot path over the whole batch on `stream` (a hipStream_t; NULL => the
  * library's stream of the current device). Asynchronous. */
 int thesia_batch_run(thesia_batch* batch, void* stream);
+/* One pass of each of n batches (e.g. one per geometry group of a multi-rate track set), spread
+ * over the library's internal streams of the current device and joined back to `stream` (NULL
+ * => the library stream): the same results as n thesia_batch_run calls, with the launches
+ * overlapping. Not part of the reference surface (its per-track loop is lib.rs:161-166).
+ * Asynchronous. */
+int thesia_batches_run(thesia_batch* const* batches, size_t n, void* stream);
 /* Runs `iters` passes bracketed by HIP events on the launch stream; returns the elapsed
  * milliseconds of all passes (synchronous). */
 int thesia_batch_run_timed(thesia_batch* batch, void* stream, int iters, float* ms);

@@ -278,6 +278,14 @@ int thesia_batch_run(thesia_batch* batch, void* stream) {
     return batch_run(reinterpret_cast<Batch*>(batch), static_cast<hipStream_t>(stream));
     GUARD_END
 }
+int thesia_batches_run(thesia_batch* const* batches, size_t n, void* stream) {
+    GUARD_BEGIN
+    if (n && !batches) return set_error(THESIA_ERR_INVALID_ARG, "null batches");
+    for (size_t i = 0; i < n; ++i)
+        if (!batches[i]) return set_error(THESIA_ERR_INVALID_ARG, "null batch");
+    return batches_run(reinterpret_cast<Batch* const*>(batches), n, static_cast<hipStream_t>(stream));
+    GUARD_END
+}
 int thesia_batch_run_timed(thesia_batch* batch, void* stream, int iters, float* ms) {
     GUARD_BEGIN
     if (!batch || iters < 1) return set_error(THESIA_ERR_INVALID_ARG, "bad argument");

@@ -815,6 +815,43 @@ int batch_run(Batch* b, hipStream_t s) {
     return THESIA_OK;
 }
 
+// Several batches (e.g. one per geometry group) on up to kRunStreams library streams of the
+// device, forked from and joined back to `s`: a small launch's ramp (the first frame of every
+// stream loaded without prefetch, the tables staged into LDS) overlaps the others' work.
+// Stream-ordered on `s` like batch_run.
+int batches_run(Batch* const* b, size_t n, hipStream_t s) {
+    if (!s) s = default_stream();
+    if (n <= 1) return n ? batch_run(b[0], s) : THESIA_OK;
+    constexpr int kRunStreams = 4;
+    struct Pool {
+        hipStream_t st[kRunStreams] = {};
+        hipEvent_t fork = nullptr, join[kRunStreams] = {};
+    };
+    static std::mutex mu;
+    static auto& pools = *new std::map<int, Pool>();  // leaked, see dev_taps
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    std::lock_guard<std::mutex> lk(mu);
+    Pool& p = pools[dev];
+    if (!p.fork) {
+        for (int i = 0; i < kRunStreams; ++i) {
+            THESIA_HIP(hipStreamCreateWithFlags(&p.st[i], hipStreamNonBlocking));
+            THESIA_HIP(hipEventCreateWithFlags(&p.join[i], hipEventDisableTiming));
+        }
+        THESIA_HIP(hipEventCreateWithFlags(&p.fork, hipEventDisableTiming));
+    }
+    const int k = (int)std::min<size_t>(kRunStreams, n);
+    THESIA_HIP(hipEventRecord(p.fork, s));
+    for (int i = 0; i < k; ++i) THESIA_HIP(hipStreamWaitEvent(p.st[i], p.fork, 0));
+    int rc = THESIA_OK;
+    for (size_t i = 0; i < n && !rc; ++i) rc = batch_run(b[i], p.st[i % k]);
+    for (int i = 0; i < k; ++i) {  // join even after an error: `s` never runs ahead of them
+        THESIA_HIP(hipEventRecord(p.join[i], p.st[i]));
+        THESIA_HIP(hipStreamWaitEvent(s, p.join[i], 0));
+    }
+    return rc;
+}
+
 // host side of Batch::range: {ord max, ord min, NaN} -> (max, min, NaN) per track
 int ranges_read(const int* d_range, size_t n, float* mx, float* mn, int* nan, hipStream_t s) {
     if (n == 0) return THESIA_OK;

@@ -78,6 +78,7 @@ _SIGS = {
     "thesia_batch_frames": (_i, [_vp, _u64p, _u64p]),
     "thesia_batch_output_bytes": (_i, [_vp, _u64p]),
     "thesia_batch_run": (_i, [_vp, _vp]),
+    "thesia_batches_run": (_i, [_vp, C.c_size_t, _vp]),
     "thesia_batch_run_timed": (_i, [_vp, _vp, _i, _fp]),
     "thesia_batch_kernel_info": (_i, [_vp, C.POINTER(_i), C.POINTER(_i), C.POINTER(_i)]),
     "thesia_synth_pcm_device": (_i, [_vp, _i, _u32, _u64, _u64, _u32, _u64]),

@@ -230,6 +230,13 @@ def ranges_read(d_range: "DeviceBuffer", n: int, offset_tracks: int = 0):
     return mx, mn, nan
 
 
+def run_batches(batches, stream=None) -> None:
+    """One pass of every batch, the launches spread over the library's streams and joined back
+    to `stream` (thesia_batches_run): the results of calling run() on each."""
+    arr = (C.c_void_p * max(len(batches), 1))(*[b.handle.value for b in batches])
+    check(lib.thesia_batches_run(arr, len(batches), stream))
+
+
 def set_render_path(path: int) -> None:
     """0: batched display launches (default); 1: per-track launches (cross-check)."""
     check(lib.thesia_set_render_path(path))

@@ -115,9 +115,9 @@ class RenderPipeline:
         self._max_sr = max((t.sr for t in self.tracks), default=0)
 
     def run_spectrograms(self) -> None:
-        """One kernel launch per geometry group (asynchronous)."""
-        for _, _, _, b in self.groups:
-            b.run()
+        """One kernel launch per geometry group, the launches overlapped on the library's
+        streams (thesia_batches_run; asynchronous, ordered before later library calls)."""
+        engine.run_batches([b for _, _, _, b in self.groups])
 
     def _spec_ptr(self, i):
         g, row0, T, bins = self.where[i]
