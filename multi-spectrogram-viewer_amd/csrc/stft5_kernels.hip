@@ -4,8 +4,7 @@
 // Same contract and the same streaming register ring as stft3_kernel (stft3_kernels.hip: each
 // wave runs two frame streams on its 32-lane halves; a stream's downmixed samples stay in
 // registers and a hop loads only its new samples). What changes is the second FFT stage, so
-// that the realfft untangle (realfft.rs:140-157) needs no cross-lane exchange, and with it the
-// register budget, so that THREE waves share a SIMD (168 VGPRs) instead of two:
+// that the realfft untangle (realfft.rs:140-157) needs no cross-lane exchange:
 //
 //   NC = 32 x 32. Stage 1 (lane j = n2): Y[j][k1] = DFT-32 over n1 of z[32 n1 + j], times
 //   W_1024^{j k1}; LDS transpose. In stft3, lane j then runs the DFT-32 of column k1 = j and
@@ -19,10 +18,12 @@
 //   Lane 0 (A = B = 0) pairs its own outputs differently (O with O, E with E, E[0] and E[8]
 //   with themselves: bins 0, NC and NC/2); per-slot selects cover it, as in stft3.
 //
-// Registers: no partner batch (32 VGPRs in stft3), the stage-1 twiddles read 4 float4 at a
-// time, the next hop's loads issued after the transposes (when the frame's registers are at
-// their fewest), the sqrt batch per half frame: 3 waves per SIMD, 12 waves (24 streams) per
-// CU. The two frames of a wave keep their LDS regions on opposite halves of the 64 banks.
+// Occupancy: the product build runs two waves per SIMD (8-wave blocks, 253 VGPRs: the ring,
+// the frame's points, the prefetched hop and the per-lane untangle rotations). Three waves
+// (12-wave blocks, <= 168 VGPRs) compile without spills only with the hop prefetched by
+// LDS-DMA and the rotations in LDS (THESIA_WV5=12 THESIA_DMA5=1 THESIA_SC5=2 THESIA_S32=1 ...),
+// and measured slower. The two frames of a wave keep their LDS regions on
+// opposite halves of the 64 banks.
 #include "stft3_core.hpp"
 
 #include <type_traits>
