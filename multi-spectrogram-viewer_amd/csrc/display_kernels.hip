@@ -996,7 +996,6 @@ __global__ void __launch_bounds__(256) resize_h_dma_kernel(uint32_t nh, const Re
     }
 }
 
-extern int g_h_dma;
 // the LDS-DMA horizontal pass for a launch (h_taps <= 48, span + taps <= 4 096 floats), else -2
 static int launch_resize_h_dma(uint32_t nh, const RenderDesc* d_desc, uint32_t n, uint32_t nw_max, int h_taps,
                                int h_span, const float* tmp, const uint8_t* cmap, uint8_t* rgb, dim3 g3,
@@ -1023,13 +1022,11 @@ static int launch_resize_h_dma(uint32_t nh, const RenderDesc* d_desc, uint32_t n
     return 0;
 }
 
-int g_h_dma = 1;  // the LDS-DMA horizontal pass: 0 off (render path 4)
-
 int launch_render_batch2(const float* spec, uint32_t bins, float max, float min,
                          const RenderDesc* d_desc, uint32_t n, uint32_t T_max, uint32_t H_max,
                          uint32_t nw_max, uint32_t nh, int h_taps, int h_span, uint32_t v_band,
                          int v_rows, int v_kv, float* tmp, const uint8_t* cmap, uint8_t* rgb,
-                         hipStream_t s) {
+                         hipStream_t s, bool h_dma) {
     if (n == 0 || nh == 0 || v_band == 0) return 0;
     if (n > 65535) return -2;
     (void)H_max;
@@ -1053,7 +1050,7 @@ int launch_render_batch2(const float* spec, uint32_t bins, float max, float min,
     dim3 g3(nxb, nh < ry_h ? nh : ry_h, n);
     // register weights up to THESIA_HKT_MAX taps (a downsampling group's 20-48 taps as an LDS
     // weight table took 44 KiB per block: two blocks per CU); more taps: the LDS table
-    if (g_h_dma) {
+    if (h_dma) {
         const int rc = launch_resize_h_dma(nh, d_desc, n, nw_max, h_taps, h_span, tmp, cmap, rgb, g3, s);
         if (rc != -2) return rc;
     }

@@ -1207,7 +1207,6 @@ int plan_fused_group(const float* d_spec, const uint64_t* row0, size_t bins, siz
 
 }  // namespace
 
-extern int g_h_dma;
 int render_rgb_fused(size_t n_groups, const float* const* d_specs, const uint64_t* const* row0s,
                      const size_t* bins, const size_t* ns, const float* up_ratio,
                      const uint32_t* nwidth, uint32_t nheight, float max, float min, uint8_t* d_rgb,
@@ -1284,7 +1283,7 @@ int render_rgb_fused(size_t n_groups, const float* const* d_specs, const uint64_
     const std::vector<FusedGroup>& groups = ws.groups;
     // the horizontal pass: LDS-DMA row staging (display_kernels.hip resize_h_dma_kernel); path 4
     // = the register-staged pass it replaced (kept for A/B, byte-identical)
-    g_h_dma = rpath == 4 ? 0 : 1;
+    const bool h_dma = rpath != 4;
     for (const FusedGroup& g : groups)
         for (size_t b = 0; b < g.ndesc; b += 65535) {  // grid.z limit
             const uint32_t nb = (uint32_t)std::min<size_t>(65535, g.ndesc - b);
@@ -1297,7 +1296,7 @@ int render_rgb_fused(size_t n_groups, const float* const* d_specs, const uint64_
             }
             if (launch_render_batch2(g.spec, g.bins, max, min, ws.desc.as<RenderDesc>() + g.desc0 + b, nb,
                                      g.T_max, g.H_max, g.nw_max, nheight, g.h_taps, g.h_span, g.v_band,
-                                     g.v_rows, g.v_kv, ws.tmp.as<float>(), cmap_ptr, d_rgb, s))
+                                     g.v_rows, g.v_kv, ws.tmp.as<float>(), cmap_ptr, d_rgb, s, h_dma))
                 return set_error(THESIA_ERR_DEVICE, "render batch launch failed");
         }
     // stream-ordered: the images are complete for every later library call (copies included)

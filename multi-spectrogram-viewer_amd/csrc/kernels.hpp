@@ -187,7 +187,7 @@ int launch_render_batch2(const float* spec, uint32_t bins, float max, float min,
                          const RenderDesc* d_desc, uint32_t n, uint32_t T_max, uint32_t H_max,
                          uint32_t nw_max, uint32_t nh, int h_taps, int h_span, uint32_t v_band,
                          int v_rows, int v_kv, float* tmp, const uint8_t* cmap, uint8_t* rgb,
-                         hipStream_t s);
+                         hipStream_t s, bool h_dma = true);  // h_dma: the LDS-DMA horizontal pass
 // The fully fused display (grey + vertical + horizontal Lanczos3 + colormap, the intermediate in
 // LDS only): a block = R output rows x 64 columns of one track; kt register taps (16/32/48) for
 // the horizontal pass, kv padded vertical taps, s_cap / g_cap the largest frame span / grey-row
