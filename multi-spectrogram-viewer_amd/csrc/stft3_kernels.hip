@@ -376,11 +376,16 @@ static int launch3_k(const StftLaunch& a, hipStream_t stream) {
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
+#ifndef THESIA_WV3_SMALL
+#define THESIA_WV3_SMALL 12  // waves per block for mono linear kinds at n_fft <= 512 (3 per SIMD)
+#endif
 template <int NC, int C, int INF>
 static int launch3_c(const StftLaunch& a, hipStream_t s) {
+    // linear kinds of mono input at n_fft <= 512 fit 168 VGPRs without spills
+    constexpr int WVS = NC <= 256 && C == 1 ? THESIA_WV3_SMALL : kWaves;
     if (a.out_kind == OUT_COMPLEX) return launch3_k<NC, 0, C, INF>(a, s);
     if (a.out_kind == OUT_MEL || a.out_kind == OUT_MEL_AMP_DB) return launch3_k<NC, 2, C, INF>(a, s);
-    return launch3_k<NC, 1, C, INF>(a, s);
+    return launch3_k<NC, 1, C, INF, 0, WVS>(a, s);
 }
 
 template <int NC>
