@@ -741,6 +741,7 @@ int batch_set_option(Batch* b, int option, int64_t value) {
             else if (value == 9 && stftx_lds_bytes((int)b->plan->n_fft) <= 163840) b->kernel = 9;
             else return set_error(THESIA_ERR_UNSUPPORTED, "kernel " + std::to_string(value) +
                                                              " does not run this batch's geometry");
+            b->kernel_forced = value != 0;
             return THESIA_OK;
         case THESIA_BATCH_OPT_MAX_BLOCKS:
             if (value < 0 || value > (1 << 30)) return set_error(THESIA_ERR_INVALID_ARG, "max_blocks out of range");
@@ -755,6 +756,7 @@ int batch_set_option(Batch* b, int option, int64_t value) {
             if (value != 0 && b->launch.out_kind == OUT_COMPLEX)
                 return set_error(THESIA_ERR_INVALID_ARG, "ranges need real output rows");
             b->range = reinterpret_cast<int*>(value);
+            if (!b->kernel_forced) b->kernel = b->auto_kernel();  // the range decides stft3 vs stft5
             return THESIA_OK;
         case THESIA_BATCH_OPT_MEL_PATH: {
             if (value < 0 || value > 3) return set_error(THESIA_ERR_INVALID_ARG, "mel_path must be 0..3");

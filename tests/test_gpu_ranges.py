@@ -48,3 +48,32 @@ def test_range_option_rejects_complex_rows():
     b = engine.Batch(plan, din, np.zeros(1, np.uint64), [4096], dout)
     with pytest.raises(Exception):
         b.set_option(engine.OPT_RANGE, 1 << 20)
+
+
+def test_auto_kernel_follows_the_range_option():
+    """Mono linear rows at n_fft 2048 run stft5 by default (measured faster); with the range
+    option the automatic choice moves to stft3, which folds the ranges into its row epilogue;
+    a forced kernel stays. The ranges equal the rows' max / min either way."""
+    rng = np.random.default_rng(5)
+    lens = [48000, 30011, 2048 * 7 + 1]
+    x = np.concatenate([(rng.standard_normal(n) * 0.2).astype(np.float32) for n in lens])
+    offs = np.cumsum([0] + lens[:-1]).astype(np.uint64)
+    plan = engine.Plan(2048, 2048, 512, engine.OUT_AMP_DB, sr=48000)
+    T = engine.Batch.frames_for(plan, lens)
+    din = engine.DeviceBuffer.from_host(x)
+    outs = []
+    for forced in (0, 5):
+        dout = engine.DeviceBuffer(T * plan.row_bins * 4)
+        b = engine.Batch(plan, din, offs, lens, dout, kernel=forced)
+        assert b.kernel == 5
+        drange = engine.DeviceBuffer(12 * len(lens))
+        b.set_option(engine.OPT_RANGE, drange.ptr.value)
+        assert b.kernel == (3 if forced == 0 else 5)
+        b.run()
+        engine.synchronize()
+        mx, mn, nan = engine.ranges_read(drange, len(lens))
+        rows = dout.to_host(np.float32, (T, plan.row_bins))
+        for i in range(len(lens)):
+            r = rows[int(b.frame0[i]):int(b.frame0[i + 1])]
+            assert mx[i] == r.max() and mn[i] == r.min() and not nan[i]
+        outs.append(rows)
