@@ -317,15 +317,35 @@ def rfft_roofline(args, din, offs, lens, fmt, n_local, n_samples):
             "kernel": kname + ", complex output (downmix+frame+window+rFFT)"}
 
 
-def traffic_from_profile(workload_key):
+def profile_record(workload_key):
     path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     try:
         with open(path) as f:
-            d = json.load(f)
-        rec = d.get(workload_key)
-        return None if rec is None else rec.get("hbm_bytes_per_launch")
+            return json.load(f).get(workload_key) or {}
     except (OSError, ValueError):
+        return {}
+
+
+def traffic_from_profile(workload_key):
+    return profile_record(workload_key).get("hbm_bytes_per_launch")
+
+
+# VALU issue ceiling (MI355X_MICROARCH.md constants table): a wave64 v_fma_f32 occupies its
+# SIMD-32 for 2 cycles, 4 SIMDs per CU, 256 CUs, 2.4 GHz peak engine clock
+VALU_ISSUE_PEAK_G = 256 * 4 * 2.4e9 / 2 / 1e9  # wave-instructions per second, in G
+
+
+def issue_ceiling(workload_key, kms):
+    """The mel kernel's other roofline: its VALU wave-instructions per launch (a PMC constant of
+    the kernel and workload, profiles/pmc_traffic.json) over the live kernel time, against the
+    chip's VALU issue peak. DESIGN.md §7: the kernel is issue-bound, not HBM-bound."""
+    n = profile_record(workload_key).get("valu_insts_per_launch")
+    if n is None:
         return None
+    achieved = n / (kms * 1e-3) / 1e9
+    return {"bound": "valu-issue", "achieved": achieved, "peak": VALU_ISSUE_PEAK_G,
+            "unit": "G wave-instructions/s", "frac": achieved / VALU_ISSUE_PEAK_G,
+            "valu_insts_per_launch": n}
 
 
 def main_selftest(args, ws, rank, pg):
@@ -623,6 +643,9 @@ def main_worker(args):
             "kernel_ms": kms,
             "algorithmic_bytes_per_launch": abytes,
         }
+        ic = issue_ceiling(wkey, kms) if batch.kernel == 5 else None
+        if ic is not None:
+            result["roofline_valu_issue"] = ic
         if kind != engine.OUT_COMPLEX and not args.no_rfft_roofline:
             result["roofline_window_rfft"] = rfft_roofline(args, din, offs, lens, fmt, n_local, n_samples)
         if ws == 1 and not args.no_cpu_baseline:
