@@ -42,3 +42,19 @@ def test_single_process_without_launcher():
 def test_failing_worker_fails_the_launch():
     r = _run("--gpus", "2", "--selftest", "--selftest-fail-rank", "1")
     assert r.returncode != 0
+
+
+def test_profile_records_behind_the_bench_line():
+    """The default bench line's `roofline.traffic` and `roofline_valu_issue` come from the PMC
+    record of its workload (profiles/pmc_traffic.json); the issue roofline is that kernel's VALU
+    wave-instructions over the kernel time against 256 CUs x 4 SIMDs x 2.4 GHz / 2 cycles."""
+    sys.path.insert(0, ROOT)
+    import bench
+    key = "mel_db_f32_2ch_2048_512"  # bench.py defaults: output, input, channels, n_fft, hop
+    assert bench.traffic_from_profile(key) > 12.96e9  # >= the algorithmic bytes per launch
+    ic = bench.issue_ceiling(key, 4.0)
+    assert ic["bound"] == "valu-issue" and ic["peak"] == 1228.8
+    assert abs(ic["achieved"] - ic["valu_insts_per_launch"] / 4e-3 / 1e9) < 1e-9 * ic["achieved"]
+    assert abs(ic["frac"] - ic["achieved"] / ic["peak"]) < 1e-12
+    assert bench.issue_ceiling("no_such_workload", 4.0) is None
+    assert bench.traffic_from_profile("no_such_workload") is None
