@@ -66,6 +66,11 @@ def parse():
                    "of kernel ids (interleaved rounds, one process), e.g. 3,5")
     p.add_argument("--mel-paths", default="", help="A/B of stft5's mel projections (THESIA_BATCH_OPT_MEL_PATH): "
                    "comma list, e.g. 1,2,3 (interleaved rounds, one process)")
+    p.add_argument("--row-store", type=int, default=0,
+                   help="complex-output row store of the window+rFFT roofline (THESIA_BATCH_OPT_ROW_STORE: "
+                        "0 lane-wise 8-byte, 1 LDS-staged 16-byte, 2 whole 128-byte lines)")
+    p.add_argument("--row-stores", default="", help="A/B of the complex-output row stores (comma list, "
+                   "interleaved rounds, one process), reported in roofline_window_rfft")
     p.add_argument("--render-paths", default="", help="c5: A/B of the display launch structures "
                    "(thesia_set_render_path), comma list, interleaved rounds")
     p.add_argument("--selftest", action="store_true",
@@ -292,42 +297,98 @@ def algorithmic_bytes(args, n_tracks, n_samples, total_frames, row_bins):
     return n_tracks * n_samples * args.channels * in_el + total_frames * row_bins * out_el
 
 
+def hbm_ceiling(din, in_bytes, dout, out_bytes):
+    """The box's own ceiling for a kernel's read : write mix, measured in this process on the
+    kernel's own two buffers (thesia_hbm_ceiling: the input read once and the output written
+    once by a coalesced float4 copy, best of 3 x 2 grid sizes)."""
+    import ctypes as C
+    from thesia._lib import lib, check
+    ms, gbps = C.c_float(), C.c_float()
+    check(lib.thesia_hbm_ceiling(din.ptr, C.c_size_t(in_bytes), dout.ptr, C.c_size_t(out_bytes), 3,
+                                 C.byref(ms), C.byref(gbps)))
+    return {"ceiling_gbs": gbps.value, "ceiling_ms": ms.value,
+            "ceiling": "thesia_hbm_ceiling on the same buffers in this process: the input read once and "
+                       "the output written once by a coalesced float4 copy (best of 3 x 2 grid sizes)"}
+
+
+def ab_row_stores(args, b):
+    import numpy as np
+    from thesia import engine
+    rs = [int(v) for v in args.row_stores.split(",")]
+    t = {q: [] for q in rs}
+    for _ in range(5):  # interleaved rounds
+        for q in rs:
+            b.set_option(engine.OPT_ROW_STORE, q)
+            b.run_timed(1)
+            t[q].append(b.run_timed(3) / 3)
+    b.set_option(engine.OPT_ROW_STORE, args.row_store)
+    return {str(q): {"median": float(np.median(v)), "min": float(min(v))} for q, v in t.items()}
+
+
 def rfft_roofline(args, din, offs, lens, fmt, n_local, n_samples):
     """BASELINE.json north_star's "window+rFFT kernel" on the same resident input: the same
     streaming kernel with complex-spectrum output ([T, F] complex64, perform_stft's result,
     lib.rs:436-440), timed with HIP events on its launch stream; algorithmic bytes = input once
-    + F x 8 B per frame. Reported beside the headline roofline, never as `value`."""
+    + F x 8 B per frame. Beside it the box's own ceiling for that read : write mix, measured in
+    this process on the same two buffers (thesia_hbm_ceiling: every input byte read once, every
+    output byte written once, coalesced float4). Reported beside the headline roofline, never as
+    `value`."""
     from thesia import engine
     plan = engine.Plan(args.n_fft, args.n_fft, args.hop, engine.OUT_COMPLEX, sr=args.sr)
     frames = engine.Batch.frames_for(plan, lens)
-    dout = engine.DeviceBuffer(frames * plan.row_bins * 8)
+    out_bytes = frames * plan.row_bins * 8
+    dout = engine.DeviceBuffer(out_bytes)
     b = engine.Batch(plan, din, offs, lens, dout, input_format=fmt, channels=args.channels,
-                     kernel=args.kernel)
+                     kernel=args.kernel, row_store=args.row_store)
     b.run_timed(2)
     kms = b.run_timed(5) / 5
     kname = KERNEL_NAMES.get(b.kernel, "?")
     in_el = 4 if args.input == "f32" else 2
-    abytes = n_local * n_samples * args.channels * in_el + frames * plan.row_bins * 8
+    in_bytes = n_local * n_samples * args.channels * in_el
+    abytes = in_bytes + out_bytes
     achieved = abytes / (kms * 1e-3) / 1e9
+    res = {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+           "frac": achieved / HBM_PEAK_GBS, "kernel_ms": kms, "algorithmic_bytes_per_launch": abytes,
+           "frames_per_s": frames / (kms * 1e-3), "row_store": args.row_store,
+           "kernel": kname + ", complex output (downmix+frame+window+rFFT)"}
+    if args.row_stores:
+        res["row_stores_ms"] = ab_row_stores(args, b)
+    res.update(hbm_ceiling(din, in_bytes, dout, out_bytes))
+    res["frac_of_ceiling"] = achieved / res["ceiling_gbs"]
     b.close()
     dout.close()
-    return {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-            "frac": achieved / HBM_PEAK_GBS, "kernel_ms": kms, "algorithmic_bytes_per_launch": abytes,
-            "frames_per_s": frames / (kms * 1e-3),
-            "kernel": kname + ", complex output (downmix+frame+window+rFFT)"}
+    return res
 
 
-def profile_record(workload_key):
+def workload_params(args, kernel):
+    """Every parameter that changes what one launch moves or issues (the key of a stored PMC
+    record: a record applies to this run only if all of them are equal)."""
+    return {"output": args.output, "input": args.input, "channels": args.channels, "n_fft": args.n_fft,
+            "hop": args.hop, "tracks_per_gpu": args.tracks, "seconds": args.seconds, "sr": args.sr,
+            "n_mels": args.n_mels if args.output == "mel_db" else 0, "kernel": kernel, "mel_path": 0}
+
+
+def profile_record(params):
+    """The PMC record of profiles/pmc_traffic.json measured on exactly this workload, or None.
+    Its counts come from a rocprofv3 run on a builder box (the file names the profile), not from
+    this run: the bench line says so next to every value it takes from it."""
     path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     try:
         with open(path) as f:
-            return json.load(f).get(workload_key) or {}
+            recs = json.load(f)
     except (OSError, ValueError):
-        return {}
+        return None
+    for rec in recs.values():
+        if rec.get("workload") == params:
+            return rec
+    return None
 
 
-def traffic_from_profile(workload_key):
-    return profile_record(workload_key).get("hbm_bytes_per_launch")
+def provenance(rec):
+    return {"profile": "profiles/" + rec.get("profile", "?"), "date": rec.get("date"), "box": rec.get("box"),
+            "measured_in_this_run": False,
+            "note": "stored rocprofv3 PMC counts of the same workload from a builder box "
+                    "(profiles/pmc_traffic.json), not measured by this run"}
 
 
 # VALU issue ceiling (MI355X_MICROARCH.md constants table): a wave64 v_fma_f32 occupies its
@@ -335,17 +396,17 @@ def traffic_from_profile(workload_key):
 VALU_ISSUE_PEAK_G = 256 * 4 * 2.4e9 / 2 / 1e9  # wave-instructions per second, in G
 
 
-def issue_ceiling(workload_key, kms):
-    """The mel kernel's other roofline: its VALU wave-instructions per launch (a PMC constant of
-    the kernel and workload, profiles/pmc_traffic.json) over the live kernel time, against the
-    chip's VALU issue peak. DESIGN.md §7: the kernel is issue-bound, not HBM-bound."""
-    n = profile_record(workload_key).get("valu_insts_per_launch")
+def issue_ceiling(rec, kms):
+    """The mel kernel's other roofline: its VALU wave-instructions per launch (a PMC count of
+    the kernel on this exact workload, profiles/pmc_traffic.json) over the live kernel time,
+    against the chip's VALU issue peak. DESIGN.md §7: the kernel is issue-bound, not HBM-bound."""
+    n = rec.get("valu_insts_per_launch") if rec else None
     if n is None:
         return None
     achieved = n / (kms * 1e-3) / 1e9
     return {"bound": "valu-issue", "achieved": achieved, "peak": VALU_ISSUE_PEAK_G,
             "unit": "G wave-instructions/s", "frac": achieved / VALU_ISSUE_PEAK_G,
-            "valu_insts_per_launch": n}
+            "valu_insts_per_launch": n, "valu_insts_source": provenance(rec)}
 
 
 def main_selftest(args, ws, rank, pg):
@@ -537,7 +598,7 @@ def main_worker(args):
     frames = engine.Batch.frames_for(plan, lens)
     dout = engine.DeviceBuffer(frames * plan.row_bins * (8 if kind == engine.OUT_COMPLEX else 4))
     batch = engine.Batch(plan, din, offs, lens, dout, input_format=fmt, channels=args.channels,
-                         kernel=args.kernel)
+                         kernel=args.kernel, row_store=args.row_store if kind == engine.OUT_COMPLEX else 0)
     assert batch.total_frames == frames
 
     for _ in range(args.warmup):
@@ -628,14 +689,15 @@ def main_worker(args):
         },
     }
     if rank == 0:
-        wkey = f"{args.output}_{args.input}_{args.channels}ch_{args.n_fft}_{args.hop}"
+        rec = profile_record(workload_params(args, batch.kernel))
         result["roofline"] = {
             "bound": "hbm",
             "achieved": achieved,
             "peak": HBM_PEAK_GBS,
             "unit": "GB/s",
             "frac": achieved / HBM_PEAK_GBS,
-            "traffic": traffic_from_profile(wkey),
+            "traffic": rec.get("hbm_bytes_per_launch") if rec else None,
+            "traffic_source": provenance(rec) if rec else "no stored PMC record of this exact workload",
             "kernel": KERNEL_NAMES.get(batch.kernel, "?")
                       + ": downmix+frame+window+rFFT+" + {"mel_db": "|X|+mel+dB", "amp_db": "|X|+dB",
                                                            "power_db": "|X|^2+dB", "complex": "complex out"}[args.output]
@@ -643,7 +705,12 @@ def main_worker(args):
             "kernel_ms": kms,
             "algorithmic_bytes_per_launch": abytes,
         }
-        ic = issue_ceiling(wkey, kms) if batch.kernel == 5 else None
+        if kind == engine.OUT_COMPLEX:
+            if args.row_stores:
+                result["roofline"]["row_stores_ms"] = ab_row_stores(args, batch)
+            result["roofline"].update(hbm_ceiling(din, n_local * per_track * el, dout, frames * plan.row_bins * 8))
+            result["roofline"]["frac_of_ceiling"] = achieved / result["roofline"]["ceiling_gbs"]
+        ic = issue_ceiling(rec, kms) if batch.kernel == 5 else None
         if ic is not None:
             result["roofline_valu_issue"] = ic
         if kind != engine.OUT_COMPLEX and not args.no_rfft_roofline:

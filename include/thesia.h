@@ -67,6 +67,13 @@ int thesia_event_create(void** event);
 int thesia_event_destroy(void* event);
 int thesia_event_record(void* event, void* stream);
 int thesia_event_elapsed_ms(void* start, void* stop, float* ms);
+/* The box's practical HBM ceiling for a read : write mix, on the caller's device buffers: every
+ * 16 B of d_src read once and every 16 B of d_dst written once (coalesced float4, grid-stride;
+ * d_dst's old contents are overwritten). Best of `reps` timed launches at two grid sizes on the
+ * library stream (synchronous): *ms and the bytes moved per second in *gbps (may be NULL). A
+ * measurement aid beside a kernel's roofline (bench.py); not part of the reference surface. */
+int thesia_hbm_ceiling(const void* d_src, size_t src_bytes, void* d_dst, size_t dst_bytes, int reps,
+                       float* ms, float* gbps);
 
 /* ---------------------------------------------------------------------------------- */
 /* host tables (bit-exact f32 restatements; computed with the same libm the reference  */
@@ -191,9 +198,11 @@ typedef enum {
     /* at most this many workgroups per launch (0 = one full occupancy wave of the device);
      * small values make every frame stream walk many frames */
     THESIA_BATCH_OPT_MAX_BLOCKS = 2,
-    /* 1 = the other output-row store method of the streaming kernel (LDS-staged 16-byte stores
-     * for complex rows / lane-wise stores for linear rows; stft3_kernel at n_fft 2048 stereo
-     * f32 only) */
+    /* output-row store method of the streaming kernel stft3 (identical bytes):
+     * 0 = default (complex rows as whole 128-byte lines, the line two rows share carried from
+     * frame to frame; linear rows LDS-staged 16-byte stores), 1 = the other method (LDS-staged
+     * 16-byte for complex / lane-wise for linear rows), 2 = complex whole lines, 3 = complex
+     * lane-wise 8-byte stores; 1 and 3 at n_fft 2048 stereo f32 only */
     THESIA_BATCH_OPT_ROW_STORE = 3,
     /* a device buffer of 3 int32 per track (value = its address, 0 = off): every run also
      * leaves each track's max / min over its output rows and a NaN flag there (the per-track

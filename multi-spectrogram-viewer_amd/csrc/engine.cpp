@@ -773,7 +773,7 @@ int batch_set_option(Batch* b, int option, int64_t value) {
             return THESIA_OK;
         }
         case THESIA_BATCH_OPT_ROW_STORE:
-            if (value < 0 || value > 1) return set_error(THESIA_ERR_INVALID_ARG, "row_store must be 0 or 1");
+            if (value < 0 || value > 3) return set_error(THESIA_ERR_INVALID_ARG, "row_store must be 0..3");
             b->launch.row_alt = (int)value;
             return THESIA_OK;
         default:

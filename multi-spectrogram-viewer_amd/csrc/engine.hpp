@@ -95,14 +95,15 @@ struct Batch {
     int kernel = 1;
     bool k3_ok = false;  // the streaming kernel supports this batch's geometry
     bool k5_ok = false;  // ... and so does its n_fft 2048 variant (stft5_kernel)
-    // automatic choice: stft5 for the mel kinds at n_fft 2048 and for mono linear rows without
-    // the range option (measured faster there; slower for complex rows, stereo linear rows, and
-    // stft3 folds the per-track range into its row epilogue), stft3 for the other
-    // streaming geometries, then the 4-waves/SIMD kernel for its sizes, else the general one
+    // automatic choice: stft5 for the mel kinds at n_fft 2048 and for linear rows without the
+    // range option (measured faster there: stereo power dB 5.64 vs 6.22 ms in round 3; slower for
+    // complex rows, 9.0 vs 6.98 ms, and stft3 folds the per-track range into its row epilogue;
+    // DESIGN.md §6), stft3 for the other streaming geometries, then the 4-waves/SIMD kernel for
+    // its sizes, else the general one
     int auto_kernel() const {
         const bool mel = launch.out_kind == OUT_MEL || launch.out_kind == OUT_MEL_AMP_DB;
-        const bool mono_lin = !mel && launch.out_kind != OUT_COMPLEX && launch.channels == 1 && !range;
-        return k5_ok && (mel || mono_lin) ? 5 : k3_ok ? 3 : plan->use_v2 ? 2 : 1;
+        const bool lin = !mel && launch.out_kind != OUT_COMPLEX && !range;
+        return k5_ok && (mel || lin) ? 5 : k3_ok ? 3 : plan->use_v2 ? 2 : 1;
     }
     bool kernel_forced = false;  // THESIA_BATCH_OPT_KERNEL set a kernel (else auto_kernel follows)
     // mel projection of stft5 (THESIA_BATCH_OPT_MEL_PATH): 0 automatic, 1 the rounds' chunk

@@ -86,7 +86,10 @@ struct StftLaunch {
     void* out = nullptr;  // packed rows: frame g at out + g * row_elems
     // scheduling / named alternatives (thesia_batch_set_option)
     int grid = 0;     // 0 => computed from occupancy, else at most this many blocks
-    int row_alt = 0;  // 1: the other row-store method (stft3 n_fft 2048 stereo f32)
+    // row-store method (stft3): 0 default (complex: whole 128-B lines; linear: LDS-
+    // staged 16-byte), 1 the other one (complex: LDS-staged 16-byte; linear: lane-wise), 2 complex
+    // whole lines, 3 complex lane-wise 8-byte; 1 and 3 at n_fft 2048 stereo f32 only
+    int row_alt = 0;
     // the reference-order kernel (stftx_kernels.hip): input point m sits at xpos[m] of the
     // rustfft prepare_radix4 order; xw8 = {twiddle(1, 8), twiddle(3, 8)}; per mel m its nonzero
     // band {first bin, bins, offset into xmel_w}
@@ -216,5 +219,8 @@ int launch_synth_pcm(void* out, int out_format, uint32_t channels, uint64_t n_tr
 void synth_phase_coeffs(uint64_t n, uint32_t sr, uint64_t* ph_a, uint64_t* ph_b);
 void synth_host(int16_t* out, uint32_t C, uint64_t track, uint64_t n, uint32_t sr, uint64_t seed,
                 const int16_t* lut);
+
+// probe_kernels.hip: read src once, write dst once (16-byte accesses, grid-stride)
+int hbm_mix(const void* src, size_t src_bytes, void* dst, size_t dst_bytes, int grid, hipStream_t s);
 
 }  // namespace thesia

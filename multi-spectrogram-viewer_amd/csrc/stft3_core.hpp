@@ -28,8 +28,9 @@ struct Geo3 {
     // linear / complex kinds stage the whole output row in the stream's region (plus up to 3
     // floats of alignment shift) so it leaves as 16-byte aligned stores
     static constexpr int ROW_FLOATS_OK(int ok) { return ok == 0 ? 2 * G2::F : G2::F; }
+    // (+32: a row staged from its 128-byte line start, line_rows, is up to 31 floats in)
     static constexpr int RS_OK(bool staged, int ok) {
-        return !staged ? RS : (RS > (ROW_FLOATS_OK(ok) + 3 + 3) / 4 * 4 ? RS : (ROW_FLOATS_OK(ok) + 3 + 3) / 4 * 4);
+        return !staged ? RS : (RS > (ROW_FLOATS_OK(ok) + 32 + 3) / 4 * 4 ? RS : (ROW_FLOATS_OK(ok) + 32 + 3) / 4 * 4);
     }
     static constexpr int BASE_FLOATS_OK(bool staged, int ok) { return WL_FLOATS + TW_FLOATS + STREAMS * RS_OK(staged, ok); }
     static_assert(P % 4 == 0, "hop = n_fft/4 must move whole points per lane");
@@ -39,8 +40,11 @@ struct Geo3 {
 // vs 6.58 ms), complex no (7.50 vs 7.41 ms; HBM write traffic equals the algorithmic bytes
 // either way). VAR bit10 flips the choice.
 constexpr bool stage_rows(int ok, int var) {
-    return ok == 1 ? (var & 1024) == 0 : ok == 0 ? (var & 1024) != 0 : false;
+    return ok == 1 ? (var & 1024) == 0 : ok == 0 ? (var & (1024 | 2048)) != 0 : false;
 }
+// complex rows staged and stored as whole 128-byte lines with the shared line carried from frame
+// to frame of a stream (VAR bit11; thesia_batch_set_option ROW_STORE = 2)
+constexpr bool line_rows(int ok, int var) { return ok == 0 && (var & 2048) != 0; }
 
 // A row of nfl floats staged in LDS (row element e at stage[sh + e], sh = the row's global
 // float offset mod 4) written with 16-byte aligned stores: whole float4 chunks from the L lanes

@@ -30,6 +30,8 @@ namespace thesia {
 // L + 2, ds_read2_b64) transpose instead of the wide one; bit6 = the previous mel4 (per-round
 // setup reads); bit7 = four mel accumulators; bit8 = ablation: |X|^2 (no v_sqrt); bit9 = the
 // sqrts not batched; bit10 (linear / complex kinds) = the other row-store method (stage_rows);
+// bit11 (complex) = rows as whole 128-byte lines, the shared line carried (line_rows; the
+// default for complex rows); bit17 (complex) = lane-wise 8-byte stores, chosen explicitly;
 // bit12 = no wave-priority phases (s_setprio; previous); bit13 / bit14 = the FFT's twiddle reads
 // and transposes at priority 1 / 2; bit15 = the mel rounds at priority 3; bit16 = the prefetch
 // loads issued at priority 3.
@@ -102,6 +104,7 @@ stft3_kernel(StftLaunch a, uint64_t fps) {
     // committed with one atomic triple per track the stream leaves
     float r_max = -INFINITY, r_min = INFINITY;
     int r_nan = 0, r_trk = -1;
+    float carry = 0.0f;  // line_rows: lane j holds float j of the line the last row ended in
     auto r_flush = [&]() {
 #pragma unroll
         for (int m = L / 2; m >= 1; m >>= 1) {  // the frame's L lanes (xor stays inside the group)
@@ -239,6 +242,35 @@ stft3_kernel(StftLaunch a, uint64_t fps) {
             if constexpr ((VAR & 2) == 0 && (VAR & 64) == 0)
                 mel4<NC, (VAR & 16) ? 4 : 8, (VAR & 128) ? 4 : 1>(a, region, mel_lds, rd_lds, k0_lds, j, g, valid);
             if constexpr ((VAR & 64) != 0) mel4_v1<NC, 8>(a, region, mel_lds, rd_lds, k0_lds, j, g, valid);
+        } else if constexpr (OK == 0 && line_rows(OK, VAR)) {
+            // whole 128-byte lines: the stream's rows are contiguous (frame g's
+            // row ends where g+1's begins), so the row is staged from its line start (sh floats
+            // into the line) and leaves as whole lines, one float4 per lane; the line it shares
+            // with the next frame is carried in a register (lane j: float j of that line) and
+            // written with the next row. Only a stream's first head and last tail are partial.
+            float* crow = static_cast<float*>(a.out) + g * (2 * F);
+            const int sh = (int)((reinterpret_cast<uintptr_t>(crow) >> 2) & 31);  // even
+            float2* st = reinterpret_cast<float2*>(region + sh);
+            untangle2<NC, kBatch>(v, j, partner, ub, [&](int k, float xr, float xi) {
+                st[k] = make_float2(xr, xi);
+            });
+            if (it > 0 && j < sh) region[j] = carry;  // the previous row's tail (same stream)
+            wave_lds_sync();
+            if (valid) {
+                float* lb = crow - sh;  // 128-byte aligned
+                const int tot = sh + 2 * F, nfull = tot >> 5, rem = tot & 31;
+                const int c0 = (it > 0 || sh == 0) ? 0 : 8;  // a stream's first head line: lane-wise
+                if (c0 && j >= sh) lb[j] = region[j];
+                for (int i = c0 + j; i < nfull * 8; i += L)
+                    *reinterpret_cast<float4*>(__builtin_assume_aligned(lb + 4 * i, 16)) =
+                        *reinterpret_cast<const float4*>(__builtin_assume_aligned(region + 4 * i, 16));
+                const float tail = region[nfull * 32 + (j < rem ? j : 0)];
+                if (g + 1 == g1) {  // the stream's last row: its tail line leaves partial
+                    if (j < rem) lb[nfull * 32 + j] = tail;
+                } else {
+                    carry = tail;
+                }
+            }
         } else if constexpr (OK == 0 && !stage_rows(OK, VAR)) {  // lane-wise 8-byte stores
             float2* crow = reinterpret_cast<float2*>(a.out) + g * F;
             untangle2<NC, kBatch>(v, j, partner, ub, [&](int k, float xr, float xi) {
@@ -353,10 +385,18 @@ static int launch3_k(const StftLaunch& a, hipStream_t stream) {
         }
     }
 #endif
-    // the named alternative row-store method (thesia_batch_set_option ROW_STORE; measured,
-    // DESIGN.md §6), compiled for the headline geometry only
-    if constexpr (VAR == 0 && WV == kWaves && NC == 1024 && OK != 2 && C == 2 && INF == IN_F32) {
-        if (a.row_alt) return launch3_k<NC, OK, C, INF, 1024>(a, stream);
+    // row-store methods (thesia_batch_set_option ROW_STORE; measured). Complex rows
+    // leave as whole 128-byte lines by default (6.83 vs 6.98 ms lane-wise, 7.10 LDS-staged 16-byte,
+    // one process); the alternatives are compiled for the headline geometry only.
+    if constexpr (VAR == 0 && WV == kWaves && OK == 0) {
+        if constexpr (NC == 1024 && C == 2 && INF == IN_F32) {
+            if (a.row_alt == 1) return launch3_k<NC, OK, C, INF, 1024>(a, stream);
+            if (a.row_alt == 3) return launch3_k<NC, OK, C, INF, 131072>(a, stream);  // lane-wise
+        }
+        return launch3_k<NC, OK, C, INF, 2048>(a, stream);
+    }
+    if constexpr (VAR == 0 && WV == kWaves && NC == 1024 && OK == 1 && C == 2 && INF == IN_F32) {
+        if (a.row_alt == 1) return launch3_k<NC, OK, C, INF, 1024>(a, stream);
     }
     constexpr int kBlock = 64 * WV;
     const int lds = lds3_bytes<NC, OK, VAR, WV>(a);

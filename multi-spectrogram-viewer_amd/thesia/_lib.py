@@ -60,6 +60,7 @@ _SIGS = {
     "thesia_event_destroy": (_i, [_vp]),
     "thesia_event_record": (_i, [_vp, _vp]),
     "thesia_event_elapsed_ms": (_i, [_vp, _vp, _fp]),
+    "thesia_hbm_ceiling": (_i, [_vp, _sz, _vp, _sz, _i, _fp, _fp]),
     "thesia_hann": (_i, [_sz, _i, _fp]),
     "thesia_calc_proper_n_fft": (_sz, [_sz]),
     "thesia_hz_to_mel": (_f, [_f]),

@@ -1,6 +1,7 @@
 """bench.py --gpus N spawns its own N worker processes (RANK / LOCAL_RANK / WORLD_SIZE /
 MASTER_* set, before any GPU or thesia import) -- the launcher plumbing and the gloo
 reductions (barrier, max time, per-rank report), on CPU via --selftest."""
+import argparse
 import json
 import os
 import subprocess
@@ -46,15 +47,28 @@ def test_failing_worker_fails_the_launch():
 
 def test_profile_records_behind_the_bench_line():
     """The default bench line's `roofline.traffic` and `roofline_valu_issue` come from the PMC
-    record of its workload (profiles/pmc_traffic.json); the issue roofline is that kernel's VALU
-    wave-instructions over the kernel time against 256 CUs x 4 SIMDs x 2.4 GHz / 2 cycles."""
+    record of exactly its workload (profiles/pmc_traffic.json: every launch parameter equal) and
+    say so (`traffic_source` / `valu_insts_source`: stored, not measured in this run); any other
+    workload (fewer tracks, another n_mels, another kernel) gets none. The issue roofline is the
+    kernel's VALU wave-instructions over the kernel time against 256 CUs x 4 SIMDs x 2.4 GHz / 2."""
     sys.path.insert(0, ROOT)
     import bench
-    key = "mel_db_f32_2ch_2048_512"  # bench.py defaults: output, input, channels, n_fft, hop
-    assert bench.traffic_from_profile(key) > 12.96e9  # >= the algorithmic bytes per launch
-    ic = bench.issue_ceiling(key, 4.0)
+    saved, sys.argv = sys.argv, ["bench.py"]
+    try:
+        args = bench.parse()
+    finally:
+        sys.argv = saved
+    rec = bench.profile_record(bench.workload_params(args, 5))
+    assert rec is not None and rec["hbm_bytes_per_launch"] > 12.96e9  # >= the algorithmic bytes
+    src = bench.provenance(rec)
+    assert src["measured_in_this_run"] is False and src["profile"].startswith("profiles/r02")
+    ic = bench.issue_ceiling(rec, 4.0)
     assert ic["bound"] == "valu-issue" and ic["peak"] == 1228.8
     assert abs(ic["achieved"] - ic["valu_insts_per_launch"] / 4e-3 / 1e9) < 1e-9 * ic["achieved"]
     assert abs(ic["frac"] - ic["achieved"] / ic["peak"]) < 1e-12
-    assert bench.issue_ceiling("no_such_workload", 4.0) is None
-    assert bench.traffic_from_profile("no_such_workload") is None
+    assert ic["valu_insts_source"]["measured_in_this_run"] is False
+    for change in ({"tracks": 100}, {"n_mels": 64}, {"seconds": 10.0}):
+        other = argparse.Namespace(**dict(vars(args), **change))
+        assert bench.profile_record(bench.workload_params(other, 5)) is None
+    assert bench.profile_record(bench.workload_params(args, 3)) is None
+    assert bench.issue_ceiling(None, 4.0) is None

@@ -77,7 +77,7 @@ _LIN_KINDS = [engine.OUT_MAG, engine.OUT_POWER, engine.OUT_AMP_DB, engine.OUT_PO
 @pytest.mark.parametrize("n_fft", [256, 2048])
 @pytest.mark.parametrize("kind", _LIN_KINDS + [engine.OUT_COMPLEX])
 @pytest.mark.parametrize("shift", [0, 1, 2, 3])
-@pytest.mark.parametrize("row_store,kernel", [(0, 3), (1, 3), (0, 5)])
+@pytest.mark.parametrize("row_store,kernel", [(0, 3), (1, 3), (2, 3), (3, 3), (0, 5)])
 def test_row_stores_any_output_alignment(n_fft, kind, shift, row_store, kernel):
     """Output rows of F floats / F float2 are not 16-byte aligned; the LDS-staged float4 row
     stores (stft3 store_row_b128: linear kinds by default, complex with the ROW_STORE option) must write
@@ -87,6 +87,8 @@ def test_row_stores_any_output_alignment(n_fft, kind, shift, row_store, kernel):
         pytest.skip("complex rows are float2: 8-byte aligned output")
     if (row_store or kernel == 5) and n_fft != 2048:
         pytest.skip("the other store method / stft5_kernel: n_fft 2048 only")
+    if row_store >= 2 and kind != engine.OUT_COMPLEX:
+        pytest.skip("whole-line / lane-wise row store options: complex rows only")
     rng = np.random.default_rng(n_fft + 7 * kind + shift)
     hop = n_fft // 4
     lens = [n_fft - 1, 5 * n_fft + 3, 33 * hop + 1, 2 * n_fft]
@@ -134,3 +136,38 @@ def test_row_stores_any_output_alignment(n_fft, kind, shift, row_store, kernel):
             scale = np.abs(r).max(axis=1, keepdims=True)
             rel = 4e-6 if kind == engine.OUT_MAG else 8e-6
             assert np.all(np.abs(g - r) <= rel * np.maximum(scale, 1e-30)), float(np.abs(g - r).max())
+
+
+@pytest.mark.parametrize("shift", [0, 2, 6, 30])
+@pytest.mark.parametrize("max_blocks", [0, 5])
+def test_line_rows_equal_lane_rows(shift, max_blocks):
+    """ROW_STORE 2 (complex rows as whole 128-byte lines, the line two rows share carried from
+    frame to frame of a stream; the default) computes the same values as the lane-wise stores
+    (ROW_STORE 3); only the store
+    pattern differs, so the whole output buffer -- guard floats around the rows included -- is
+    bit-identical, at every line offset of the output pointer and with many streams (every
+    stream's first head line and last tail line are partial)."""
+    rng = np.random.default_rng(100 + shift + max_blocks)
+    n_fft, hop = 2048, 512
+    lens = [int(v) for v in rng.integers(n_fft - 1, 40 * n_fft, 37)]
+    tracks = [(rng.standard_normal((n, 2)) * 0.3).astype(np.float32) for n in lens]
+    plan = engine.Plan(n_fft, n_fft, hop, engine.OUT_COMPLEX)
+    flat = np.concatenate([t.reshape(-1) for t in tracks])
+    offs = np.cumsum([0] + [t.size for t in tracks[:-1]])
+    din = engine.DeviceBuffer.from_host(flat)
+    T = engine.Batch.frames_for(plan, lens)
+    fl = plan.row_bins * 2
+    guard = 64
+    host = np.full(T * fl + 2 * guard, np.float32(-777.25), np.float32)
+    outs = []
+    for rs in (3, 2, 0):
+        dout = engine.DeviceBuffer.from_host(host)
+        b = engine.Batch(plan, din, offs, lens, dout.ptr.value + (guard - 32 + shift) * 4,
+                         input_format=engine.IN_F32, channels=2, max_blocks=max_blocks, row_store=rs,
+                         kernel=3)
+        b.run()
+        engine.synchronize()
+        outs.append(dout.to_host(np.float32))
+        b.close()
+        dout.close()
+    assert outs[0].view(np.uint32).tobytes() == outs[1].view(np.uint32).tobytes() == outs[2].view(np.uint32).tobytes()
