@@ -38,9 +38,11 @@ KERNEL_NAMES = {1: "thesia::stft_kernel (general)", 2: "thesia::stft2_kernel (ge
 def parse():
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
-    p.add_argument("--workload", choices=["c4", "c3", "c5"], default="c4",
+    p.add_argument("--workload", choices=["c4", "c3", "c5", "viewer"], default="c4",
                    help="c4 (default, BASELINE.json metric): 48 kHz 30 s stereo, mel-128; "
-                        "c3: 48 kHz 10 s mono, mel-128; c5: mixed rates / n_fft, dB + RGB render")
+                        "c3: 48 kHz 10 s mono, mel-128; c5: mixed rates / n_fft, dB + RGB render; "
+                        "viewer: the reference's own four criterion benches (benches/bench.rs) "
+                        "through the drop-in MultiTrack path")
     p.add_argument("--steps", type=int, default=20)
     p.add_argument("--warmup", type=int, default=3)
     p.add_argument("--tracks", type=int, default=1000, help="tracks per GPU")
@@ -512,6 +514,156 @@ def main_c5(args, ws, rank, pg, device):
     p.close()
 
 
+def _median_s(fn, reps, warm=1):
+    import numpy as np
+    from thesia import engine
+    for _ in range(warm):
+        fn()
+    engine.synchronize()
+    t = []
+    for _ in range(reps):
+        t0 = time.perf_counter()
+        fn()
+        engine.synchronize()
+        t.append(time.perf_counter() - t0)
+    return float(np.median(t))
+
+
+def main_viewer(args, rank):
+    """The reference's own measurement spec, benches/bench.rs (criterion; it does not compile at
+    this revision, bench.rs:86, and reads the absent samples/sample.wav: the 48 kHz substitute
+    of tests/fixtures.py stands in). Four entries, each with the GPU time of the drop-in path
+    and the oracle's CPU time beside it:
+      get_melspectrogram  bench.rs:7-25,62-77: 1 s @ 48 kHz, win 1920 / hop 480 / n_fft 2048
+                          (the viewer geometry, lib.rs:43-46), default n_mel, amp dB
+      draw_spec           bench.rs:79-95: grey -> Lanczos3 + colormap RGB, 100 px/s x 500
+      add_tracks          bench.rs:32-45: MultiTrack.add_tracks of the sample six times (ids 0-5)
+      get_spec_image      bench.rs:47-60: get_spec_image(0, 100, 500) after that add
+    plus the kernels behind add_tracks on the same six tracks: the reference-order stftx
+    (MultiTrack's, bit-exact) and the batch engine's fast kernel for that geometry."""
+    import tempfile
+    import wave
+    import numpy as np
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import fixtures
+    import oracle_ffi as O
+    import thesia
+    from thesia import engine, display
+
+    sr, win, hop, n_fft = 48000, 1920, 480, 2048
+    pcm16 = fixtures.c1_substitute()
+    x_full = fixtures.s16_to_f32(pcm16)
+    x1 = x_full[:sr]  # bench.rs:66 slice ..sr
+    fb = O.calc_mel_fb_default(sr, n_fft)
+    n_mel = fb.shape[1]
+    out = {"metric": "viewer drop-in path: the four criterion benches of benches/bench.rs, GPU vs oracle CPU",
+           "unit": "ms per call", "higher_is_better": False, "dtype": "f32",
+           "data": "tests/fixtures.py c1_substitute (the 48 kHz sample stand-in, 2 113 529 samples, int16 WAV)",
+           "config": {"workload": "viewer", "sr": sr, "win": win, "hop": hop, "n_fft": n_fft, "n_mel_default": n_mel},
+           "entries": {}}
+    E = out["entries"]
+
+    # -- get_melspectrogram: 1 s, reference-order kernel and the fast kernel, kernel-only and host-in/out
+    plan = engine.Plan(n_fft, win, hop, engine.OUT_MEL_AMP_DB, sr=sr)
+    din = engine.DeviceBuffer.from_host(x1)
+    T1 = engine.Batch.frames_for(plan, [len(x1)])
+    dout = engine.DeviceBuffer(T1 * plan.row_bins * 4)
+    ent = {"frames": T1, "n_mel": plan.row_bins}
+    for name, k in (("stftx (reference order, bit-exact)", 9), ("fast kernel", 0)):
+        b = engine.Batch(plan, din, [0], [len(x1)], dout, kernel=k)
+        b.run_timed(3)
+        kms = b.run_timed(50) / 50
+        host = np.empty((T1, plan.row_bins), np.float32)
+
+        def call():  # host PCM in, host dB rows out (what perform_stft + dot + dB hand back)
+            from thesia._lib import lib, check
+            import ctypes as C
+            check(lib.thesia_memcpy_h2d(din.ptr, x1.ctypes.data_as(C.c_void_p), x1.nbytes))
+            b.run()
+            check(lib.thesia_memcpy_d2h(host.ctypes.data_as(C.c_void_p), dout.ptr, host.nbytes))
+        ent[name] = {"kernel": b.kernel, "kernel_ms": kms, "call_ms_host_in_out": 1e3 * _median_s(call, 50)}
+        b.close()
+    t_cpu = _median_s(lambda: O.track_spec(x1, win, hop, n_fft, O.TRACK_MEL_DB, fb), 20)
+    ent["cpu_oracle_ms"] = 1e3 * t_cpu
+    ent["cpu"] = "oracle track_spec, 1 thread (one FFT plan, dense mel dot, 3-pass dB)"
+    E["get_melspectrogram"] = ent
+    spec = O.track_spec(x1, win, hop, n_fft, O.TRACK_MEL_DB, fb)
+
+    # -- draw_spec: grey of that spectrogram (up_ratio 1) -> RGB 100 px/s x 500
+    grey = O.spec_to_grey(spec, 1.0, float(spec.max()), float(spec.min()))
+    nw = 100 * len(x1) // sr
+    dgrey = engine.DeviceBuffer.from_host(grey)
+    drgb = engine.DeviceBuffer(nw * 500 * 3)
+    from thesia._lib import lib, check
+    g_dev = _median_s(lambda: check(lib.thesia_grey_to_rgb_device(dgrey.ptr, grey.shape[1], grey.shape[0],
+                                                                  nw, 500, drgb.ptr)), 50)
+    g_host = _median_s(lambda: display.grey_to_rgb(grey, nw, 500), 20)
+    E["draw_spec"] = {"nwidth": nw, "nheight": 500, "gpu_ms_device_buffers": 1e3 * g_dev,
+                      "gpu_ms_host_in_out": 1e3 * g_host,
+                      "cpu_oracle_ms": 1e3 * _median_s(lambda: O.grey_to_rgb(grey, nw, 500), 10)}
+
+    # -- add_tracks x6 and get_spec_image through MultiTrack, from a WAV file like the reference
+    tmp = tempfile.mkdtemp(prefix="thesia_viewer_")
+    path = os.path.join(tmp, "sample.wav")
+    with wave.open(path, "wb") as w:
+        w.setnchannels(1)
+        w.setsampwidth(2)
+        w.setframerate(sr)
+        w.writeframes(pcm16.astype("<i2").tobytes())
+    mt = thesia.MultiTrack()
+    ids = [0, 1, 2, 3, 4, 5]
+    paths = "\n".join([path] * 6)
+    t_add = _median_s(lambda: mt.add_tracks(ids, paths), 5)
+    nwi = int(np.float32(100.0) * np.float32(len(x_full)) / np.float32(sr))
+    t_img = _median_s(lambda: mt.get_spec_image(0, 100.0, 500), 10)
+    # the CPU side: the reference's structure, one track per rayon worker (lib.rs:161-166)
+    from concurrent.futures import ThreadPoolExecutor
+
+    def cpu_add():
+        with ThreadPoolExecutor(6) as ex:
+            specs = list(ex.map(lambda _: O.track_spec(x_full, win, hop, n_fft, O.TRACK_MEL_DB, fb), ids))
+        mx = min(max(float(v.max()) for v in specs), 0.0)
+        mn = max(min(float(v.min()) for v in specs), mx - 120.0)
+        with ThreadPoolExecutor(6) as ex:
+            return list(ex.map(lambda v: O.spec_to_grey(v, 1.0, mx, mn), specs))
+    t0 = time.perf_counter()
+    greys = cpu_add()
+    t_cpu_add = time.perf_counter() - t0
+    t_cpu_img = _median_s(lambda: O.grey_to_rgb(greys[0], nwi, 500), 3)
+    E["add_tracks"] = {"tracks": 6, "samples_per_track": len(x_full), "gpu_ms": 1e3 * t_add,
+                       "gpu": "MultiTrack.add_tracks: WAV parse + int16 upload + decode + stftx + range + grey, synchronous",
+                       "cpu_oracle_ms": 1e3 * t_cpu_add, "cpu_threads": 6,
+                       "cpu": "oracle track_spec per track on 6 threads (rayon par_iter, lib.rs:161-166) + range + "
+                              "spec_to_grey; no WAV parse"}
+    E["get_spec_image"] = {"nwidth": nwi, "nheight": 500, "gpu_ms": 1e3 * t_img,
+                           "gpu": "MultiTrack.get_spec_image: Lanczos3 + colormap on the device + RGB copy to the host",
+                           "cpu_oracle_ms": 1e3 * t_cpu_img, "cpu": "oracle grey_to_rgb, 1 thread"}
+    del mt
+    os.remove(path)
+    os.rmdir(tmp)
+
+    # -- the kernels behind add_tracks on the same six tracks (int16 input, as MultiTrack uploads)
+    n = len(pcm16)
+    flat = np.concatenate([pcm16] * 6)
+    din6 = engine.DeviceBuffer.from_host(flat)
+    offs = [i * n for i in range(6)]
+    T6 = engine.Batch.frames_for(plan, [n] * 6)
+    dout6 = engine.DeviceBuffer(T6 * plan.row_bins * 4)
+    kk = {}
+    for name, k in (("stftx", 9), ("fast", 0)):
+        b = engine.Batch(plan, din6, offs, [n] * 6, dout6, input_format=engine.IN_S16, kernel=k)
+        b.run_timed(2)
+        kms = b.run_timed(10) / 10
+        abytes = flat.nbytes + T6 * plan.row_bins * 4
+        kk[name] = {"kernel": b.kernel, "kernel_ms": kms, "frames_per_s": T6 / (kms * 1e-3),
+                    "algorithmic_gbs": abytes / (kms * 1e-3) / 1e9,
+                    "hbm_frac": abytes / (kms * 1e-3) / 1e9 / HBM_PEAK_GBS}
+        b.close()
+    E["add_tracks_kernels"] = dict(kk, frames=T6, algorithmic_bytes=flat.nbytes + T6 * plan.row_bins * 4)
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+
+
 def end_to_end(args, plan, kind):
     """PCIe-inclusive rate of the C4 path (H2D int16 + D2H), reported beside the
     value, never as it: a sample of the shard's geometry as int16 PCM (the WAV encoding, 2 B per
@@ -572,6 +724,11 @@ def main_worker(args):
     # one rank per GPU; on a box with fewer GPUs than ranks (a rehearsal) ranks share devices
     device = local % max(1, engine.device_count())
     engine.set_device(device)
+    if args.workload == "viewer":
+        main_viewer(args, rank)
+        if pg is not None:
+            pg.destroy_process_group()
+        return
     if args.workload == "c5":
         main_c5(args, ws, rank, pg, device)
         if pg is not None:

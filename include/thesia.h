@@ -174,7 +174,9 @@ int thesia_batch_run(thesia_batch* batch, void* stream);
 /* One pass of each of n batches (e.g. one per geometry group of a multi-rate track set), spread
  * over the library's internal streams of the current device and joined back to `stream` (NULL
  * => the library stream): the same results as n thesia_batch_run calls, with the launches
- * overlapping. Not part of the reference surface (its per-track loop is lib.rs:161-166).
+ * overlapping -- so the batches must share nothing they write: distinct handles
+ * (THESIA_ERR_INVALID_ARG for a repeated one), output rows and range buffers that do not
+ * overlap. Not part of the reference surface (its per-track loop is lib.rs:161-166).
  * Asynchronous. */
 int thesia_batches_run(thesia_batch* const* batches, size_t n, void* stream);
 /* Runs `iters` passes bracketed by HIP events on the launch stream; returns the elapsed
@@ -356,6 +358,10 @@ int thesia_mt_get_spec(const thesia_mt* mt, uint64_t id, float* out, size_t cap_
 int thesia_mt_get_grey(const thesia_mt* mt, uint64_t id, float* out, size_t cap_floats,
                        uint32_t* width, uint32_t* height);
 int thesia_mt_track_count(const thesia_mt* mt, size_t* n);
+/* Device bytes the tracks hold (wav + spectrogram buffers, each shared buffer once, + greys).
+ * Tracks added by one call share buffers; removals that leave a buffer at most half used move its
+ * survivors into their own buffers and free it (the reference frees per track, lib.rs:265-292). */
+int thesia_mt_device_bytes(const thesia_mt* mt, size_t* bytes);
 /* the track's mono wav (audio.rs:9-37 decode + lib.rs:42 channel sum) as held on the device */
 int thesia_mt_get_wav(const thesia_mt* mt, uint64_t id, float* out, size_t cap_floats,
                       size_t* n_samples);

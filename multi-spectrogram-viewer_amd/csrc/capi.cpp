@@ -762,4 +762,10 @@ int thesia_mt_track_count(const thesia_mt* mt, size_t* n) {
     return THESIA_OK;
 }
 
+int thesia_mt_device_bytes(const thesia_mt* mt, size_t* bytes) {
+    if (!mt || !bytes) return set_error(THESIA_ERR_INVALID_ARG, "null argument");
+    *bytes = M(mt)->device_bytes();
+    return THESIA_OK;
+}
+
 }  // extern "C"

@@ -824,6 +824,12 @@ int batch_run(Batch* b, hipStream_t s) {
 int batches_run(Batch* const* b, size_t n, hipStream_t s) {
     if (!s) s = default_stream();
     if (n <= 1) return n ? batch_run(b[0], s) : THESIA_OK;
+    {  // the batches run concurrently: the same batch twice would race on its output and ranges
+        std::vector<const Batch*> seen(b, b + n);
+        std::sort(seen.begin(), seen.end());
+        if (std::adjacent_find(seen.begin(), seen.end()) != seen.end() || seen.front() == nullptr)
+            return set_error(THESIA_ERR_INVALID_ARG, "batches_run: a batch handle appears twice (or is null)");
+    }
     constexpr int kRunStreams = 4;
     struct Pool {
         hipStream_t st[kRunStreams] = {};
@@ -990,9 +996,54 @@ int grey_to_rgb_device(const float* d_grey, uint32_t w, uint32_t h, uint32_t nw,
     return THESIA_OK;
 }
 
+static int minmax_segments_core(size_t n_groups, const float* const* d_x, const uint64_t* const* row0,
+                                const size_t* bins, const size_t* ns, float* mx, float* mn, int* nan,
+                                hipStream_t s);
+
+// Calls of more than 65535 tracks (the launch's grid.y limit) run as consecutive pieces of at
+// most that many tracks (a group's track range is cut where needed: row0 + i0 is the row table of
+// its tracks i0.. as it stands); the outputs stay in the concatenated group order.
 int minmax_segments_multi(size_t n_groups, const float* const* d_x, const uint64_t* const* row0,
                           const size_t* bins, const size_t* ns, float* mx, float* mn, int* nan,
                           hipStream_t s) {
+    constexpr size_t kMax = 65535;
+    size_t ntr = 0;
+    for (size_t k = 0; k < n_groups; ++k) ntr += ns[k];
+    if (ntr <= kMax) return minmax_segments_core(n_groups, d_x, row0, bins, ns, mx, mn, nan, s);
+    std::vector<const float*> px;
+    std::vector<const uint64_t*> pr;
+    std::vector<size_t> pb, pn;
+    size_t in_piece = 0, done = 0;
+    auto flush = [&]() -> int {
+        if (px.empty()) return THESIA_OK;
+        const int rc = minmax_segments_core(px.size(), px.data(), pr.data(), pb.data(), pn.data(), mx + done,
+                                            mn + done, nan + done, s);
+        done += in_piece;
+        in_piece = 0;
+        px.clear(); pr.clear(); pb.clear(); pn.clear();
+        return rc;
+    };
+    for (size_t k = 0; k < n_groups; ++k) {
+        for (size_t i0 = 0; i0 < ns[k];) {
+            const size_t c = std::min(ns[k] - i0, kMax - in_piece);
+            px.push_back(d_x[k]);
+            pr.push_back(row0[k] + i0);
+            pb.push_back(bins[k]);
+            pn.push_back(c);
+            in_piece += c;
+            i0 += c;
+            if (in_piece == kMax) {
+                const int rc = flush();
+                if (rc) return rc;
+            }
+        }
+    }
+    return flush();
+}
+
+static int minmax_segments_core(size_t n_groups, const float* const* d_x, const uint64_t* const* row0,
+                                const size_t* bins, const size_t* ns, float* mx, float* mn, int* nan,
+                                hipStream_t s) {
     // one launch over every group's tracks: segment bounds are element offsets from the lowest
     // group buffer (one flat device address space), one table upload, one readback
     const float* base = nullptr;
@@ -1005,7 +1056,6 @@ int minmax_segments_multi(size_t n_groups, const float* const* d_x, const uint64
         tot += (row0[k][ns[k]] - row0[k][0]) * bins[k];
     }
     if (ntr == 0) return THESIA_OK;
-    if (ntr > 65535) return set_error(THESIA_ERR_INVALID_ARG, "more than 65535 tracks in one range call");
     // [lo, hi) per track: each track closed by its own end, so no segment spans the gap
     // between two groups' buffers
     std::vector<uint64_t> lo(ntr), hi(ntr);

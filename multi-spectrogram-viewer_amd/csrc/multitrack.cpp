@@ -267,18 +267,21 @@ int MultiTrack::update_spec_greys(int* changed_out) {
         int rc = jobs.back().buf.alloc(std::max<size_t>((size_t)gh * tr.T, 1) * sizeof(float));
         if (rc) return rc;
     }
+    // every grey is formed into its new buffer first; the range, max_sr and the tracks' greys
+    // are committed only once all of them succeeded (a failure leaves the old state whole)
+    for (Job& j : jobs)
+        if (launch_spec_to_grey(j.tr->spec(), (uint32_t)j.tr->T, (uint32_t)j.tr->bins, j.h, max_db,
+                                min_db, j.buf.as<float>(), default_stream()))
+            return set_error(THESIA_ERR_DEVICE, "spec_to_grey launch failed");
+    THESIA_HIP(hipStreamSynchronize(default_stream()));
     max_db_ = max_db;
     min_db_ = min_db;
     max_sr_ = max_sr;
     for (Job& j : jobs) {
-        if (launch_spec_to_grey(j.tr->spec(), (uint32_t)j.tr->T, (uint32_t)j.tr->bins, j.h, max_db_,
-                                min_db_, j.buf.as<float>(), default_stream()))
-            return set_error(THESIA_ERR_DEVICE, "spec_to_grey launch failed");
         j.tr->grey = std::move(j.buf);
         j.tr->grey_h = j.h;
         j.tr->has_grey = true;
     }
-    THESIA_HIP(hipStreamSynchronize(default_stream()));
     if (changed_out) *changed_out = changed ? 1 : 0;
     return THESIA_OK;
 }
@@ -298,6 +301,7 @@ int MultiTrack::remove_track(uint64_t id, int* changed) {
         id_max_sec_ = best_id;
         max_sec_ = best;
     }
+    compact_pools();
     bool used = false;  // lib.rs:287-290 evict per-sr caches
     for (auto& kv : tracks_) used |= kv.second.sr == sr;
     if (!used) {
@@ -305,6 +309,64 @@ int MultiTrack::remove_track(uint64_t id, int* changed) {
         if (pit != plans_.end()) { delete pit->second; plans_.erase(pit); }
     }
     return update_spec_greys(changed);
+}
+
+// The tracks of one add_tracks call and sample rate share their wav / spectrogram buffers (one
+// batched launch wrote them). When removals leave a buffer at most half used, its surviving
+// tracks move into buffers of their own (device-to-device copies) and the pool is freed, so a
+// long session does not keep removed tracks' samples in HBM (the reference frees per track,
+// lib.rs:265-292). Best effort: if an allocation fails the tracks keep sharing.
+void MultiTrack::compact_pools() {
+    struct Use { size_t live = 0; std::vector<Track*> tracks; };
+    std::map<DevBuf*, Use> wav_use, spec_use;
+    for (auto& kv : tracks_) {
+        Track& tr = kv.second;
+        if (tr.wav_pool) {
+            Use& u = wav_use[tr.wav_pool.get()];
+            u.live += tr.n * sizeof(float);
+            u.tracks.push_back(&tr);
+        }
+        if (tr.spec_pool) {
+            Use& u = spec_use[tr.spec_pool.get()];
+            u.live += (size_t)tr.T * tr.bins * sizeof(float);
+            u.tracks.push_back(&tr);
+        }
+    }
+    hipStream_t s = default_stream();
+    bool copied = false;
+    auto move_out = [&](std::map<DevBuf*, Use>& use, bool wav) {
+        for (auto& [pool, u] : use) {
+            if (u.live * 2 > pool->bytes) continue;
+            for (Track* tr : u.tracks) {
+                auto nb = std::make_shared<DevBuf>();
+                const size_t bytes = wav ? tr->n * sizeof(float) : (size_t)tr->T * tr->bins * sizeof(float);
+                if (nb->alloc(std::max<size_t>(bytes, 4))) return;
+                const float* src = wav ? tr->wav() : tr->spec();
+                if (bytes && hipMemcpyAsync(nb->p, src, bytes, hipMemcpyDeviceToDevice, s) != hipSuccess) return;
+                copied = true;
+                if (wav) { tr->wav_pool = nb; tr->wav_off = 0; }
+                else { tr->spec_pool = nb; tr->spec_off = 0; }
+            }
+        }
+    };
+    move_out(wav_use, true);
+    move_out(spec_use, false);
+    // the old pools are released once the last shared_ptr goes; the copies read them first
+    if (copied) (void)hipStreamSynchronize(s);
+}
+
+size_t MultiTrack::device_bytes() const {
+    std::map<const DevBuf*, size_t> pools;
+    size_t greys = 0;
+    for (auto& kv : tracks_) {
+        const Track& tr = kv.second;
+        if (tr.wav_pool) pools[tr.wav_pool.get()] = tr.wav_pool->bytes;
+        if (tr.spec_pool) pools[tr.spec_pool.get()] = tr.spec_pool->bytes;
+        greys += tr.grey.bytes;
+    }
+    size_t b = greys;
+    for (auto& kv : pools) b += kv.second;
+    return b;
 }
 
 const Track* MultiTrack::find(uint64_t id) const {

@@ -70,10 +70,13 @@ class MultiTrack {
     float min_db() const { return min_db_; }
     float max_sec() const { return max_sec_; }
     size_t size() const { return tracks_.size(); }
+    // device bytes the tracks hold: their wav / spectrogram buffers (shared ones once) and greys
+    size_t device_bytes() const;
 
   private:
     int make_plan(const Track& tr, Plan** out) const;
     int update_spec_greys(int* changed);
+    void compact_pools();
 
     Setting set_;
     std::map<uint64_t, Track> tracks_;

@@ -104,7 +104,7 @@ stft3_kernel(StftLaunch a, uint64_t fps) {
     // committed with one atomic triple per track the stream leaves
     float r_max = -INFINITY, r_min = INFINITY;
     int r_nan = 0, r_trk = -1;
-    float carry = 0.0f;  // line_rows: lane j holds float j of the line the last row ended in
+    float carry[32 / L];  // line_rows: floats j + c*L of the line the last row ended in
     auto r_flush = [&]() {
 #pragma unroll
         for (int m = L / 2; m >= 1; m >>= 1) {  // the frame's L lanes (xor stays inside the group)
@@ -246,29 +246,37 @@ stft3_kernel(StftLaunch a, uint64_t fps) {
             // whole 128-byte lines: the stream's rows are contiguous (frame g's
             // row ends where g+1's begins), so the row is staged from its line start (sh floats
             // into the line) and leaves as whole lines, one float4 per lane; the line it shares
-            // with the next frame is carried in a register (lane j: float j of that line) and
-            // written with the next row. Only a stream's first head and last tail are partial.
+            // with the next frame is carried in registers (lane j: floats j + c*L of that line)
+            // and written with the next row. Only a stream's first head and last tail are partial.
+            static_assert(L <= 32 && 32 % L == 0, "a frame's lanes tile a 128-byte line");
+            constexpr int CW = 32 / L;  // carry floats per lane
             float* crow = static_cast<float*>(a.out) + g * (2 * F);
             const int sh = (int)((reinterpret_cast<uintptr_t>(crow) >> 2) & 31);  // even
             float2* st = reinterpret_cast<float2*>(region + sh);
             untangle2<NC, kBatch>(v, j, partner, ub, [&](int k, float xr, float xi) {
                 st[k] = make_float2(xr, xi);
             });
-            if (it > 0 && j < sh) region[j] = carry;  // the previous row's tail (same stream)
+#pragma unroll
+            for (int c = 0; c < CW; ++c)  // the previous row's tail (same stream)
+                if (it > 0 && j + c * L < sh) region[j + c * L] = carry[c];
             wave_lds_sync();
             if (valid) {
                 float* lb = crow - sh;  // 128-byte aligned
                 const int tot = sh + 2 * F, nfull = tot >> 5, rem = tot & 31;
-                const int c0 = (it > 0 || sh == 0) ? 0 : 8;  // a stream's first head line: lane-wise
-                if (c0 && j >= sh) lb[j] = region[j];
-                for (int i = c0 + j; i < nfull * 8; i += L)
+                const bool head = it == 0 && sh != 0;  // a stream's first head line: float by float
+#pragma unroll
+                for (int c = 0; c < CW; ++c)
+                    if (head && j + c * L >= sh) lb[j + c * L] = region[j + c * L];
+                for (int i = (head ? 8 : 0) + j; i < nfull * 8; i += L)
                     *reinterpret_cast<float4*>(__builtin_assume_aligned(lb + 4 * i, 16)) =
                         *reinterpret_cast<const float4*>(__builtin_assume_aligned(region + 4 * i, 16));
-                const float tail = region[nfull * 32 + (j < rem ? j : 0)];
-                if (g + 1 == g1) {  // the stream's last row: its tail line leaves partial
-                    if (j < rem) lb[nfull * 32 + j] = tail;
-                } else {
-                    carry = tail;
+                const bool last = g + 1 == g1;  // the stream's last row: its tail line leaves partial
+#pragma unroll
+                for (int c = 0; c < CW; ++c) {
+                    const int e = j + c * L;
+                    const float tail = region[nfull * 32 + (e < rem ? e : 0)];
+                    if (!last) carry[c] = tail;
+                    else if (e < rem) lb[nfull * 32 + e] = tail;
                 }
             }
         } else if constexpr (OK == 0 && !stage_rows(OK, VAR)) {  // lane-wise 8-byte stores

@@ -128,6 +128,7 @@ _SIGS = {
     "thesia_mt_get_spec": (_i, [_vp, _u64, _fp, _sz, C.POINTER(_sz), C.POINTER(_sz)]),
     "thesia_mt_get_grey": (_i, [_vp, _u64, _fp, _sz, C.POINTER(_u32), C.POINTER(_u32)]),
     "thesia_mt_track_count": (_i, [_vp, C.POINTER(_sz)]),
+    "thesia_mt_device_bytes": (_i, [_vp, C.POINTER(_sz)]),
 }
 
 for _name, (_res, _args) in _SIGS.items():

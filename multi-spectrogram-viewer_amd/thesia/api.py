@@ -187,6 +187,12 @@ class MultiTrack:
         check(lib.thesia_mt_get_grey(self.h, id, out.ctypes.data_as(_fp), out.size, C.byref(w), C.byref(h)))
         return out
 
+    def device_bytes(self) -> int:
+        """HBM the tracks hold (thesia_mt_device_bytes)."""
+        n = C.c_size_t()
+        check(lib.thesia_mt_device_bytes(self.h, C.byref(n)))
+        return n.value
+
     def __len__(self):
         n = C.c_size_t()
         check(lib.thesia_mt_track_count(self.h, C.byref(n)))

@@ -57,7 +57,7 @@ def global_db_range(local_max: float, local_min: float, local_max_sr: int, db_ra
     all_reduce(MAX) of (max, -min, max_sr) on host tensors; otherwise the local values are
     global. Three scalars are latency-bound on any transport, and the engine's buffers are not
     torch tensors, so a non-gloo group (RCCL "nccl") is shadowed by a gloo group over the same
-    ranks (created once, collectively) instead of staging the scalars on a GPU."""
+    ranks (made once on every rank by init_host_groups) instead of staging the scalars on a GPU."""
     import numpy as np
 
     mx, mn, sr = float(local_max), float(local_min), int(local_max_sr)
@@ -78,18 +78,43 @@ def global_db_range(local_max: float, local_min: float, local_max_sr: int, db_ra
     return gmax, gmin, sr
 
 
-_GLOO_SHADOW = {}
+_GLOO_SHADOW = {}  # tuple of global ranks -> gloo group over them
+
+
+def _ranks_key(dist, group):
+    return tuple(range(dist.get_world_size())) if group is None else tuple(dist.get_process_group_ranks(group))
+
+
+def init_host_groups(groups=(), force: bool = False) -> None:
+    """Create the gloo groups the range exchange runs on: one over the world and one over each
+    group in `groups`, in that order. Call it on EVERY rank, right after init_process_group:
+    new_group is collective over the whole default group (ranks outside a subgroup must enter it
+    too, in the same order), so creating a shadow lazily inside global_db_range -- where only a
+    subgroup's members would call -- could deadlock or mismatch groups. With a gloo default group
+    nothing is created (the groups themselves serve) unless `force` (tests: a gloo group standing
+    in for an RCCL one)."""
+    import torch.distributed as dist
+
+    for g in (None,) + tuple(groups):
+        if not force and dist.get_backend(g) == "gloo":
+            continue
+        key = _ranks_key(dist, g)
+        if key not in _GLOO_SHADOW:
+            _GLOO_SHADOW[key] = dist.new_group(ranks=list(key), backend="gloo")
 
 
 def _host_group(dist, group):
-    """`group` itself when it is gloo, else a gloo group over the same ranks (cached)."""
+    """The gloo group the three scalars are reduced on: a shadow made by init_host_groups for
+    `group`'s ranks (keyed by the rank tuple, never by id(): a collected group's id can be
+    reused), else `group` itself when it is gloo. A non-gloo group without a shadow is an error:
+    a lazy new_group here could deadlock (see init_host_groups)."""
+    key = _ranks_key(dist, group)
+    if key in _GLOO_SHADOW:
+        return _GLOO_SHADOW[key]
     if dist.get_backend(group) == "gloo":
         return group
-    key = id(group)
-    if key not in _GLOO_SHADOW:
-        ranks = None if group is None else dist.get_process_group_ranks(group)
-        _GLOO_SHADOW[key] = dist.new_group(ranks=ranks, backend="gloo")
-    return _GLOO_SHADOW[key]
+    raise RuntimeError("global_db_range over a non-gloo group needs thesia.shard.init_host_groups() "
+                       "called on every rank right after init_process_group")
 
 
 def up_ratio(sr: int, max_sr: int, freq_scale_mel: bool) -> float:

@@ -16,7 +16,7 @@ def c1_substitute() -> np.ndarray:
     clipped to int16, cut to the 2 113 529 samples audio.rs:66 expects. Returns int16 [n]."""
     from scipy.signal import resample_poly
 
-    x = np.load(os.path.join(GOLDEN, "sample_24k_full.npz"))["pcm_24k"].astype(np.float64)
+    x = np.load(os.path.join(GOLDEN, "samples_full.npz"))["pcm_24k"].astype(np.float64)
     y = np.clip(np.round(resample_poly(x, 2, 1)), -32768, 32767).astype(np.int16)
     assert y.shape[0] >= C1_LEN
     return y[:C1_LEN]
@@ -25,3 +25,12 @@ def c1_substitute() -> np.ndarray:
 def s16_to_f32(x: np.ndarray) -> np.ndarray:
     """hound int -> f32 as open_audio_file does for 16-bit PCM (audio.rs:16-19): i / 2^15."""
     return (x.astype(np.float32) / np.float32(32768.0)).astype(np.float32)
+
+
+SAMPLE_TAGS = ["8k", "16k", "22k05", "24k", "44k1"]
+
+
+def samples_full():
+    """The five committed sample WAVs whole: [(int16 pcm, sr)] in rate order."""
+    z = np.load(os.path.join(GOLDEN, "samples_full.npz"))
+    return [(z[f"pcm_{t}"], int(z[f"sr_{t}"])) for t in SAMPLE_TAGS]

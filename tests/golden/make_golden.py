@@ -13,8 +13,9 @@ reference is mounted at /root/reference; the GPU box never reads the reference).
      audio.rs:44-70    the missing 48 kHz sample's expected header (documentation only)
 2. samples_excerpt.npz -- int16 excerpts (first 1.5 s) of the reference's sample WAVs
    (data fixtures from /root/reference/samples), keyed by sample rate, plus full lengths.
-3. sample_24k_full.npz -- the whole 24 kHz sample (int16, 1 056 765 samples), the source of
-   the 48 kHz substitute for the missing samples/sample_48k.wav (config C1, SURVEY.md §8d;
+3. samples_full.npz -- the five sample WAVs whole (int16, 44.03 s each): config C2 at the size
+   BASELINE.json names, and (the 24 kHz one, 1 056 765 samples) the source of the 48 kHz
+   substitute for the missing samples/sample_48k.wav (config C1, SURVEY.md §8d;
    tests/fixtures.py c1_substitute).
 """
 import json
@@ -75,15 +76,21 @@ def samples():
     return out
 
 
-def sample_24k_full():
-    w = wave.open(os.path.join(REF, "samples", "sample_24k.wav"))
-    assert w.getnchannels() == 1 and w.getsampwidth() == 2 and w.getframerate() == 24000
-    return {"pcm_24k": np.frombuffer(w.readframes(w.getnframes()), np.int16), "sr": np.array(24000)}
+def samples_full():
+    """The five committed sample WAVs whole (int16 mono, 44.03 s each): BASELINE.json configs[1]
+    (C2) names them at full length; the 24 kHz one is also the source of the 48 kHz substitute."""
+    out = {}
+    for tag in ["8k", "16k", "22k05", "24k", "44k1"]:
+        w = wave.open(os.path.join(REF, "samples", f"sample_{tag}.wav"))
+        assert w.getnchannels() == 1 and w.getsampwidth() == 2
+        out[f"pcm_{tag}"] = np.frombuffer(w.readframes(w.getnframes()), np.int16)
+        out[f"sr_{tag}"] = np.array(w.getframerate())
+    return out
 
 
 if __name__ == "__main__":
     with open(os.path.join(HERE, "kats.json"), "w") as f:
         json.dump(kats(), f, indent=1)
     np.savez_compressed(os.path.join(HERE, "samples_excerpt.npz"), **samples())
-    np.savez_compressed(os.path.join(HERE, "sample_24k_full.npz"), **sample_24k_full())
-    print("wrote kats.json, samples_excerpt.npz, sample_24k_full.npz")
+    np.savez_compressed(os.path.join(HERE, "samples_full.npz"), **samples_full())
+    print("wrote kats.json, samples_excerpt.npz, samples_full.npz")

@@ -1,7 +1,7 @@
 """GPU parity on the BASELINE.json configurations at sizes the
 oracle finishes in seconds, plus size-independent properties at full size.
 
-  C2  the reference's 6 sample rates (5 committed excerpts + the 48 kHz substitute),
+  C2  the reference's 6 sample rates (the 5 committed samples whole + the 48 kHz substitute),
       n_fft 2048 / hop 512, power dB, one batch over all tracks (s16 input, audio.rs:16-19)
   C3  48 kHz 10 s mono tracks, n_fft 2048 / hop 512, mel-128 + amp dB
   C5  mixed rates x per-track n_fft in {256..2048}, amp dB -> global range -> grey ->
@@ -13,6 +13,7 @@ import os
 import numpy as np
 import pytest
 
+import fixtures
 import oracle_ffi as O
 from thesia import engine, pipeline, shard
 from tolerances import DB_MAX, DB_P9999, db_clamped_err
@@ -29,8 +30,11 @@ def _excerpts_s16(golden_dir):
     return out
 
 
-def test_c2_six_sample_rates_power_db(golden_dir):
-    tracks = _excerpts_s16(golden_dir)
+def test_c2_six_sample_rates_power_db():
+    """C2 at the size BASELINE.json names: the five sample WAVs whole (44.03 s each) + the
+    48 kHz substitute (2 113 529 samples), 13 946 frames in one batch."""
+    tracks = fixtures.samples_full() + [(fixtures.c1_substitute(), 48000)]
+    assert sum(engine.Batch.frames_for(engine.Plan(2048, 2048, 512, engine.OUT_POWER_DB), [len(t)]) for t, _ in tracks) == 13946
     n_fft, hop = 2048, 512
     plan = engine.Plan(n_fft, n_fft, hop, engine.OUT_POWER_DB)
     flat = np.concatenate([t for t, _ in tracks])

@@ -119,3 +119,27 @@ def test_add_tracks_error_leaves_state_unchanged(tmp_path, excerpts):
         mt.add_tracks([0, 1], p + "\n" + str(tmp_path / "missing.wav"))
     assert e.value.code == -2 and "os error" in str(e.value)
     assert len(mt) == 0
+
+
+def test_remove_frees_shared_pools():
+    """Ten tracks added by one call share one wav and one spectrogram buffer (one batched
+    launch); removing nine of them moves the survivor into buffers of its own and frees the
+    pools (the reference frees per track, lib.rs:265-292), its spectrogram bit-unchanged."""
+    rng = np.random.default_rng(5)
+    pcm = [(rng.standard_normal(48000 + 977 * i) * 0.1).astype(np.float32) for i in range(10)]
+    mt = thesia.MultiTrack()
+    mt.add_tracks_pcm(list(range(10)), pcm, [24000] * 10)
+    full = mt.device_bytes()
+    spec9 = mt.get_spec(9)
+    for i in range(9):
+        mt.remove_track(i)
+    assert len(mt) == 1
+    win, hop, n_fft = O.track_params(24000)
+    T, bins = spec9.shape
+    own = len(pcm[9]) * 4 + T * bins * 4  # wav + spectrogram of the survivor
+    grey = mt.get_grey(9)
+    left = mt.device_bytes()
+    assert left <= own + grey.nbytes + 4096, (full, left, own)
+    assert left < full / 5
+    assert np.array_equal(mt.get_spec(9).view(np.uint32), spec9.view(np.uint32))
+    assert len(mt.get_spec_image(9, 100.0, 64)) == int(np.float32(100.0) * np.float32(len(pcm[9])) / np.float32(24000)) * 64 * 3

@@ -171,3 +171,37 @@ def test_line_rows_equal_lane_rows(shift, max_blocks):
         b.close()
         dout.close()
     assert outs[0].view(np.uint32).tobytes() == outs[1].view(np.uint32).tobytes() == outs[2].view(np.uint32).tobytes()
+
+
+@pytest.mark.parametrize("n_fft", [256, 512, 1024])
+@pytest.mark.parametrize("max_blocks", [0, 2])
+def test_line_rows_all_sizes(n_fft, max_blocks):
+    """The whole-line complex row stores at every streaming size (a frame on L = 8 / 16 / 32
+    lanes, the carried line spread over 32 / L floats per lane): rows equal the oracle's
+    perform_stft within the STFT tolerance, guard floats on both sides untouched, with many
+    streams and with few long ones."""
+    rng = np.random.default_rng(n_fft + max_blocks)
+    hop = n_fft // 4
+    lens = [int(v) for v in rng.integers(n_fft - 1, 30 * n_fft, 23)]
+    tracks = [(rng.standard_normal((n, 2)) * 0.3).astype(np.float32) for n in lens]
+    plan = engine.Plan(n_fft, n_fft, hop, engine.OUT_COMPLEX)
+    flat = np.concatenate([t.reshape(-1) for t in tracks])
+    offs = np.cumsum([0] + [t.size for t in tracks[:-1]])
+    din = engine.DeviceBuffer.from_host(flat)
+    T = engine.Batch.frames_for(plan, lens)
+    fl = plan.row_bins * 2
+    guard, shift = 64, 14  # rows start 56 bytes into a 128-byte line
+    sentinel = np.float32(-4321.5)
+    dout = engine.DeviceBuffer.from_host(np.full(T * fl + 2 * guard, sentinel, np.float32))
+    b = engine.Batch(plan, din, offs, lens, dout.ptr.value + (guard - 32 + shift) * 4,
+                     input_format=engine.IN_F32, channels=2, max_blocks=max_blocks, kernel=3)
+    b.run()
+    engine.synchronize()
+    res = dout.to_host(np.float32)
+    lo = guard - 32 + shift
+    assert np.all(res[:lo] == sentinel) and np.all(res[lo + T * fl:] == sentinel)
+    got = res[lo:lo + T * fl]
+    for i, t in enumerate(tracks):
+        ref = O.perform_stft(_mono_fold(t), n_fft, hop, n_fft)
+        rows = got[int(b.frame0[i]) * fl:int(b.frame0[i + 1]) * fl].view(np.complex64).reshape(ref.shape)
+        assert stft_frame_err(rows, ref) <= STFT_REL, i

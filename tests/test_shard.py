@@ -100,3 +100,52 @@ def test_world_size_2_gloo_matches_single_process():
     ref = shard.global_db_range(max(r[0] for r in ranges), min(r[1] for r in ranges),
                                 max(sr for _, sr in tracks))
     assert res[0][2] == res[1][2] == ref
+
+
+def _sub_worker(rank, world, port, q):
+    """3 ranks; a subgroup {0, 2} stands in for an RCCL group (its gloo shadow forced): every rank
+    creates the shadows eagerly, then only the subgroup's members exchange their ranges."""
+    import torch.distributed as dist
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    sub = dist.new_group(ranks=[0, 2], backend="gloo")
+    shard.init_host_groups([sub], force=True)
+    out = None
+    if rank in (0, 2):
+        out = shard.global_db_range(-10.0 * (rank + 1), -100.0 - rank, 8000 * (rank + 1), group=sub)
+    dist.barrier()
+    q.put((rank, out, sorted(shard._GLOO_SHADOW)))
+    dist.destroy_process_group()
+
+
+def test_subgroup_exchange_with_eager_shadow_groups():
+    import torch.multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_sub_worker, args=(r, 3, port, q)) for r in range(3)]
+    for p in procs:
+        p.start()
+    res = sorted(q.get(timeout=120) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    ref = shard.global_db_range(-10.0, -102.0, 24000)  # max over {0, 2}, min over {0, 2}
+    assert res[0][1] == res[2][1] == ref and res[1][1] is None
+    assert all(r[2] == [(0, 1, 2), (0, 2)] for r in res)  # same shadows on every rank, keyed by ranks
+
+
+def test_non_gloo_group_without_shadow_is_an_error():
+    class FakeDist:  # an RCCL default group, no init_host_groups call
+        def get_world_size(self):
+            return 2
+
+        def get_backend(self, group=None):
+            return "nccl"
+
+        def get_process_group_ranks(self, group):
+            return [0, 1]
+    import pytest as _pt
+    with _pt.raises(RuntimeError, match="init_host_groups"):
+        shard._host_group(FakeDist(), None)
