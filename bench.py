@@ -73,6 +73,8 @@ def parse():
                         "0 lane-wise 8-byte, 1 LDS-staged 16-byte, 2 whole 128-byte lines)")
     p.add_argument("--row-stores", default="", help="A/B of the complex-output row stores (comma list, "
                    "interleaved rounds, one process), reported in roofline_window_rfft")
+    p.add_argument("--render-path", type=int, default=-1, help="c5: the display launch structure "
+                   "(thesia_set_render_path; -1 = the library default)")
     p.add_argument("--render-paths", default="", help="c5: A/B of the display launch structures "
                    "(thesia_set_render_path), comma list, interleaved rounds")
     p.add_argument("--selftest", action="store_true",
@@ -445,6 +447,8 @@ def main_c5(args, ws, rank, pg, device):
     tracks = []
     for i in mine:  # the generator is indexed by the global track id
         tracks += pipeline.c5_tracks(1, seconds=args.seconds, first=i, channels=args.channels)
+    if args.render_path >= 0:
+        engine.set_render_path(args.render_path)
     p = pipeline.RenderPipeline(tracks, px_per_sec=100.0, nheight=500, pinned_output=True)
 
     def step(want_rgb=False):
@@ -481,7 +485,7 @@ def main_c5(args, ws, rank, pg, device):
             for q in rp:
                 engine.set_render_path(q)
                 res[q].append(p.display_timed(3)["display_ms"])
-        engine.set_render_path(0)
+        engine.set_render_path(max(args.render_path, 0))
         if rank == 0:
             print(json.dumps({"render_paths_ms": {str(q): {"median": float(np.median(t)), "min": float(min(t))}
                                                   for q, t in res.items()}}), flush=True)
@@ -502,7 +506,8 @@ def main_c5(args, ws, rank, pg, device):
                                    f"grey + Lanczos3 + colormap RGB at 100 px/s x 500 px",
                        "ranks": ws, "per_rank_frames": summ["per_rank_frames"],
                        "tracks_per_gpu": len(tracks), "images_per_s": total / dt,
-                       "geometry_groups": len(p.groups), "frames_per_gpu": p.total_frames,
+                       "spectrogram_batches": len(p.groups), "display_groups": p._n_disp,
+                       "frames_per_gpu": p.total_frames,
                        "ms_per_step_with_rgb_copied_to_host": dt_host * 1e3,
                        "parallelism": f"file-sharded x{ws} (LPT), one all_reduce of 3 scalars"},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",

@@ -18,12 +18,13 @@
 //   Lane 0 (A = B = 0) pairs its own outputs differently (O with O, E with E, E[0] and E[8]
 //   with themselves: bins 0, NC and NC/2); per-slot selects cover it, as in stft3.
 //
-// Occupancy: the product build runs two waves per SIMD (8-wave blocks, 253 VGPRs: the ring,
-// the frame's points, the prefetched hop and the per-lane untangle rotations). Three waves
-// (12-wave blocks, <= 168 VGPRs) compile without spills only with the hop prefetched by
-// LDS-DMA and the rotations in LDS (THESIA_WV5=12 THESIA_DMA5=1 THESIA_SC5=2 THESIA_S32=1 ...),
-// and measured slower. The two frames of a wave keep their LDS regions on
-// opposite halves of the 64 banks.
+// Occupancy: two waves per SIMD (8-wave blocks, 253 VGPRs: the ring, the frame's points, the
+// prefetched hop and the per-lane untangle rotations). Three waves (12-wave blocks, <= 168
+// VGPRs) compiled without spills only with the hop prefetched by LDS-DMA, the rotations in LDS
+// and 32-bit frame words, and measured slower; those compile-time variants (and
+// the unfused window / split partner-row reads) were removed from this file in round 3 and live
+// in git history (commit 490a8f5, THESIA_WV5 / DMA5 / SC5 / S32 / WF5 / BH5 / TWC5 / PF5). The
+// two frames of a wave keep their LDS regions on opposite halves of the 64 banks.
 #include "stft3_core.hpp"
 
 #include <type_traits>
@@ -47,33 +48,10 @@ namespace thesia {
 #define MARK5(x, i)
 #endif
 
-#ifndef THESIA_WV5
-#define THESIA_WV5 8
-#endif
-#ifndef THESIA_WF5
-#define THESIA_WF5 1
-#endif
-#ifndef THESIA_BH5
-#define THESIA_BH5 1
-#endif
-#ifndef THESIA_SC5
-#define THESIA_SC5 1
-#endif
-#ifndef THESIA_TWC5
-#define THESIA_TWC5 8
-#endif
-// the next hop's samples by LDS-DMA (global_load_lds_dwordx4, no VGPRs) into the wave's two
-// stream regions after the mel, stereo f32 only (experiment: three waves per SIMD)
-#ifndef THESIA_DMA5
-#define THESIA_DMA5 0
-#endif
-#ifndef THESIA_S32
-#define THESIA_S32 0
-#endif
 struct Geo5 {
     static constexpr int NC = 1024, L = 32, P = 32, FPW = 2, F = NC + 1, SH = P / 4;
     static constexpr int S = L + 4;       // transpose row stride (16 lanes of a b128 read: distinct banks)
-    static constexpr int WV = THESIA_WV5;  // waves per block: 4 per SIMD x WV/4
+    static constexpr int WV = 8;          // waves per block: 2 per SIMD
     static constexpr int BLOCK = 64 * WV;
     static constexpr int STREAMS = WV * FPW;
     // region per stream: the transpose (P * S = 1152 floats), the |X| row (1028) or a staged
@@ -82,17 +60,8 @@ struct Geo5 {
     static constexpr int RS = 1184, RS_MIN = 1152;
     static constexpr int WL_STRIDE = 2 * P + 4, WL_FLOATS = L * WL_STRIDE;
     static constexpr int TW_FLOATS = 2 * P * L;
-    static constexpr int SCT_FLOATS = THESIA_SC5 == 2 ? 16 * L * 2 : 0;  // rotation table (SC5 == 2)
-    static constexpr int TAB_FLOATS = WL_FLOATS + TW_FLOATS + SCT_FLOATS;
-    static constexpr int TWC = THESIA_TWC5;  // stage-1 twiddle float4 reads per batch
-    static constexpr int BH = THESIA_BH5;    // parts the partner row B is read in
-#if THESIA_DMA5
-    static constexpr int PF_POS = 3;  // the DMA lands in the stream regions: after the mel
-#elif defined(THESIA_PF5)
-    static constexpr int PF_POS = THESIA_PF5;  // where the next hop's loads issue (3: after the mel)
-#else
-    static constexpr int PF_POS = WV == 8 ? 0 : 2;  // where the next hop's loads issue
-#endif
+    static constexpr int TAB_FLOATS = WL_FLOATS + TW_FLOATS;
+    static constexpr int TWC = 8;  // stage-1 twiddle float4 reads per batch
     static_assert(RS_MIN >= P * S && RS_MIN >= F + 6 && RS_MIN % 4 == 0 && RS % 4 == 0, "region");
 };
 
@@ -114,27 +83,12 @@ __device__ __forceinline__ void rot16(float2 ub, float& s, float& co) {
 // The realfft untangle of slots I0 <= i < I1 (see the header): calls
 // epi(k, re, im, integral_constant<2 (i - I0) + h>) for bin k (h = 0) and NC - k (h = 1).
 // v[ce_pos(16, i)] = E[i], v[16 + ce_pos(16, i)] = O[i].
-// rotation sources: the (sin, cos) of slot i rotated per frame from the two bases, or read
-// from a per-lane table computed once (THESIA_SC5: 32 VGPRs for 64 VALU per frame pair)
-struct RotBases {
-    float2 lo, hi;
-    template <int I>
-    __device__ __forceinline__ void get(float& s, float& co) const { rot16<I>(I < 8 ? lo : hi, s, co); }
-};
+// The (sin, cos) of slot i come from a per-lane table computed once from the lane's two bases
+// (32 VGPRs held for 64 VALU per frame pair).
 struct RotTable {
     const float2 (&t)[16];
     template <int I>
     __device__ __forceinline__ void get(float& s, float& co) const { s = t[I].x; co = t[I].y; }
-};
-// the same values from an LDS table [16][L] (THESIA_SC5 == 2: no registers held across frames)
-struct RotLds {
-    const float2* t;  // + lane j
-    template <int I>
-    __device__ __forceinline__ void get(float& s, float& co) const {
-        const float2 v = t[I * Geo5::L];
-        s = v.x;
-        co = v.y;
-    }
 };
 
 template <int I0, int I1, class Rot, class Epi>
@@ -290,9 +244,6 @@ stft5_kernel(StftLaunch a, uint64_t fps, int rs) {
     int* k0_lds = reinterpret_cast<int*>(mel_lds + (OK == 2 && !packed ? a.mel4_rows * L : 0));
     int2* rd_lds = reinterpret_cast<int2*>(k0_lds + (OK == 2 && !packed ? a.mel4_rounds * L : 0));
     int* xo_lds = reinterpret_cast<int*>(rd_lds + (OK == 2 && !packed ? a.mel4_rounds : 0));
-#if THESIA_SC5 == 2
-    float2* sct_lds = reinterpret_cast<float2*>(lds + G::WL_FLOATS + G::TW_FLOATS);
-#endif
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int slot = lane / L, j = lane % L;
     const bool lane0 = j == 0;
@@ -320,35 +271,19 @@ stft5_kernel(StftLaunch a, uint64_t fps, int rs) {
     }
     // untangle bases: slots 0..7 start at bin kb_lo (lane 0: 32), slots 8..15 at bin j
     float2 ub_lo = a.sincos[lane0 ? 32 : j], ub_hi = a.sincos[j];
-#if THESIA_SC5 == 2
-    if (threadIdx.x < L)
-        static_for<0, 16>([&](auto ic) {
-            constexpr int i = decltype(ic)::value;
-            float sv, cv;
-            rot16<i>(i < 8 ? ub_lo : ub_hi, sv, cv);
-            sct_lds[i * L + j] = make_float2(sv, cv);
-        });
-    const RotLds rot{sct_lds + j};
-#elif THESIA_SC5
     float2 sct[16];
     static_for<0, 16>([&](auto ic) {
         constexpr int i = decltype(ic)::value;
         rot16<i>(i < 8 ? ub_lo : ub_hi, sct[i].x, sct[i].y);
     });
     const RotTable rot{sct};
-#endif
     const int kb_lo = lane0 ? 32 : j;
     __syncthreads();
 
     const uint64_t total = a.total_frames;
     const uint64_t stream = ((uint64_t)blockIdx.x * G::WV + wave) * FPW + slot;
-#if THESIA_S32  // 32-bit frame / sample words (total frames < 2^32, tracks < 2^31 samples)
-    using FI = uint32_t;
-    using SI = int32_t;
-#else
     using FI = uint64_t;
     using SI = int64_t;
-#endif
     const FI g0 = (FI)(stream * fps);
     const FI g1 = (FI)(stream * fps + fps < total ? stream * fps + fps : total);
     const int hop = a.hop;
@@ -357,8 +292,6 @@ stft5_kernel(StftLaunch a, uint64_t fps, int rs) {
 
     float2 raw[P];
     CT pre[SH];
-    constexpr bool kDma = THESIA_DMA5 && C == 2 && INF == IN_F32;
-    float* wave_area = work + wave * FPW * rs;  // the wave's two stream regions, contiguous
     bool pre_ok = false;
     int hint = -1;
     FI g_beg = 1, g_end = 0;
@@ -376,10 +309,6 @@ stft5_kernel(StftLaunch a, uint64_t fps, int rs) {
         MARK5(top, 7);
         const FI g = g0 + (FI)it;
         const bool valid = g < g1;
-#if !THESIA_SC5
-        asm volatile("" : "+v"(ub_lo.x), "+v"(ub_lo.y), "+v"(ub_hi.x), "+v"(ub_hi.y));
-        const RotBases rot{ub_lo, ub_hi};
-#endif
         // opaque per frame: keeps the per-lane offsets (window row, transpose rows, untangle
         // bins) inside the loop instead of hoisted as loop invariants into dozens of VGPRs
         int wj = j, wjb = jb, wkb = kb_lo;
@@ -397,27 +326,11 @@ stft5_kernel(StftLaunch a, uint64_t fps, int rs) {
             start = (SI)(g - g_beg) * hop - NC;  // half_win = NC, pad_left = 0
         }
         // ---- the frame's raw samples: shift by SH points + the prefetched hop ----
-        if constexpr (kDma) {  // the hop landed in the wave's regions by LDS-DMA: into the ring first
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            if (pre_ok) {
-#pragma unroll
-                for (int q = 0; q < SH; ++q) pre[q] = reinterpret_cast<const CT*>(wave_area + q * 256)[lane];
-#pragma unroll
-                for (int n1 = 0; n1 < P - SH; ++n1) raw[n1] = raw[n1 + SH];
-#pragma unroll
-                for (int q = 0; q < SH; ++q) raw[P - SH + q] = CK::mix(pre[q]);
-            }
-            // the other stream's lanes may refill their region below (generic loads): their
-            // writes must not pass these reads (a cross-lane hazard the per-thread model misses)
-            wave_lds_sync();
-        }
         if (pre_ok) {
-            if constexpr (!kDma) {
 #pragma unroll
-                for (int n1 = 0; n1 < P - SH; ++n1) raw[n1] = raw[n1 + SH];
+            for (int n1 = 0; n1 < P - SH; ++n1) raw[n1] = raw[n1 + SH];
 #pragma unroll
-                for (int q = 0; q < SH; ++q) raw[P - SH + q] = CK::mix(pre[q]);
-            }
+            for (int q = 0; q < SH; ++q) raw[P - SH + q] = CK::mix(pre[q]);
         } else if (valid && start >= 0 && start + 2 * NC <= n && ((base + (uint64_t)start * C) % (2 * C)) == 0) {
             const CT* src = reinterpret_cast<const CT*>(in + base + (uint64_t)start * C) + j;
             static_for<0, P / 8>([&](auto gc) {
@@ -435,9 +348,8 @@ stft5_kernel(StftLaunch a, uint64_t fps, int rs) {
             for (int n1 = 0; n1 < P; ++n1) raw[n1] = make_float2(0.f, 0.f);
         }
         MARK5(loaded, 0);
-        // ---- prefetch the next frame's hop of new samples (its points P-SH .. P-1): right
-        // after the window at 2 waves/SIMD (a whole frame to land, as stft3), after the
-        // untangle at 3 (register budget) ----
+        // ---- prefetch the next frame's hop of new samples (its points P-SH .. P-1) right
+        // away: a whole frame to land, as stft3 ----
         auto prefetch = [&]() {
             const SI nstart = start + hop;
             const bool nxt = valid && g + 1 < g1 && g + 1 < g_end && nstart + 2 * NC <= n &&
@@ -445,25 +357,13 @@ stft5_kernel(StftLaunch a, uint64_t fps, int rs) {
                              ((base + (uint64_t)(nstart + 2 * L * (P - SH)) * C) % (2 * C)) == 0;
             if (nxt) {
                 const CT* src = reinterpret_cast<const CT*>(in + base + (uint64_t)(nstart + 2 * L * (P - SH)) * C) + j;
-                if constexpr (kDma) {
-                    // lane l of the wave lands at byte 16 l of each 1 KiB block: stream s's 32
-                    // lanes fill bytes [512 s, 512 s + 512); the regions' last reads are done
-                    wave_lds_sync();
 #pragma unroll
-                    for (int q = 0; q < SH; ++q)
-                        __builtin_amdgcn_global_load_lds(
-                            (__attribute__((address_space(1))) void*)(src + L * q),
-                            (__attribute__((address_space(3))) void*)(wave_area + q * 256), 16, 0, 0);
-                } else {
-#pragma unroll
-                    for (int q = 0; q < SH; ++q) pre[q] = src[L * q];
-                }
+                for (int q = 0; q < SH; ++q) pre[q] = src[L * q];
             }
             pre_ok = nxt;
         };
-        if constexpr (G::PF_POS == 0) prefetch();
+        prefetch();
         // ---- stage 1: DFT-32 over n1, twiddles W_NC^{j k1} ----
-#if THESIA_WF5
         // window (lib.rs:379, with the 1/2 of realfft.rs:148-154 folded in) inside the first
         // radix-4 level of the DFT-32 (dif_fft's N = 32 level): the products of inputs 2 and 3
         // are formed once and the ones of inputs 0 and 1 ride in the butterfly fmas (12 VALU per
@@ -497,19 +397,6 @@ stft5_kernel(StftLaunch a, uint64_t fps, int rs) {
         dif_fft<8, 1, 16, P>(v);
         dif_fft<8, 1, 24, P>(v);
         pin(v);
-#else
-        // window (lib.rs:379, with the 1/2 of realfft.rs:148-154 folded in)
-        float2 v[P];
-        static_for<0, P / 2>([&](auto qc) {
-            constexpr int q = decltype(qc)::value;
-            const float4 w = wrow[q];
-            v[2 * q] = make_float2(raw[2 * q].x * w.x, raw[2 * q].y * w.y);
-            v[2 * q + 1] = make_float2(raw[2 * q + 1].x * w.z, raw[2 * q + 1].y * w.w);
-        });
-        pin(v);
-        dif_fft<P, 1, 0, P>(v);
-        pin(v);
-#endif
         MARK5(stage1, 1);
         {
             const float4* tp = reinterpret_cast<const float4*>(twtab) + wj;
@@ -558,28 +445,25 @@ stft5_kernel(StftLaunch a, uint64_t fps, int rs) {
                 constexpr int nn = decltype(nc)::value;
                 put(v[nn], get(v[nn]) + get(v[nn + 16]));
             });
-            // row B (in THESIA_BH5 parts): v[16 + n].e = B[n] - B[n + 16]
-            static_for<0, G::BH>([&](auto hc) {
-                constexpr int h = decltype(hc)::value, QP = 4 / G::BH;  // float4 pairs per part
-                if constexpr (G::BH > 1) __builtin_amdgcn_sched_barrier(0);
-                float4 xb[2 * QP];
-                static_for<0, QP>([&](auto qc) {
-                    constexpr int q = h * QP + decltype(qc)::value;
-                    xb[decltype(qc)::value] = rb[q];
-                    xb[QP + decltype(qc)::value] = rb[q + 4];
+            // row B: v[16 + n].e = B[n] - B[n + 16]
+            {
+                float4 xb[8];
+                static_for<0, 4>([&](auto qc) {
+                    constexpr int q = decltype(qc)::value;
+                    xb[q] = rb[q];
+                    xb[4 + q] = rb[q + 4];
                 });
-                static_for<0, QP>([&](auto uc) {
-                    constexpr int u = decltype(uc)::value, n0 = 4 * (h * QP + u);
-                    put(v[16 + n0], xb[u].x - xb[u + QP].x);
-                    put(v[17 + n0], xb[u].y - xb[u + QP].y);
-                    put(v[18 + n0], xb[u].z - xb[u + QP].z);
-                    put(v[19 + n0], xb[u].w - xb[u + QP].w);
+                static_for<0, 4>([&](auto uc) {
+                    constexpr int u = decltype(uc)::value, n0 = 4 * u;
+                    put(v[16 + n0], xb[u].x - xb[u + 4].x);
+                    put(v[17 + n0], xb[u].y - xb[u + 4].y);
+                    put(v[18 + n0], xb[u].z - xb[u + 4].z);
+                    put(v[19 + n0], xb[u].w - xb[u + 4].w);
                 });
-            });
+            }
         }
         wave_lds_sync();
         MARK5(transposed, 3);
-        if constexpr (G::PF_POS == 1) prefetch();
         MARK5(prefetched, 4);
         // ---- stage 2: W_32^n on B's differences, then the two DFT-16s ----
         static_for<1, 16>([&](auto nc) {
@@ -629,7 +513,6 @@ stft5_kernel(StftLaunch a, uint64_t fps, int rs) {
                 for (int k = F; k < Geo2<NC>::F4; ++k) region[k] = 0.0f;
             }
             wave_lds_sync();
-            if constexpr (G::PF_POS == 2) prefetch();
             MARK5(untangled, 6);
             if (packed) {
                 if (a.melp_steps == 2) melp5<2>(a, region, pm_lds, pw_lds, j, g, valid);
@@ -640,9 +523,7 @@ stft5_kernel(StftLaunch a, uint64_t fps, int rs) {
             else if (a.mel_chunks == 4) mel4p<NC, 4>(a, region, mel_lds, xo_lds, j, g, valid);
             else mel4<NC, 8, 1>(a, region, mel_lds, rd_lds, k0_lds, j, g, valid);
 #endif
-            if constexpr (G::PF_POS == 3) prefetch();
         } else if constexpr (OK == 0) {  // lane-wise 8-byte stores
-            if constexpr (G::PF_POS == 2) prefetch();
             float2* crow = reinterpret_cast<float2*>(a.out) + g * F;
             auto st = [&](int k, float xr, float xi, auto) {
                 if (valid) st_out(crow + k, make_float2(xr, xi));
@@ -679,7 +560,6 @@ stft5_kernel(StftLaunch a, uint64_t fps, int rs) {
                 stg[NC] = val_of(ar - bi, 0.0f);
             }
             wave_lds_sync();
-            if constexpr (G::PF_POS == 2) prefetch();
             if (valid) store_row_b128<L>(frow, sh, region, F, j);
         }
     }

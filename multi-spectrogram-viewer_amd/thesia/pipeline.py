@@ -3,10 +3,12 @@ per-track n_fft, dB + colormap render) over the HBM-resident engine.
 
 The reference computes this one track at a time inside MultiTrack (lib.rs:112-136 for the
 spectrogram, lib.rs:193-263 for the global range and grey images, lib.rs:294-298 for the RGB
-image). Here tracks are grouped by geometry -- (sample rate, n_fft): one Plan (window, tables)
+image). Here tracks are grouped by geometry -- n_fft / win / hop: one Plan (window, tables)
 and one Batch (one kernel launch over all the group's tracks) per group -- and the spectrograms
 never leave HBM: the per-track max/min, grey image, Lanczos3 resize and colormap run on the
-device, and only the RGB bytes come back.
+device, and only the RGB bytes come back. (Amp dB rows do not depend on the rate, so the
+spectrogram batches are per (n_fft, win, hop, layout) with every rate inside; the display
+groups are per batch and rate.)
 
 Semantics follow the viewer with FreqScale::Linear (the C5 config names no mel): amp dB
 (decibel.rs:79-88), global range max = min(max, 0), min = max(min, max - db_range) over ALL
@@ -46,11 +48,14 @@ class Rendered:
 
 
 def _geometry(t: Track):
+    """The spectrogram batch a track joins: amp dB rows do not depend on the sample rate (the
+    window is hann(win) / n_fft, lib.rs:138-140; the rate only picks the mel filterbank), so
+    tracks of every rate with one n_fft / win / hop / layout share one launch."""
     win = t.win_length or t.n_fft
     hop = t.hop_length or t.n_fft // 4
     ch = 1 if t.pcm.ndim == 1 else t.pcm.shape[1]
     fmt = engine.IN_S16 if t.pcm.dtype == np.int16 else engine.IN_F32
-    return (t.sr, t.n_fft, win, hop, ch, fmt)
+    return (t.n_fft, win, hop, ch, fmt)
 
 
 class RenderPipeline:
@@ -70,10 +75,14 @@ class RenderPipeline:
         groups: "OrderedDict[tuple, List[int]]" = OrderedDict()
         for i, t in enumerate(self.tracks):
             groups.setdefault(_geometry(t), []).append(i)
-        self.groups = []
+        self.groups = []  # spectrogram batches: (plan, din, dout, batch), one launch each
         self.where = {}  # track -> (group index, row offset, T, bins)
-        for (sr, n_fft, win, hop, ch, fmt), idx in groups.items():
-            plan = engine.Plan(n_fft, win, hop, engine.OUT_AMP_DB, sr=sr)
+        # display groups: the tracks of one batch and one sample rate (contiguous in the batch:
+        # tracks are ordered by rate inside it), so the display's tap counts follow the rate
+        disp = []  # (batch index, first track in the batch, count)
+        for (n_fft, win, hop, ch, fmt), idx in groups.items():
+            idx.sort(key=lambda i: (self.tracks[i].sr, i))
+            plan = engine.Plan(n_fft, win, hop, engine.OUT_AMP_DB, sr=self.tracks[idx[0]].sr)
             flat = np.concatenate([np.ascontiguousarray(self.tracks[i].pcm).reshape(-1) for i in idx])
             lens = [self.tracks[i].pcm.shape[0] for i in idx]
             offs = np.cumsum([0] + [self.tracks[i].pcm.size for i in idx[:-1]]).astype(np.uint64)
@@ -83,22 +92,29 @@ class RenderPipeline:
             b = engine.Batch(plan, din, offs, lens, dout, input_format=fmt, channels=ch)
             g = len(self.groups)
             self.groups.append((plan, din, dout, b))
+            k0 = 0
             for k, i in enumerate(idx):
                 f0, f1 = int(b.frame0[k]), int(b.frame0[k + 1])
                 self.where[i] = (g, f0 * plan.row_bins, f1 - f0, plan.row_bins)
+                if k + 1 == len(idx) or self.tracks[idx[k + 1]].sr != self.tracks[i].sr:
+                    disp.append((g, k0, k + 1 - k0))
+                    k0 = k + 1
+        self._batch_order = [i for idx in groups.values() for i in idx]
         self.total_frames = sum(grp[3].total_frames for grp in self.groups)
         # display geometry, fixed for the pipeline's life: every group in one library call
         # (thesia_minmax_segments_multi / thesia_render_rgb_multi), tracks in group order
         self._geo = []
         for i, t in enumerate(self.tracks):
             self._geo.append(int(np.float32(px_per_sec) * np.float32(t.pcm.shape[0]) / np.float32(t.sr)))
-        self._order = np.array([i for idx in groups.values() for i in idx], np.int64)
-        ng = len(self.groups)
+        self._order = np.array(self._batch_order, np.int64)  # = display groups in order
+        ng = len(disp)
         self._row0 = [np.ascontiguousarray(b.frame0, np.uint64) for _, _, _, b in self.groups]
-        self._c_specs = (C.c_void_p * max(ng, 1))(*[dout.ptr.value for _, _, dout, _ in self.groups])
-        self._c_row0 = (_u64p * max(ng, 1))(*[r.ctypes.data_as(_u64p) for r in self._row0])
-        self._c_bins = (C.c_size_t * max(ng, 1))(*[plan.row_bins for plan, _, _, _ in self.groups])
-        self._c_ns = (C.c_size_t * max(ng, 1))(*[len(idx) for idx in groups.values()])
+        self._c_specs = (C.c_void_p * max(ng, 1))(*[self.groups[g][2].ptr.value for g, _, _ in disp])
+        self._c_row0 = (_u64p * max(ng, 1))(*[C.cast(self._row0[g].ctypes.data + 8 * k0, _u64p)
+                                             for g, k0, _ in disp])
+        self._c_bins = (C.c_size_t * max(ng, 1))(*[self.groups[g][0].row_bins for g, _, _ in disp])
+        self._c_ns = (C.c_size_t * max(ng, 1))(*[n for _, _, n in disp])
+        self._n_disp = ng
         self._nw = np.array([self._geo[i] for i in self._order], np.uint32)
         self._sizes = self._nw.astype(np.uint64) * nheight * 3
         self._off = np.concatenate([[0], np.cumsum(self._sizes)[:-1]]).astype(np.uint64)
@@ -108,9 +124,9 @@ class RenderPipeline:
         # folded into the streaming kernel's row epilogue): 3 int32 per track, call order
         self._d_range = engine.DeviceBuffer(12 * max(len(self._order), 1))
         t0 = 0
-        for (_, _, _, b), ntr in zip(self.groups, self._c_ns):
+        for _, _, _, b in self.groups:
             b.set_option(engine.OPT_RANGE, self._d_range.ptr.value + 12 * t0)
-            t0 += ntr
+            t0 += len(b.frame0) - 1
         self._up = {}  # max_sr -> up_ratio per track (call order)
         self._max_sr = max((t.sr for t in self.tracks), default=0)
 
@@ -150,7 +166,7 @@ class RenderPipeline:
                            for i in self._order.tolist()], np.float32)
             self._up[max_sr] = up
         check(lib.thesia_render_rgb_multi(
-            len(self.groups), self._c_specs, self._c_row0, self._c_bins, self._c_ns,
+            self._n_disp, self._c_specs, self._c_row0, self._c_bins, self._c_ns,
             up.ctypes.data_as(_fp), self._nw.ctypes.data_as(C.POINTER(C.c_uint32)), self.nheight,
             gmax, gmin, self._rgb.ptr, self._off.ctypes.data_as(_u64p)))
         total = self._rgb_total

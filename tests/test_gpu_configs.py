@@ -16,7 +16,7 @@ import pytest
 import fixtures
 import oracle_ffi as O
 from thesia import engine, pipeline, shard
-from tolerances import DB_MAX, DB_P9999, db_clamped_err
+from tolerances import DB_MAX, DB_P9999, db_clamped_err, db_err_relative_to_oracle, stft_f64
 
 pytestmark = pytest.mark.gpu
 
@@ -47,13 +47,18 @@ def test_c2_six_sample_rates_power_db():
     b.run()
     engine.synchronize()
     got = dout.to_host(np.float32, (T, plan.row_bins))
+    w = (O.hann(n_fft) / np.float32(n_fft)).astype(np.float32)
     for k, (pcm, sr) in enumerate(tracks):
         x = (0.0 + pcm.astype(np.float32) / np.float32(32768.0)).astype(np.float32)  # lib.rs:42 fold
         ref = O.power_to_db_default(O.norm_sqr(O.perform_stft(x, n_fft, hop, n_fft)))
         g = got[int(b.frame0[k]):int(b.frame0[k + 1])]
         assert g.shape == ref.shape
-        mx, p = db_clamped_err(g, ref)
-        assert mx <= DB_MAX and p <= DB_P9999, (sr, mx, p)
+        # the reference's own f32 error at the -120 dB floor of a 44 s real recording reaches
+        # 0.39 dB (16 kHz sample): the bound is relative to it (tolerances.py)
+        X = stft_f64(x, n_fft, hop, n_fft, w)
+        exact = 10.0 * np.log10(np.maximum(X.real ** 2 + X.imag ** 2, 1e-36))
+        ok, ge, oe = db_err_relative_to_oracle(g, ref, exact)
+        assert ok, (sr, ge, oe)
 
 
 def test_c3_mel128_mono_10s():
@@ -98,7 +103,7 @@ def test_c5_mixed_rate_render_pipeline():
         assert r.rgb.tobytes() == img.tobytes(), (t.sr, t.n_fft)  # display path bit-exact
 
 
-@pytest.mark.parametrize("path", [0, 1, 2, 3, 4])  # two-kernel (LDS-DMA horizontal) / per-track / three-stage / single-kernel / register-staged horizontal
+@pytest.mark.parametrize("path", [0, 1, 2, 3, 4, 5])  # two-kernel (LDS-DMA horizontal) / per-track / three-stage / single-kernel / register-staged horizontal / band-streaming
 @pytest.mark.parametrize("px_per_sec", [73.0, 30.0, 9.0, 2.0])  # 30: 17-64 taps; 9, 2: wider spans
 @pytest.mark.parametrize("nheight", [90, 400, 600])  # 400, 600: H -> nheight downsampling ~2.5, taller
 def test_render_batch_ragged_groups(path, px_per_sec, nheight):
@@ -107,17 +112,22 @@ def test_render_batch_ragged_groups(path, px_per_sec, nheight):
     three-stage one) and the per-track launches produce the oracle's bytes for every image
     (ragged T, nwidth and workspace offsets; staged and direct horizontal spans)."""
     engine.set_render_path(path)
+    c0 = engine.render_counts()
     try:
         _ragged(px_per_sec, nheight)
     finally:
         engine.set_render_path(0)
+    if path == 5:  # the band-streaming kernel ran (for the groups whose LDS it fits)
+        assert engine.render_counts()[2] > c0[2]
 
 
 def _ragged(px_per_sec, nheight):
     base = pipeline.c5_tracks(12, seconds=0.6)
     tracks = []
-    for k, t in enumerate(base[:4] * 3):  # 4 geometries x 3 lengths each
-        n = int(t.pcm.shape[0] * (0.5 + 0.35 * (k // 4))) + 3 * k
+    # the 12 (rate, n_fft) geometries x 2 lengths: 4 spectrogram batches (one per n_fft) of 3
+    # rates each, so every display group is a slice of a batch's rows
+    for k, t in enumerate(base * 2):
+        n = int(t.pcm.shape[0] * (0.5 + 0.45 * (k // 12))) + 3 * k
         n = max(n, t.n_fft)
         tracks.append(pipeline.Track(t.pcm[:n].copy(), t.sr, t.n_fft))
     out = pipeline.render_tracks(tracks, px_per_sec=px_per_sec, nheight=nheight, keep_db=True)

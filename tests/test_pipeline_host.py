@@ -11,4 +11,7 @@ def test_c5_generator_cycles_rates_and_sizes():
     assert len({(t.sr, t.n_fft) for t in ts}) == 12
     assert all(t.pcm.dtype == np.int16 and t.pcm.ndim == 1 and len(t.pcm) == round(0.05 * t.sr)
                for t in ts)
-    assert pipeline._geometry(ts[0]) == (8000, 256, 256, 64, 1, 1)
+    # spectrogram batches are per n_fft / win / hop / layout (amp dB rows do not depend on the
+    # rate): the 12 (rate, n_fft) pairs fall into 4 batches of 3 rates each
+    assert pipeline._geometry(ts[0]) == (256, 256, 64, 1, 1)
+    assert len({pipeline._geometry(t) for t in ts}) == 4
