@@ -279,17 +279,10 @@ int thesia_minmax_segments_device(const float* d_spec, const uint64_t* row0, siz
  * one pass over the spectrogram, then one for horizontal Lanczos3 + colormap (row spans staged
  * by LDS-DMA), every track of a call in each launch; 1 = per-track launches (the reference's one
  * image at a time structure); 2 = every track in one launch per stage: grey, vertical,
- * horizontal + colormap; 3 = one kernel per group for the whole display (the intermediate in
- * LDS) where the group's tiles fit, else as 0; 4 = as 0 with the previous register-staged
- * horizontal pass (3 and 4 measured slower on C5: kept selectable and parity-tested,
- * DESIGN.md §4); 5 = the band-streaming kernel (a block walks a band of output rows of one
- * track left to right, the intermediate in an LDS ring, nothing recomputed) where its LDS fits,
- * else as 0. */
+ * horizontal + colormap. (Single-kernel displays -- the intermediate in LDS, per tile or as a
+ * ring walked by a band of rows -- were built, byte-exact, and measured 1.5-4.7x slower on C5:
+ * DESIGN.md §4.) */
 int thesia_set_render_path(int path);
-/* Geometry groups rendered so far by the batched display, per launch structure (process-wide,
- * monotonic): out[0] two-kernel (grey + vertical, horizontal + colormap), out[1] single-kernel
- * (path 3), out[2] band-streaming (path 5). Diagnostic (tests check which structure ran). */
-int thesia_render_counts(uint64_t out[3]);
 int thesia_render_rgb_batch_device(const float* d_spec, const uint64_t* row0, size_t bins,
                                    size_t n, const float* up_ratio, const uint32_t* nwidth,
                                    uint32_t nheight, float max, float min, uint8_t* d_rgb,

@@ -357,11 +357,7 @@ int thesia_batch_set_option(thesia_batch* batch, int option, int64_t value) {
 }
 
 int thesia_set_render_path(int path) { return set_render_path(path); }
-int thesia_render_counts(uint64_t out[3]) {
-    if (!out) return set_error(THESIA_ERR_INVALID_ARG, "null argument");
-    render_counts(out);
-    return THESIA_OK;
-}
+
 
 int thesia_synth_pcm_device(void* d_out, int format, uint32_t channels, uint64_t n_tracks,
                             uint64_t n_samples, uint32_t sr, uint64_t seed) {

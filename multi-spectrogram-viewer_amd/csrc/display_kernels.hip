@@ -1068,440 +1068,6 @@ int launch_render_batch2(const float* spec, uint32_t bins, float max, float min,
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
-// ------------------------------------------------------------------------------------
-// Fully fused display (launch_render_fused): grey + vertical Lanczos3 + horizontal Lanczos3 +
-// colormap in one kernel; the f32 intermediate between the passes lives in LDS only
-// ------------------------------------------------------------------------------------
-// A block owns a tile of R output rows x kFPx output columns of one track. The horizontal taps
-// of those columns reach frames [xa, xa + S) of the track; the vertical taps of those rows reach
-// grey rows [ya, ya + G) (each row's taps zero-padded to kv as in grey_vert_kernel: exact).
-// 1) the grey tile [G][S] is formed from the dB spectrogram (flat (frame, row) staging, all of a
-//    thread's loads in flight together); 2) the vertical sums of the R rows for every frame of
-//    the span go to an LDS tile [R][S] (lane = frame, wave-uniform rows, float4 weight
-//    broadcasts) -- exactly the values grey_vert_kernel would store to HBM; 3) the horizontal
-//    sums of the tile's columns read that LDS tile (KT register weights, zero-padded), the
-//    colormap writes RGB bytes to LDS, and the tile's rows leave as aligned 32-bit words. Rows
-//    below oz are colormap(+0) (their vertical sums are +0 exactly; the horizontal sum of +0
-//    terms is +0). Every sum runs in the reference's order, so the bytes equal the two-kernel
-//    path's and the oracle's.
-constexpr int kFPx = 64;  // output columns per block
-template <int KT>
-__global__ void __launch_bounds__(256) render_fused_kernel(const float* spec, uint32_t bins, float max,
-                                                           float min, uint32_t nh, const RenderDesc* d,
-                                                           const uint8_t* cmap, uint8_t* rgb, int R, int kv,
-                                                           int s_cap, int g_cap) {
-    extern __shared__ __attribute__((aligned(16))) float fsm[];
-    const RenderDesc r = d[blockIdx.z];
-    const uint32_t ox0 = blockIdx.x * kFPx, ob = blockIdx.y * (uint32_t)R;
-    if (ox0 >= r.nw || ob >= nh) return;  // block-uniform
-    const int tid = threadIdx.x, lane = tid & 63;
-    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const uint32_t npx = r.nw - ox0 < (uint32_t)kFPx ? r.nw - ox0 : (uint32_t)kFPx;
-    const uint32_t oy1 = ob + (uint32_t)R < nh ? ob + (uint32_t)R : nh;
-    const uint32_t nrow = oy1 - ob;
-    const uint32_t oyz = ob > r.oz ? ob : r.oz;  // first row with a nonzero vertical sum
-    const int32_t xa = r.hl[ox0];
-    const int32_t S = r.hl[ox0 + npx - 1] + r.hc[ox0 + npx - 1] - xa;  // <= s_cap (host)
-    const int SP = s_cap + KT;            // tmp row stride: span + KT zero columns
-    const int GS = (s_cap | 63) + 2;      // grey row stride (== 1 mod 64: conflict-free staging)
-    float* wl = fsm;                                  // [R][kv] zero-padded vertical weights
-    int* meta = reinterpret_cast<int*>(wl + R * kv);  // [R] first grey row of each output row
-    float* tmp = reinterpret_cast<float*>(meta + ((R + 3) & ~3));  // [R][SP]
-    float* gt = tmp + R * SP;                         // [g_cap][GS]
-    uint8_t* out = reinterpret_cast<uint8_t*>(gt + g_cap * GS);  // [R][kFPx * 3]
-    uint8_t* cm = out + R * kFPx * 3;
-    if (tid < 30) cm[tid] = cmap[tid];
-    const int32_t H = (int32_t)r.H, top = (int32_t)r.H - (int32_t)bins;
-    if (oyz < oy1) {
-        const uint32_t jz = oyz - ob;  // rows [jz, nrow) are formed
-        const int32_t ya = r.vl[oyz];
-        const int32_t G = r.vl[oy1 - 1] - ya + kv;  // <= g_cap (host)
-        const float* sp = spec + r.spec_off;
-        // 1) grey tile: element e = (frame f, row k), k fastest (consecutive bins of one frame)
-        const int total = S * G;
-        const uint32_t mrec = G > 1 ? (uint32_t)((0x100000000ull + G - 1) / (uint32_t)G) : 0u;
-        for (int e0 = 0; e0 < total; e0 += 256 * 8) {
-            float v[8];
-#pragma unroll
-            for (int i = 0; i < 8; ++i) {
-                const uint32_t e = (uint32_t)(e0 + 256 * i + tid);
-                const uint32_t f = G > 1 ? __umulhi(e, mrec) : e;
-                const int32_t k = (int32_t)(e - f * (uint32_t)G), y = ya + k;
-                v[i] = 0.0f;
-                if ((int)e < total && y >= top && y < H)
-                    v[i] = sp[(uint64_t)(uint32_t)(xa + (int32_t)f) * bins + (uint32_t)(H - 1 - y)];
-            }
-#pragma unroll
-            for (int i = 0; i < 8; ++i) {
-                const uint32_t e = (uint32_t)(e0 + 256 * i + tid);
-                const uint32_t f = G > 1 ? __umulhi(e, mrec) : e;
-                const int32_t k = (int32_t)(e - f * (uint32_t)G), y = ya + k;
-                if ((int)e < total) gt[k * GS + (int)f] = (y >= top && y < H) ? grey_of(v[i], max, min) : 0.0f;
-            }
-        }
-        for (uint32_t e = tid; e < nrow * (uint32_t)kv; e += 256) {
-            const uint32_t j = e / (uint32_t)kv, i = e - j * (uint32_t)kv;
-            float w = 0.0f;
-            if (j >= jz) {
-                const uint32_t oy = ob + j;
-                if ((int32_t)i < r.vc[oy]) w = r.vw[r.vo[oy] + i];
-            }
-            wl[e] = w;
-        }
-        for (uint32_t j = tid; j < nrow; j += 256) meta[j] = j >= jz ? r.vl[ob + j] - ya : 0;
-        // tmp columns [S, S + KT): zeros (the horizontal sums run KT terms branch-free)
-        for (int e = tid; e < (int)nrow * KT; e += 256) tmp[(e / KT) * SP + S + (e % KT)] = 0.0f;
-        __syncthreads();
-        // 2) vertical sums: wave w takes frame chunks w, w + 4, ...; lane = frame
-        const float4* wl4 = reinterpret_cast<const float4*>(wl);
-        const int kv4 = kv >> 2;
-        for (int x0 = wave * 64; x0 < S; x0 += 256) {
-            const int x = x0 + lane;
-            const bool ok = x < S;
-            const float* col = gt + x;
-            uint32_t j = jz;
-            for (; j + 3 < nrow; j += 4) {
-                int lq[4];
-#pragma unroll
-                for (int q = 0; q < 4; ++q) lq[q] = __builtin_amdgcn_readfirstlane(meta[j + q]);
-                float t[4] = {0.0f, 0.0f, 0.0f, 0.0f};
-                for (int i4 = 0; i4 < kv4; ++i4) {
-#pragma unroll
-                    for (int q = 0; q < 4; ++q) {
-                        const float4 w = wl4[(j + q) * kv4 + i4];
-                        const float* c = col + (lq[q] + 4 * i4) * GS;
-                        t[q] += c[0] * w.x;
-                        t[q] += c[GS] * w.y;
-                        t[q] += c[2 * GS] * w.z;
-                        t[q] += c[3 * GS] * w.w;
-                    }
-                }
-                if (ok) {
-#pragma unroll
-                    for (int q = 0; q < 4; ++q) tmp[(j + q) * SP + x] = t[q];
-                }
-            }
-            for (; j < nrow; ++j) {
-                const int l = __builtin_amdgcn_readfirstlane(meta[j]);
-                float t = 0.0f;
-                for (int i4 = 0; i4 < kv4; ++i4) {
-                    const float4 w = wl4[j * kv4 + i4];
-                    const float* c = col + (l + 4 * i4) * GS;
-                    t += c[0] * w.x;
-                    t += c[GS] * w.y;
-                    t += c[2 * GS] * w.z;
-                    t += c[3 * GS] * w.w;
-                }
-                if (ok) tmp[j * SP + x] = t;
-            }
-        }
-    }
-    __syncthreads();
-    // 3) horizontal sums + colormap: column c = tid & 63, rows j = tid >> 6, + 4, ...
-    {
-        const uint32_t c = (uint32_t)lane;
-        const bool act = c < npx;
-        const uint32_t ox = ox0 + c;
-        int32_t l = 0, n = 0;
-        const float* wr = r.hw;
-        if (act) {
-            l = r.hl[ox] - xa;
-            n = r.hc[ox];
-            wr = r.hw + r.ho[ox];
-        }
-        float w[KT];
-#pragma unroll
-        for (int i = 0; i < KT; ++i) w[i] = i < n ? wr[i] : 0.0f;
-        for (uint32_t j = (uint32_t)wave; j < nrow; j += 4) {
-            float t = 0.0f;
-            if (ob + j >= oyz) {
-                const float* row = tmp + j * SP + l;
-#pragma unroll
-                for (int i = 0; i < KT; ++i) t += row[i] * w[i];
-            }
-            if (act) colormap_px(t, cm, out + j * (kFPx * 3) + 3 * c);
-        }
-    }
-    __syncthreads();
-    // the tile's RGB rows: aligned 32-bit words (3-byte pixels stored lane by lane would be byte
-    // stores at stride 3)
-    const uint32_t nb = 3 * npx;
-    for (uint32_t j = (uint32_t)wave; j < nrow; j += 4) {
-        const uint8_t* sg = out + j * (kFPx * 3);
-        uint8_t* g = rgb + r.rgb_off + ((uint64_t)(ob + j) * r.nw + ox0) * 3;
-        const uint32_t mis = (uint32_t)(reinterpret_cast<uintptr_t>(g) & 3);
-        const uint32_t head = mis ? (4 - mis < nb ? 4 - mis : nb) : 0;
-        if ((uint32_t)lane < head) g[lane] = sg[lane];
-        const uint32_t nwords = (nb - head) / 4;
-        uint32_t* gw = reinterpret_cast<uint32_t*>(g + head);
-        for (uint32_t k = lane; k < nwords; k += 64) {
-            const uint32_t b = head + 4 * k;
-            gw[k] = (uint32_t)sg[b] | ((uint32_t)sg[b + 1] << 8) | ((uint32_t)sg[b + 2] << 16) |
-                    ((uint32_t)sg[b + 3] << 24);
-        }
-        for (uint32_t b = head + 4 * nwords + lane; b < nb; b += 64) g[b] = sg[b];
-    }
-}
-
-int render_fused_lds_bytes(int R, int kv, int s_cap, int g_cap, int kt) {
-    const int SP = s_cap + kt, GS = (s_cap | 63) + 2;
-    return (R * kv + ((R + 3) & ~3) + R * SP + g_cap * GS) * 4 + R * kFPx * 3 + 32;
-}
-
-int launch_render_fused(const float* spec, uint32_t bins, float max, float min, const RenderDesc* d_desc,
-                        uint32_t n, uint32_t nw_max, uint32_t nh, int kt, int R, int kv, int s_cap,
-                        int g_cap, const uint8_t* cmap, uint8_t* rgb, hipStream_t s) {
-    if (n == 0 || nh == 0) return 0;
-    if (n > 65535 || R <= 0 || R > 64 || (kv & 3) || kv <= 0) return -2;
-    const int lds = render_fused_lds_bytes(R, kv, s_cap, g_cap, kt);
-    if (lds > 163840) return -2;
-    auto kern = kt == 48 ? render_fused_kernel<48> : kt == 32 ? render_fused_kernel<32>
-              : kt == 16 ? render_fused_kernel<16> : nullptr;
-    if (!kern) return -2;
-    if (hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
-                            hipFuncAttributeMaxDynamicSharedMemorySize, lds) != hipSuccess)
-        return -1;
-    dim3 g((nw_max + kFPx - 1) / kFPx, (nh + R - 1) / R, n);
-    hipLaunchKernelGGL(kern, g, dim3(256), lds, s, spec, bins, max, min, nh, d_desc, cmap, rgb, R, kv,
-                       s_cap, g_cap);
-    return hipGetLastError() == hipSuccess ? 0 : -1;
-}
-
-// ------------------------------------------------------------------------------------
-// Band-streaming display (render path 5): grey + vertical Lanczos3 + horizontal Lanczos3 +
-// colormap in one kernel, the f32 intermediate never leaves LDS and is never recomputed.
-// ------------------------------------------------------------------------------------
-// A block owns a band of R output rows of one track and walks the image's columns left to right
-// in chunks of CC. The vertical sums of the band (the intermediate rows) live in an LDS ring of
-// RW frame slots, [slot][R + 1] (row fastest): a chunk needs frames [hl[c0], hl[c1-1] + hc[c1-1]);
-// the frames it adds to the ring are the ones no earlier chunk needed, so every vertical sum is
-// formed once per band. The new frames are formed in steps of up to 64:
-//  1) a step's grey rows [ya, ya + G) (the band's taps, each row's taps zero-padded to kv: exact,
-//     as in grey_vert_kernel) come from the dB spectrogram -- every load of the step issued at
-//     once into registers, and issued one step AHEAD (during the previous step's sums and the
-//     previous chunk's horizontal pass), then written as grey values into the LDS tile gt[G][65];
-//  2) vertical sums: lane = frame, four wave-uniform rows per step, float4 weight broadcasts:
-//     ring[frame][j] = sum_i grey[vl[j] + i][frame] * wv[j][i] (t = 0; t += in * w);
-//  3) per chunk, horizontal sums: lane = output row j, wave-uniform column c (a wave takes
-//     columns w, w + 4, ...): t = sum_i ring[hl[c] + i][j] * wh[c][i], the taps zero-padded to a
-//     multiple of 4 (the padded slots hold finite values of other frames or +0: exact);
-//     colormap into an LDS tile [R][CC * 3], whose rows leave as aligned 32-bit words.
-// Rows below oz have vertical sums +0 exactly and horizontal sums +0: colormap(+0) without any
-// arithmetic. Every sum runs in the reference's order: the bytes equal the two-kernel path's.
-constexpr int kStreamThreads = 256;
-constexpr int kStreamLoads = 32;  // grey loads per thread per step (host: G x 64 <= 256 x 32)
-__global__ void __launch_bounds__(kStreamThreads, 2) render_stream_kernel(
-    const float* spec, uint32_t bins, float max, float min, uint32_t nh, const RenderDesc* d,
-    const uint8_t* cmap, uint8_t* rgb, int R, int CC, int RW, int GC, int kv, int KH) {
-    extern __shared__ __attribute__((aligned(16))) float ssm[];
-    const RenderDesc r = d[blockIdx.z];
-    const uint32_t ob = blockIdx.x * (uint32_t)R;
-    if (ob >= nh) return;  // block-uniform
-    const int tid = threadIdx.x, lane = tid & 63;
-    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const int RS = R + 1;                      // ring slot stride (conflict-free either way)
-    const uint32_t nrow = nh - ob < (uint32_t)R ? nh - ob : (uint32_t)R;
-    const uint32_t jz = r.oz > ob ? (r.oz - ob < nrow ? r.oz - ob : nrow) : 0u;  // rows [jz, nrow) formed
-    // LDS carve-up (host: render_stream_lds_bytes)
-    float* ring = ssm;                                    // [RW][RS]
-    float* gt = ring + RW * RS;                           // [GC][65]
-    float* wv = gt + GC * 65;                             // [R][kv] vertical weights, zero-padded
-    float* wh = wv + R * kv;                              // [CC][KH] horizontal weights, zero-padded
-    int* meta = reinterpret_cast<int*>(wh + CC * KH);     // [R] first tile row of each output row
-    int* hlc = meta + R;                                  // [CC] first frame of each column
-    uint8_t* out = reinterpret_cast<uint8_t*>(hlc + CC);  // [R][CC * 3]
-    uint8_t* cm = out + ((R * CC * 3 + 15) & ~15);
-    if (tid < 30) cm[tid] = cmap[tid];
-    const uint32_t ringsz = (uint32_t)(RW * RS);
-    for (uint32_t e = tid; e < ringsz; e += kStreamThreads) ring[e] = 0.0f;  // finite padded reads
-    const int32_t H = (int32_t)r.H, top = (int32_t)r.H - (int32_t)bins;
-    const float* sp = spec + r.spec_off;
-    const bool formed = jz < nrow;
-    int32_t ya = 0, G = 0;
-    if (formed) {
-        ya = r.vl[ob + jz];
-        G = r.vl[ob + nrow - 1] - ya + kv;  // <= GC (host)
-        for (uint32_t e = tid; e < (uint32_t)R * (uint32_t)kv; e += kStreamThreads) {
-            const uint32_t j = e / (uint32_t)kv, i = e - j * (uint32_t)kv;
-            float w = 0.0f;
-            if (j >= jz && j < nrow && (int32_t)i < r.vc[ob + j]) w = r.vw[r.vo[ob + j] + i];
-            wv[e] = w;
-        }
-        for (uint32_t j = tid; j < (uint32_t)R; j += kStreamThreads)
-            meta[j] = (j >= jz && j < nrow) ? r.vl[ob + j] - ya : 0;
-    }
-    const float4* wv4 = reinterpret_cast<const float4*>(wv);
-    const int kv4 = kv >> 2, KH4 = KH >> 2;
-    const uint32_t mrec = G > 1 ? (uint32_t)((0x100000000ull + G - 1) / (uint32_t)G) : 0u;
-    const uint32_t nchunk = (r.nw + (uint32_t)CC - 1) / (uint32_t)CC;
-    auto xb_of = [&](uint32_t c) -> int32_t {  // frames chunk c reads end here
-        const uint32_t last = (c + 1) * (uint32_t)CC < r.nw ? (c + 1) * (uint32_t)CC - 1 : r.nw - 1;
-        return r.hl[last] + r.hc[last];
-    };
-    // the step after frames [0, xd) are formed, chunk c being current: (first frame, count, chunk)
-    struct Step { int32_t x0, nf; uint32_t c; };
-    auto step_after = [&](int32_t xd, uint32_t c) -> Step {
-        for (; c < nchunk; ++c) {
-            const int32_t xb = xb_of(c);
-            if (xd < xb) return Step{xd, xb - xd < 64 ? xb - xd : 64, c};
-        }
-        return Step{xd, 0, nchunk};
-    };
-    // a step's loads: element e = tid + 256 q = (frame f, tile row k), k fastest
-    float pv[kStreamLoads];
-    auto issue = [&](const Step& st) {
-        const int total = st.nf * G;
-#pragma unroll
-        for (int q = 0; q < kStreamLoads; ++q) {
-            const uint32_t e = (uint32_t)(kStreamThreads * q + tid);
-            const uint32_t f = G > 1 ? __umulhi(e, mrec) : e;
-            const int32_t k = (int32_t)(e - f * (uint32_t)G), y = ya + k;
-            pv[q] = 0.0f;
-            if ((int)e < total && y >= top && y < H)
-                pv[q] = sp[(uint64_t)(uint32_t)(st.x0 + (int32_t)f) * bins + (uint32_t)(H - 1 - y)];
-        }
-    };
-    auto consume = [&](const Step& st) {
-        const int total = st.nf * G;
-#pragma unroll
-        for (int q = 0; q < kStreamLoads; ++q) {
-            const uint32_t e = (uint32_t)(kStreamThreads * q + tid);
-            const uint32_t f = G > 1 ? __umulhi(e, mrec) : e;
-            const int32_t k = (int32_t)(e - f * (uint32_t)G), y = ya + k;
-            if ((int)e < total) gt[k * 65 + (int)f] = (y >= top && y < H) ? grey_of(pv[q], max, min) : 0.0f;
-        }
-    };
-    Step pend = formed ? step_after(0, 0) : Step{0, 0, nchunk};
-    if (pend.nf > 0) issue(pend);
-    uint8_t* orow = rgb + r.rgb_off + (uint64_t)ob * r.nw * 3;
-    for (uint32_t ci = 0; ci < nchunk; ++ci) {
-        const uint32_t c0 = ci * (uint32_t)CC;
-        const uint32_t ncol = r.nw - c0 < (uint32_t)CC ? r.nw - c0 : (uint32_t)CC;
-        __syncthreads();  // the previous chunk's horizontal reads of wh / hlc / ring and its stores
-        for (uint32_t e = tid; e < (uint32_t)CC * (uint32_t)KH; e += kStreamThreads) {
-            const uint32_t c = e / (uint32_t)KH, i = e - c * (uint32_t)KH;
-            float w = 0.0f;
-            if (c < ncol && (int32_t)i < r.hc[c0 + c]) w = r.hw[r.ho[c0 + c] + i];
-            wh[e] = w;
-        }
-        for (uint32_t c = tid; c < (uint32_t)CC; c += kStreamThreads) hlc[c] = c < ncol ? r.hl[c0 + c] : 0;
-        // 1-2) this chunk's new frames, step by step, the next step's loads in flight meanwhile
-        bool synced = false;
-        while (pend.nf > 0 && pend.c == ci) {  // block-uniform
-            const Step cur = pend;
-            consume(cur);
-            __syncthreads();  // gt complete
-            pend = step_after(cur.x0 + cur.nf, ci);
-            if (pend.nf > 0) issue(pend);
-            {
-                const bool ok = lane < cur.nf;
-                float* slot = ring + ((cur.x0 + lane) & (RW - 1)) * RS;
-                const float* col = gt + lane;
-                uint32_t j = jz + (uint32_t)wave * 4;
-                for (; j + 3 < nrow; j += 16) {
-                    int lq[4];
-#pragma unroll
-                    for (int q = 0; q < 4; ++q) lq[q] = __builtin_amdgcn_readfirstlane(meta[j + q]);
-                    float t[4] = {0.0f, 0.0f, 0.0f, 0.0f};
-                    for (int i4 = 0; i4 < kv4; ++i4) {
-#pragma unroll
-                        for (int q = 0; q < 4; ++q) {
-                            const float4 w = wv4[(j + q) * kv4 + i4];
-                            const float* c = col + (lq[q] + 4 * i4) * 65;
-                            t[q] += c[0] * w.x;
-                            t[q] += c[65] * w.y;
-                            t[q] += c[130] * w.z;
-                            t[q] += c[195] * w.w;
-                        }
-                    }
-                    if (ok) {
-#pragma unroll
-                        for (int q = 0; q < 4; ++q) slot[j + q] = t[q];
-                    }
-                }
-                for (; j < nrow; ++j) {  // the band's last rows (fewer than 4 left for this wave)
-                    const int l = __builtin_amdgcn_readfirstlane(meta[j]);
-                    float t = 0.0f;
-                    for (int i4 = 0; i4 < kv4; ++i4) {
-                        const float4 w = wv4[j * kv4 + i4];
-                        const float* c = col + (l + 4 * i4) * 65;
-                        t += c[0] * w.x;
-                        t += c[65] * w.y;
-                        t += c[130] * w.z;
-                        t += c[195] * w.w;
-                    }
-                    if (ok) slot[j] = t;
-                }
-            }
-            __syncthreads();  // gt free again; the new ring slots visible
-            synced = true;
-        }
-        if (!synced) __syncthreads();  // wh / hlc visible (block-uniform)
-        // 3) horizontal sums + colormap: lane = row, wave-uniform columns
-        {
-            const uint32_t j = (uint32_t)lane;
-            const bool act = j < nrow;
-            const bool live = j >= jz && act;
-            const float4* wh4 = reinterpret_cast<const float4*>(wh);
-            for (uint32_t c = (uint32_t)wave; c < ncol; c += kStreamThreads / 64) {
-                const int l = __builtin_amdgcn_readfirstlane(hlc[c]);
-                float t = 0.0f;
-                if (live) {
-                    for (int i4 = 0; i4 < KH4; ++i4) {
-                        const float4 w = wh4[c * KH4 + i4];
-                        const int f = l + 4 * i4;
-                        t += ring[((f + 0) & (RW - 1)) * RS + j] * w.x;
-                        t += ring[((f + 1) & (RW - 1)) * RS + j] * w.y;
-                        t += ring[((f + 2) & (RW - 1)) * RS + j] * w.z;
-                        t += ring[((f + 3) & (RW - 1)) * RS + j] * w.w;
-                    }
-                }
-                if (act) colormap_px(t, cm, out + j * (uint32_t)(CC * 3) + 3 * c);
-            }
-        }
-        __syncthreads();
-        // the chunk's RGB rows as aligned 32-bit words
-        const uint32_t nb = 3 * ncol;
-        for (uint32_t j = (uint32_t)wave; j < nrow; j += kStreamThreads / 64) {
-            const uint8_t* sg = out + j * (uint32_t)(CC * 3);
-            uint8_t* g = orow + ((uint64_t)j * r.nw + c0) * 3;
-            const uint32_t mis = (uint32_t)(reinterpret_cast<uintptr_t>(g) & 3);
-            const uint32_t head = mis ? (4 - mis < nb ? 4 - mis : nb) : 0;
-            if ((uint32_t)lane < head) g[lane] = sg[lane];
-            const uint32_t nwords = (nb - head) / 4;
-            uint32_t* gw = reinterpret_cast<uint32_t*>(g + head);
-            for (uint32_t k = lane; k < nwords; k += 64) {
-                const uint32_t b = head + 4 * k;
-                gw[k] = (uint32_t)sg[b] | ((uint32_t)sg[b + 1] << 8) | ((uint32_t)sg[b + 2] << 16) |
-                        ((uint32_t)sg[b + 3] << 24);
-            }
-            for (uint32_t b = head + 4 * nwords + lane; b < nb; b += 64) g[b] = sg[b];
-        }
-    }
-}
-
-int render_stream_lds_bytes(int R, int CC, int RW, int GC, int kv, int KH) {
-    return (RW * (R + 1) + GC * 65 + R * kv + CC * KH + R + CC) * 4 + ((R * CC * 3 + 15) & ~15) + 32;
-}
-
-int launch_render_stream(const float* spec, uint32_t bins, float max, float min, const RenderDesc* d_desc,
-                         uint32_t n, uint32_t nh, int R, int CC, int RW, int GC, int kv, int KH,
-                         const uint8_t* cmap, uint8_t* rgb, hipStream_t s) {
-    if (n == 0 || nh == 0) return 0;
-    if (n > 65535 || R <= 0 || R > 64 || CC <= 0 || RW < 4 || (RW & (RW - 1)) || (kv & 3) || kv <= 0 ||
-        (KH & 3) || KH <= 0 || GC <= 0 || (GC & 3) || GC * 64 > kStreamThreads * kStreamLoads)
-        return -2;
-    const int lds = render_stream_lds_bytes(R, CC, RW, GC, kv, KH);
-    if (lds > 163840) return -2;
-    if (hipFuncSetAttribute(reinterpret_cast<const void*>(render_stream_kernel),
-                            hipFuncAttributeMaxDynamicSharedMemorySize, lds) != hipSuccess)
-        return -1;
-    dim3 g((nh + R - 1) / R, 1, n);
-    hipLaunchKernelGGL(render_stream_kernel, g, dim3(kStreamThreads), lds, s, spec, bins, max, min, nh, d_desc,
-                       cmap, rgb, R, CC, RW, GC, kv, KH);
-    return hipGetLastError() == hipSuccess ? 0 : -1;
-}
-
 int launch_resize_h_rgb(const float* in, uint32_t w, uint32_t nh, uint32_t nw,
                         const int32_t* left, const int32_t* cnt, const int32_t* woff,
                         const float* wts, int max_taps, const uint8_t* cmap, uint8_t* out,

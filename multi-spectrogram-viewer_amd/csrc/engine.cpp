@@ -909,13 +909,10 @@ int minmax_device(const float* d_x, uint64_t n, float* mx, float* mn, bool* nan,
 }
 
 static int g_render_path = 0;  // thesia_set_render_path
-static uint64_t g_render_counts[3] = {0, 0, 0};  // groups rendered: two-kernel / single-kernel / band-streaming
-void render_counts(uint64_t* out) {
-    for (int i = 0; i < 3; ++i) out[i] = __atomic_load_n(&g_render_counts[i], __ATOMIC_RELAXED);
-}
+
 int render_path() { return __atomic_load_n(&g_render_path, __ATOMIC_RELAXED); }
 int set_render_path(int path) {
-    if (path < 0 || path > 5) return set_error(THESIA_ERR_INVALID_ARG, "render path must be 0 .. 5");
+    if (path < 0 || path > 2) return set_error(THESIA_ERR_INVALID_ARG, "render path must be 0 .. 2");
     __atomic_store_n(&g_render_path, path, __ATOMIC_RELAXED);
     return THESIA_OK;
 }
@@ -1122,9 +1119,6 @@ int minmax_segments_device(const float* d_x, const uint64_t* row0, size_t bins, 
     return minmax_segments_multi(1, &d_x, &row0, &bins, &n, mx, mn, nan, s);
 }
 
-#ifndef THESIA_FUSED_LDS
-#define THESIA_FUSED_LDS 49152  // LDS per block of the single-kernel display (render path 3)
-#endif
 #ifndef THESIA_VBAND
 #define THESIA_VBAND 64  // widest vertical band tried (64 beat 128-512 on C5: more blocks)
 #endif
@@ -1158,12 +1152,6 @@ struct FusedGroup {
     uint64_t tmp_tot = 0;         // intermediate floats ([nheight][T] per track)
     uint32_t T_max = 0, H_max = 0, nw_max = 0, v_band = 1;
     int h_taps = 0, h_span = 0, v_rows = 1, v_kv = 4;
-    // the single-kernel display (launch_render_fused), when the group's tiles fit
-    bool fused = false;
-    int f_R = 0, f_kt = 0, f_scap = 0, f_gcap = 0;
-    // the band-streaming display (launch_render_stream), when its LDS fits
-    bool stream = false;
-    int s_R = 0, s_CC = 0, s_RW = 0, s_GC = 0, s_KH = 0;
 };
 
 // Host planning of one group: a RenderDesc per non-empty track (appended to `desc`), the
@@ -1231,77 +1219,6 @@ int plan_fused_group(const float* d_spec, const uint64_t* row0, size_t bins, siz
     };
     g.v_band = THESIA_VBAND;
     while (!band_need(g.v_band, &g.v_rows) && g.v_band > 1) g.v_band /= 2;
-    // band-streaming display (render path 5): the most rows per band, then the widest column
-    // chunk, whose grey tile, intermediate ring and tiles fit two blocks per CU (else one)
-    if (render_path() == 5 && g.ndesc > 0) {
-        const int KH = (g.h_taps + 3) & ~3;
-        std::vector<const DevTaps*> hts;
-        for (size_t t = g.desc0; t < desc.size(); ++t) {
-            const DevTaps* ht = nullptr;
-            if (dev_taps(desc[t].T, desc[t].nw, &ht)) return THESIA_ERR_DEVICE;
-            hts.push_back(ht);
-        }
-        auto span_need = [&](int CC) {
-            int sp = 4;
-            for (size_t t = 0; t < hts.size(); ++t) {
-                const uint32_t nw = desc[g.desc0 + t].nw;
-                for (uint32_t c0 = 0; c0 < nw; c0 += (uint32_t)CC) {
-                    const uint32_t c1 = std::min(nw, c0 + (uint32_t)CC) - 1;
-                    sp = std::max(sp, hts[t]->h_left[c1] + hts[t]->h_count[c1] - hts[t]->h_left[c0]);
-                }
-            }
-            return sp;
-        };
-        for (int cap : {81920, 163840}) {
-            for (int R : {64, 32, 16}) {
-                int gc = 1;
-                band_need((uint32_t)R, &gc);
-                gc = (gc + 3) & ~3;
-                if (gc > 128) continue;  // a step's loads: <= 32 per thread
-                for (int CC : {64, 32, 16}) {
-                    int rw = 4;
-                    while (rw < span_need(CC)) rw *= 2;
-                    if (render_stream_lds_bytes(R, CC, rw, gc, kv, KH) <= cap) {
-                        g.stream = true;
-                        g.s_R = R; g.s_CC = CC; g.s_RW = rw; g.s_GC = gc; g.s_KH = KH;
-                        break;
-                    }
-                }
-                if (g.stream) break;
-            }
-            if (g.stream) break;
-        }
-    }
-    // single-kernel display (render path 3; measured 1.5-2.9x slower per group than the two
-    // kernels on C5): horizontal taps in registers (<= 48), the widest frame
-    // span of a 64-column tile, and the most output rows per tile whose grey rows, span and
-    // intermediate fit THESIA_FUSED_LDS bytes of LDS
-    if (render_path() == 3 && g.ndesc > 0) {
-        const int kt = g.h_taps <= 16 ? 16 : g.h_taps <= 32 ? 32 : g.h_taps <= 48 ? 48 : 0;
-        int s_need = 1;
-        for (size_t t = g.desc0; t < desc.size(); ++t) {
-            const DevTaps* ht = nullptr;
-            if (dev_taps(desc[t].T, desc[t].nw, &ht)) return THESIA_ERR_DEVICE;
-            for (uint32_t o0 = 0; o0 < desc[t].nw; o0 += 64) {
-                const uint32_t o1 = std::min(desc[t].nw, o0 + 64) - 1;
-                s_need = std::max(s_need, ht->h_left[o1] + ht->h_count[o1] - ht->h_left[o0]);
-            }
-        }
-        if (kt && s_need <= 4096) {
-            for (int R : {16, 12, 8, 4}) {
-                int g_need = 1;
-                band_need((uint32_t)R, &g_need);
-                if (render_fused_lds_bytes(R, kv, s_need, g_need, kt) <= THESIA_FUSED_LDS) {
-                    g.fused = true;
-                    g.f_R = R;
-                    g.f_kt = kt;
-                    g.f_scap = s_need;
-                    g.f_gcap = g_need;
-                    break;
-                }
-            }
-        }
-    }
     return THESIA_OK;
 }
 
@@ -1381,28 +1298,12 @@ int render_rgb_fused(size_t n_groups, const float* const* d_specs, const uint64_
         ws.key = std::move(key);
     }
     const std::vector<FusedGroup>& groups = ws.groups;
-    for (const FusedGroup& g : groups)  // which launch structure each group ran (tests, reports)
-        if (g.ndesc) __atomic_add_fetch(&g_render_counts[g.stream ? 2 : g.fused ? 1 : 0], 1, __ATOMIC_RELAXED);
-    // the horizontal pass: LDS-DMA row staging (display_kernels.hip resize_h_dma_kernel); path 4
-    // = the register-staged pass it replaced (kept for A/B, byte-identical)
-    const bool h_dma = rpath != 4;
+    // the horizontal pass: LDS-DMA row staging (display_kernels.hip resize_h_dma_kernel; the
+    // register-staged pass of the three-stage path where a span does not fit)
+    const bool h_dma = true;
     for (const FusedGroup& g : groups)
         for (size_t b = 0; b < g.ndesc; b += 65535) {  // grid.z limit
             const uint32_t nb = (uint32_t)std::min<size_t>(65535, g.ndesc - b);
-            if (g.stream) {
-                if (launch_render_stream(g.spec, g.bins, max, min, ws.desc.as<RenderDesc>() + g.desc0 + b, nb,
-                                         nheight, g.s_R, g.s_CC, g.s_RW, g.s_GC, g.v_kv, g.s_KH, cmap_ptr,
-                                         d_rgb, s))
-                    return set_error(THESIA_ERR_DEVICE, "band-streaming render launch failed");
-                continue;
-            }
-            if (g.fused) {
-                if (launch_render_fused(g.spec, g.bins, max, min, ws.desc.as<RenderDesc>() + g.desc0 + b, nb,
-                                        g.nw_max, nheight, g.f_kt, g.f_R, g.v_kv, g.f_scap, g.f_gcap, cmap_ptr,
-                                        d_rgb, s))
-                    return set_error(THESIA_ERR_DEVICE, "fused render launch failed");
-                continue;
-            }
             if (launch_render_batch2(g.spec, g.bins, max, min, ws.desc.as<RenderDesc>() + g.desc0 + b, nb,
                                      g.T_max, g.H_max, g.nw_max, nheight, g.h_taps, g.h_span, g.v_band,
                                      g.v_rows, g.v_kv, ws.tmp.as<float>(), cmap_ptr, d_rgb, s, h_dma))
@@ -1467,7 +1368,7 @@ int render_rgb_batch_device(const float* d_spec, const uint64_t* row0, size_t bi
     int crc = 0;
     const uint8_t* cmap_ptr = colormap_device(&crc);
     if (crc) return crc;
-    if (render_path() == 0 || render_path() >= 3) {
+    if (render_path() == 0) {
         const size_t ns[1] = {n};
         const size_t bs[1] = {bins};
         return render_rgb_fused(1, &d_spec, &row0, bs, ns, up_ratio, nwidth, nheight, max, min, d_rgb,

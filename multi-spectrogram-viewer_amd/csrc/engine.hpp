@@ -125,7 +125,6 @@ int ranges_read(const int* d_range, size_t n, float* mx, float* mn, int* nan, hi
 // launches (grey, vertical, horizontal + colormap)
 int render_path();
 int set_render_path(int path);
-void render_counts(uint64_t* out);  // thesia_render_counts
 
 // ---- display helpers on device buffers (used by MultiTrack and the C ABI) ----
 int grey_to_rgb_device(const float* d_grey, uint32_t w, uint32_t h, uint32_t nw, uint32_t nh,

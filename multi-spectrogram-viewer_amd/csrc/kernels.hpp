@@ -191,22 +191,6 @@ int launch_render_batch2(const float* spec, uint32_t bins, float max, float min,
                          uint32_t nw_max, uint32_t nh, int h_taps, int h_span, uint32_t v_band,
                          int v_rows, int v_kv, float* tmp, const uint8_t* cmap, uint8_t* rgb,
                          hipStream_t s, bool h_dma = true);  // h_dma: the LDS-DMA horizontal pass
-// The fully fused display (grey + vertical + horizontal Lanczos3 + colormap, the intermediate in
-// LDS only): a block = R output rows x 64 columns of one track; kt register taps (16/32/48) for
-// the horizontal pass, kv padded vertical taps, s_cap / g_cap the largest frame span / grey-row
-// span of a tile in the launch (host-computed). Same bytes as launch_render_batch2.
-int render_fused_lds_bytes(int R, int kv, int s_cap, int g_cap, int kt);
-int launch_render_fused(const float* spec, uint32_t bins, float max, float min, const RenderDesc* d_desc,
-                        uint32_t n, uint32_t nw_max, uint32_t nh, int kt, int R, int kv, int s_cap,
-                        int g_cap, const uint8_t* cmap, uint8_t* rgb, hipStream_t s);
-// The band-streaming display (render path 5): a block = R output rows of one track walking its
-// columns in chunks of CC; the band's vertical sums in an LDS ring of RW (a power of two) frame
-// slots, the grey rows of up to 64 new frames in an LDS tile of GC rows; kv / KH the vertical /
-// horizontal taps padded to multiples of 4. Same bytes as launch_render_batch2.
-int render_stream_lds_bytes(int R, int CC, int RW, int GC, int kv, int KH);
-int launch_render_stream(const float* spec, uint32_t bins, float max, float min, const RenderDesc* d_desc,
-                         uint32_t n, uint32_t nh, int R, int CC, int RW, int GC, int kv, int KH,
-                         const uint8_t* cmap, uint8_t* rgb, hipStream_t s);
 int launch_spec_to_grey(const float* spec, uint32_t T, uint32_t bins, uint32_t H, float max,
                         float min, float* grey, hipStream_t s);
 int launch_resize_v(const float* in, uint32_t w, uint32_t h, uint32_t nh, const int32_t* left,

@@ -237,14 +237,6 @@ def run_batches(batches, stream=None) -> None:
     check(lib.thesia_batches_run(arr, len(batches), stream))
 
 
-def render_counts():
-    """Geometry groups rendered so far per display structure: (two-kernel, single-kernel,
-    band-streaming) -- thesia_render_counts."""
-    out = np.zeros(3, np.uint64)
-    check(lib.thesia_render_counts(out.ctypes.data_as(_u64p)))
-    return tuple(int(v) for v in out)
-
-
 def set_render_path(path: int) -> None:
     """0: batched display launches (default); 1: per-track launches (cross-check)."""
     check(lib.thesia_set_render_path(path))

@@ -103,7 +103,7 @@ def test_c5_mixed_rate_render_pipeline():
         assert r.rgb.tobytes() == img.tobytes(), (t.sr, t.n_fft)  # display path bit-exact
 
 
-@pytest.mark.parametrize("path", [0, 1, 2, 3, 4, 5])  # two-kernel (LDS-DMA horizontal) / per-track / three-stage / single-kernel / register-staged horizontal / band-streaming
+@pytest.mark.parametrize("path", [0, 1, 2])  # two-kernel (LDS-DMA horizontal) / per-track / three-stage
 @pytest.mark.parametrize("px_per_sec", [73.0, 30.0, 9.0, 2.0])  # 30: 17-64 taps; 9, 2: wider spans
 @pytest.mark.parametrize("nheight", [90, 400, 600])  # 400, 600: H -> nheight downsampling ~2.5, taller
 def test_render_batch_ragged_groups(path, px_per_sec, nheight):
@@ -112,13 +112,10 @@ def test_render_batch_ragged_groups(path, px_per_sec, nheight):
     three-stage one) and the per-track launches produce the oracle's bytes for every image
     (ragged T, nwidth and workspace offsets; staged and direct horizontal spans)."""
     engine.set_render_path(path)
-    c0 = engine.render_counts()
     try:
         _ragged(px_per_sec, nheight)
     finally:
         engine.set_render_path(0)
-    if path == 5:  # the band-streaming kernel ran (for the groups whose LDS it fits)
-        assert engine.render_counts()[2] > c0[2]
 
 
 def _ragged(px_per_sec, nheight):
