@@ -266,6 +266,10 @@ int thesia_plan_create(const thesia_plan_desc* desc, thesia_plan** plan) {
     GUARD_END
 }
 int thesia_plan_destroy(thesia_plan* plan) {
+    // a plan's tables may still be read by work the caller enqueued on its own streams; its
+    // buffers return to the stream-ordered pool (DevBuf), so wait for the device first, as the
+    // hipFree this replaced did
+    if (plan) (void)hipDeviceSynchronize();
     delete reinterpret_cast<Plan*>(plan);
     return THESIA_OK;
 }
@@ -286,6 +290,7 @@ int thesia_batch_create(thesia_plan* plan, const thesia_batch_desc* desc, thesia
     GUARD_END
 }
 int thesia_batch_destroy(thesia_batch* batch) {
+    if (batch) (void)hipDeviceSynchronize();  // see thesia_plan_destroy
     delete reinterpret_cast<Batch*>(batch);
     return THESIA_OK;
 }
