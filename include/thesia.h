@@ -188,14 +188,13 @@ int thesia_batch_kernel_info(const thesia_batch* batch, int* lds_bytes, int* til
 
 /* Which fused kernel runs the batch: 1 stft_kernel (general), 2 stft2_kernel (4 waves/SIMD),
  * 3 stft3_kernel (streaming; win = n_fft, hop = n_fft/4), 5 stft5_kernel (streaming, n_fft 2048:
- * untangle pairs co-resident in a lane), 6 stft6_kernel (streaming, n_fft 2048, mel kinds: one
- * 64-lane frame per wave, 3 waves/SIMD), 9 stftx_kernel (the reference's operation order). */
+ * untangle pairs co-resident in a lane), 9 stftx_kernel (the reference's operation order). */
 int thesia_batch_kernel(const thesia_batch* batch, int* kernel);
 
 /* Named alternatives of a batch (none changes what is computed, only how; all results stay
  * within the parity contract). Not part of the reference surface. */
 typedef enum {
-    /* 0 = automatic (streaming kernel where its geometry allows), 1 / 2 / 3 / 5 / 6 / 9 = force
+    /* 0 = automatic (streaming kernel where its geometry allows), 1 / 2 / 3 / 5 / 9 = force
      * that kernel (THESIA_ERR_UNSUPPORTED if it cannot run the geometry) */
     THESIA_BATCH_OPT_KERNEL = 1,
     /* at most this many workgroups per launch (0 = one full occupancy wave of the device);
@@ -216,8 +215,7 @@ typedef enum {
     /* mel projection of stft5_kernel (the mel kinds at n_fft 2048): 0 = automatic, 1 = the
      * filter rounds as one chunk stream, 2 / 3 = the packed stream (filters dealt to lanes by
      * load) with 2 / 3 float4 steps per chunk. Every path is the same k-ascending fma chain
-     * per mel (identical bits). stft6_kernel: 0 automatic, 2 / 3 its 64-lane packed stream with
-     * 2 / 3 steps per chunk (wide filters as two chains, summed). */
+     * per mel (identical bits). */
     THESIA_BATCH_OPT_MEL_PATH = 5
 } thesia_batch_option;
 int thesia_batch_set_option(thesia_batch* batch, int option, int64_t value);

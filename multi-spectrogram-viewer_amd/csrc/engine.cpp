@@ -305,35 +305,31 @@ static int build_mel4(Plan* p) {
     return rc;
 }
 
-// The packed mel stream (kernels.hpp melp_*), S float4 steps per chunk, for stft5's 32 lanes
-// per frame or stft6's 64. Every filter is padded to whole chunks: its first chunk starts at a
-// multiple of 4 bins at or before its band and the weights outside the band are zero, so the
-// lane's k-ascending fma chain adds only +0 terms around the band and each mel is the same chain
-// as mel4's (bit-exact with it). The filters are dealt to the lanes largest first onto the least
-// loaded lane (LPT) and a lane runs its filters back to back: a frame costs the largest lane
-// load in chunks (mel-128 @ 48 kHz / 2048, 32 lanes: 11 chunks of 2 steps, where the rounds pad
-// every lane to the round's widest band and take 32 steps). With 64 lanes the widest filters
-// would set that load, so (L = 64 only) a filter wider than a cap runs as two pieces — bins
-// [lo, mid) and [mid, hi), each its own chain from +0 on its own lane — whose sums the kernel adds
-// at the output (slot A + slot B; the cap with the fewest chunks per frame). Placement: which
-// lane runs which sequence, the order of a lane's pieces and each piece's start within its slack
-// are searched (seeded random restarts + coordinate descent) for the fewest LDS cycles of the
-// |X| reads (a ds_read_b128 is served in build_mel4's 16-lane groups; per group, the lanes of one
-// 16-byte slot mod 16 cost one cycle per distinct address).
+// stft5's packed mel stream (kernels.hpp melp_*), S float4 steps per chunk. Every filter is
+// padded to whole chunks: its first chunk starts at a multiple of 4 bins at or before its band
+// and the weights outside the band are zero, so the lane's k-ascending fma chain adds only +0
+// terms around the band and each mel is the same chain as mel4's (bit-exact with it). The
+// filters are dealt to the 32 lanes largest first onto the least loaded lane (LPT) and a lane
+// runs its filters back to back: a frame costs the largest lane load in chunks (mel-128 @ 48 kHz
+// / 2048: 11 chunks of 2 steps, where the rounds pad every lane to the round's widest band and
+// take 32 steps). Placement: which lane runs which filter sequence, the order of a lane's
+// filters and each filter's start within its slack are searched (seeded random restarts +
+// coordinate descent) for the fewest LDS cycles of the |X| reads (a ds_read_b128 is served in
+// build_mel4's 16-lane groups; per group, the lanes of one 16-byte slot mod 16 cost one cycle
+// per distinct address).
 static const int kLdsG[2][16] = {{0, 1, 2, 3, 12, 13, 14, 15, 20, 21, 22, 23, 24, 25, 26, 27},
                                  {4, 5, 6, 7, 8, 9, 10, 11, 16, 17, 18, 19, 28, 29, 30, 31}};
 
-static int build_melp(Plan* p, int S, int L, Plan::Melp& out) {
+static int build_melp(Plan* p, int S, Plan::Melp& out) {
     out.chunks = 0;
     out.steps = S;
+    constexpr int L = 32;
     const long F = (long)p->NC + 1, F4 = (F + 3) / 4 * 4;
     const int M = (int)p->n_mels;
-    const bool two = L == 64;  // two-piece filters, slot B per mel
-    const int region = two ? kStft6Region : kStft5Region;
-    if ((L != 32 && L != 64) || p->NC != 1024 || F4 != kMelpOut || M <= 0 ||
-        kMelpOut + (two ? 2 : 1) * M + kMelpDummies > region)
-        return THESIA_OK;  // not the streaming geometry / the mel slots do not fit the region
-    std::vector<long> flo(M), fhi(M);
+    if (p->NC != 1024 || F4 != kMelpOut || M <= 0 || kMelpOut + M + kMelpDummies > kStft5Region)
+        return THESIA_OK;  // not stft5's geometry / the mel slots do not fit the region
+    struct Flt { long kmin, kmax; int ch; };
+    std::vector<Flt> fl(M);
     for (int m = 0; m < M; ++m) {
         long lo = -1, hi = -1;
         for (long k = 0; k < F; ++k)
@@ -342,78 +338,34 @@ static int build_melp(Plan* p, int S, int L, Plan::Melp& out) {
                 hi = k + 1;
             }
         if (lo < 0) lo = hi = 0;  // empty filter: one chunk of zero weights (its mel is +0)
-        flo[m] = lo;
-        fhi[m] = hi;
+        const long lo4 = lo / 4 * 4;
+        const int ch = (int)((std::max(1L, (hi - lo4 + 3) / 4) + S - 1) / S);
+        const long span = 4L * S * ch;
+        if (span > F4) return THESIA_OK;
+        fl[m] = Flt{std::max(0L, (hi - span + 3) / 4 * 4), std::min(lo4, F4 - span), ch};
     }
-    auto chunks_of = [&](long lo, long hi) {
-        return (int)((std::max(1L, (hi - lo / 4 * 4 + 3) / 4) + S - 1) / S);
-    };
-    struct Item {
-        int m, slot;    // mel, output slot (m: whole filter or first piece; M + m: second piece)
-        long lo, hi;    // the piece's bins (weights outside are zero)
-        long kmin, kmax;
-        int ch;
-    };
-    int maxch = 1;
-    for (int m = 0; m < M; ++m) maxch = std::max(maxch, chunks_of(flo[m], fhi[m]));
-    std::vector<Item> items;
-    std::vector<std::vector<int>> seq;
-    int C = -1;
-    for (int cap = maxch; cap >= (two ? (maxch + 1) / 2 : maxch); --cap) {
-        std::vector<Item> it;
-        for (int m = 0; m < M; ++m) {
-            const int ch = chunks_of(flo[m], fhi[m]);
-            if (ch <= cap) {
-                it.push_back(Item{m, m, flo[m], fhi[m], 0, 0, ch});
-            } else {
-                const long mid = flo[m] / 4 * 4 + 4L * S * ((ch + 1) / 2);
-                it.push_back(Item{m, m, flo[m], mid, 0, 0, chunks_of(flo[m], mid)});
-                it.push_back(Item{m, M + m, mid, fhi[m], 0, 0, chunks_of(mid, fhi[m])});
-            }
-        }
-        bool fits = true;
-        for (auto& x : it) {
-            const long span = 4L * S * x.ch;
-            if (span > F4) fits = false;
-            x.kmin = std::max(0L, (x.hi - span + 3) / 4 * 4);
-            x.kmax = std::min(x.lo / 4 * 4, F4 - span);
-        }
-        if (!fits) continue;
-        std::vector<int> order(it.size());
-        for (size_t i = 0; i < it.size(); ++i) order[i] = (int)i;
-        std::stable_sort(order.begin(), order.end(), [&](int a, int b) { return it[a].ch > it[b].ch; });
-        std::vector<std::vector<int>> sq(L);
-        std::vector<int> load(L, 0);
-        for (int f : order) {
-            const int j = (int)(std::min_element(load.begin(), load.end()) - load.begin());
-            sq[j].push_back(f);
-            load[j] += it[f].ch;
-        }
-        const int cc = *std::max_element(load.begin(), load.end());
-        if (C < 0 || cc < C) {
-            C = cc;
-            items = it;
-            seq = sq;
-        }
+    std::vector<int> order(M);
+    for (int m = 0; m < M; ++m) order[m] = m;
+    std::stable_sort(order.begin(), order.end(), [&](int a, int b) { return fl[a].ch > fl[b].ch; });
+    std::vector<std::vector<int>> seq(L);
+    std::vector<int> load(L, 0);
+    for (int f : order) {
+        const int j = (int)(std::min_element(load.begin(), load.end()) - load.begin());
+        seq[j].push_back(f);
+        load[j] += fl[f].ch;
     }
-    if (C < 0 || C > 64) return THESIA_OK;
-    const int NI = (int)items.size();
+    const int C = *std::max_element(load.begin(), load.end());
+    if (C > 64) return THESIA_OK;
 
-    const int NG = L / 16;  // 16-lane groups of a ds_read_b128
-    std::vector<std::vector<int>> groups(NG);
-    std::vector<int> grp(L);
-    for (int g = 0; g < NG; ++g)
-        for (int i = 0; i < 16; ++i) {
-            const int j = kLdsG[g & 1][i] + 32 * (g >> 1);
-            groups[g].push_back(j);
-            grp[j] = g;
-        }
+    int grp[L];
+    for (int g = 0; g < 2; ++g)
+        for (int i = 0; i < 16; ++i) grp[kLdsG[g][i]] = g;
     std::vector<long> offs((size_t)L * C);  // |X| float offset per (lane, chunk); -1 = idle
     auto cell = [&](int c, int g) {
         long seen[16][16];
         int cnt[16] = {0}, worst = 0;
         for (int i = 0; i < 16; ++i) {
-            const long o = offs[(size_t)groups[g][i] * C + c];
+            const long o = offs[(size_t)kLdsG[g][i] * C + c];
             if (o < 0) continue;
             const int s = (int)((o / 4) & 15);
             bool dup = false;
@@ -423,8 +375,8 @@ static int build_melp(Plan* p, int S, int L, Plan::Melp& out) {
         }
         return worst;
     };
-    std::vector<int> lane_of(NI), c0_of(NI), best_lane, best_c0;
-    std::vector<long> k0(NI), best_k0;
+    std::vector<int> lane_of(M), c0_of(M), best_lane, best_c0;
+    std::vector<long> k0(M), best_k0;
     long best = -1;
     uint64_t rs = 0x9E3779B97F4A7C15ull;  // fixed seed: the plan's tables are deterministic
     auto rnd = [&](uint64_t n) {
@@ -446,28 +398,27 @@ static int build_melp(Plan* p, int S, int L, Plan::Melp& out) {
             for (int f : sq[s]) {
                 lane_of[f] = perm[s];
                 c0_of[f] = c;
-                k0[f] = items[f].kmax;
-                for (int i = 0; i < items[f].ch; ++i) offs[(size_t)perm[s] * C + c + i] = k0[f] + 4L * S * i;
-                c += items[f].ch;
+                k0[f] = fl[f].kmax;
+                for (int i = 0; i < fl[f].ch; ++i) offs[(size_t)perm[s] * C + c + i] = k0[f] + 4L * S * i;
+                c += fl[f].ch;
             }
         }
         for (int pass = 0; pass < 2; ++pass)
-            for (int f = 0; f < NI; ++f) {
+            for (int f = 0; f < M; ++f) {
                 const int j = lane_of[f], g = grp[j];
                 long bk = k0[f];
                 int bc = 1 << 30;
-                for (long k = items[f].kmax; k >= items[f].kmin; k -= 4) {
-                    for (int i = 0; i < items[f].ch; ++i) offs[(size_t)j * C + c0_of[f] + i] = k + 4L * S * i;
+                for (long k = fl[f].kmax; k >= fl[f].kmin; k -= 4) {
+                    for (int i = 0; i < fl[f].ch; ++i) offs[(size_t)j * C + c0_of[f] + i] = k + 4L * S * i;
                     int cost = 0;
-                    for (int i = 0; i < items[f].ch; ++i) cost += cell(c0_of[f] + i, g);
+                    for (int i = 0; i < fl[f].ch; ++i) cost += cell(c0_of[f] + i, g);
                     if (cost < bc) { bc = cost; bk = k; }
                 }
                 k0[f] = bk;
-                for (int i = 0; i < items[f].ch; ++i) offs[(size_t)j * C + c0_of[f] + i] = bk + 4L * S * i;
+                for (int i = 0; i < fl[f].ch; ++i) offs[(size_t)j * C + c0_of[f] + i] = bk + 4L * S * i;
             }
         long total = 0;
-        for (int c = 0; c < C; ++c)
-            for (int g = 0; g < NG; ++g) total += cell(c, g);
+        for (int c = 0; c < C; ++c) total += cell(c, 0) + cell(c, 1);
         if (best < 0 || total < best) {
             best = total;
             best_lane = lane_of;
@@ -477,40 +428,35 @@ static int build_melp(Plan* p, int S, int L, Plan::Melp& out) {
     }
     // tables: meta rows r = 0 .. C + 1 ({woff(r-1), keep(r-1), xoff(r), 0}); weight rows of
     // chunks 0 .. C (chunk C: the pipeline's read-ahead padding, zero weights)
-    const int dummy0 = kMelpOut + (two ? 2 : 1) * M;
     std::fill(offs.begin(), offs.end(), -1L);
     std::vector<int> woff((size_t)(C + 1) * L), keep((size_t)(C + 1) * L, -1);
     for (int j = 0; j < L; ++j)
-        for (int c = 0; c <= C; ++c) woff[(size_t)c * L + j] = (dummy0 + (j & (kMelpDummies - 1))) * 4;
+        for (int c = 0; c <= C; ++c) woff[(size_t)c * L + j] = (kMelpOut + M + (j & (kMelpDummies - 1))) * 4;
     std::vector<float> wt((size_t)(C + 1) * S * L * 4, 0.0f);
-    std::vector<int> bo(std::max(M, 1), (int)F);  // slot B per mel; region[F] = +0
-    for (int f = 0; f < NI; ++f) {
-        const Item& x = items[f];
+    for (int f = 0; f < M; ++f) {
         const int j = best_lane[f];
-        for (int i = 0; i < x.ch; ++i) {
+        for (int i = 0; i < fl[f].ch; ++i) {
             const int c = best_c0[f] + i;
             offs[(size_t)j * C + c] = best_k0[f] + 4L * S * i;
             for (int u = 0; u < S; ++u)
                 for (int e = 0; e < 4; ++e) {
                     const long k = best_k0[f] + 4L * (S * i + u) + e;
-                    wt[(((size_t)c * S + u) * L + j) * 4 + e] =
-                        k >= x.lo && k < x.hi && k < F ? p->mel_fb[(size_t)k * M + x.m] : 0.0f;
+                    wt[(((size_t)c * S + u) * L + j) * 4 + e] = k < F ? p->mel_fb[(size_t)k * M + f] : 0.0f;
                 }
         }
-        const int cl = best_c0[f] + x.ch - 1;
-        woff[(size_t)cl * L + j] = (kMelpOut + x.slot) * 4;
+        const int cl = best_c0[f] + fl[f].ch - 1;
+        woff[(size_t)cl * L + j] = (kMelpOut + f) * 4;
         keep[(size_t)cl * L + j] = 0;
-        if (x.slot >= M) bo[x.m] = kMelpOut + x.slot;
     }
     // idle chunks read an address another lane of their group reads (a broadcast: no cycle)
     std::vector<int> xoff((size_t)(C + 1) * L, 0);
     for (int c = 0; c < C; ++c)
-        for (int g = 0; g < NG; ++g) {
+        for (int g = 0; g < 2; ++g) {
             long any = 0;
             for (int i = 0; i < 16; ++i)
-                if (offs[(size_t)groups[g][i] * C + c] >= 0) { any = offs[(size_t)groups[g][i] * C + c]; break; }
+                if (offs[(size_t)kLdsG[g][i] * C + c] >= 0) { any = offs[(size_t)kLdsG[g][i] * C + c]; break; }
             for (int i = 0; i < 16; ++i) {
-                const int j = groups[g][i];
+                const int j = kLdsG[g][i];
                 const long o = offs[(size_t)j * C + c];
                 xoff[(size_t)c * L + j] = (int)((o >= 0 ? o : any) * 4);
             }
@@ -524,7 +470,6 @@ static int build_melp(Plan* p, int S, int L, Plan::Melp& out) {
         }
     int rc = out.meta.upload(meta.data(), meta.size() * sizeof(int4));
     if (!rc) rc = out.wt.upload(wt.data(), wt.size() * sizeof(float));
-    if (!rc && two) rc = out.bo.upload(bo.data(), bo.size() * sizeof(int));
     if (!rc) out.chunks = C;
     return rc;
 }
@@ -610,16 +555,6 @@ int plan_create(const thesia_plan_desc& d, Plan** out) {
         }
         if (tw3.empty()) tw3.assign(2, 0.0f);
     }
-    // stft6's twiddles: [64][16] W_NC^{j k1}, then [4][16] W_64^{b c} = W_NC^{16 b c} (NC 1024)
-    std::vector<float> tw6(2, 0.0f);
-    if (p->NC == 1024) {
-        tw6.assign(2 * (64 * 16 + 4 * 16), 0.0f);
-        for (size_t i = 0; i < 64 * 16 + 4 * 16; ++i) {
-            const size_t e = i < 64 * 16 ? ((i / 16) * (i % 16)) % p->NC : (16 * ((i - 1024) / 16) * (i % 16)) % p->NC;
-            tw6[2 * i] = tw[2 * e];
-            tw6[2 * i + 1] = tw[2 * e + 1];
-        }
-    }
     std::vector<float> sc = rfft_sin_cos(d.n_fft);
     const bool power = d.output == THESIA_OUT_POWER || d.output == THESIA_OUT_POWER_DB;
     p->log_amin = power ? log10f(1e-36f) : log10f(1e-18f);  // decibel.rs:7-8, :43
@@ -627,7 +562,6 @@ int plan_create(const thesia_plan_desc& d, Plan** out) {
     if (!rc) rc = p->tw.upload(tw.data(), tw.size() * sizeof(float));
     if (!rc) rc = p->tw2.upload(tw2.data(), tw2.size() * sizeof(float));
     if (!rc) rc = p->tw3.upload(tw3.data(), tw3.size() * sizeof(float));
-    if (!rc) rc = p->tw6.upload(tw6.data(), tw6.size() * sizeof(float));
     if (!rc) rc = p->sincos.upload(sc.data(), sc.size() * sizeof(float));
     // the reference-order kernel: rustfft prepare_radix4 positions (oracle cfft_tab) and the
     // base butterfly_8 twiddles
@@ -661,19 +595,14 @@ int plan_create(const thesia_plan_desc& d, Plan** out) {
         }
         if (!rc) rc = build_mel(p);
         if (!rc) rc = build_mel4(p);
-        for (int i = 0; i < 2 && !rc; ++i) rc = build_melp(p, 2 + i, 32, p->melp[i]);
-        for (int i = 0; i < 2 && !rc; ++i) rc = build_melp(p, 2 + i, 64, p->melp6[i]);
+        for (int i = 0; i < 2 && !rc; ++i) rc = build_melp(p, 2 + i, p->melp[i]);
         if (!rc) {  // default: the fewest estimated instructions per chunk stream (5 + 6 S each)
-            for (int v = 0; v < 2; ++v) {
-                Plan::Melp* mp = v == 0 ? p->melp : p->melp6;
-                int& best = v == 0 ? p->melp_best : p->melp6_best;
-                long bc = -1;
-                for (int i = 0; i < 2; ++i)
-                    if (mp[i].chunks > 0) {
-                        const long c = (long)mp[i].chunks * (5 + 6 * mp[i].steps);
-                        if (bc < 0 || c < bc) { bc = c; best = i; }
-                    }
-            }
+            long bc = -1;
+            for (int i = 0; i < 2; ++i)
+                if (p->melp[i].chunks > 0) {
+                    const long c = (long)p->melp[i].chunks * (5 + 6 * p->melp[i].steps);
+                    if (bc < 0 || c < bc) { bc = c; p->melp_best = i; }
+                }
         }
         if (!rc) {  // the reference-order kernel: each mel's nonzero band, weights flat
             const size_t M = p->n_mels;
@@ -804,9 +733,6 @@ int batch_create(Plan* plan, const thesia_batch_desc& d, Batch** out) {
         b->apply_mel_path();
     }
     b->k5_ok = k5_geo && stft5_lds_bytes(L) <= 163840;
-    b->k6_ok = b->k3_ok && stft6_supports((int)plan->n_fft, (int)plan->win, (int)plan->hop, d.input_format,
-                                          (int)d.channels, plan->out_kind) &&
-               plan->melp6_best >= 0 && stft6_lds_bytes(b->launch6()) <= 163840;
     b->kernel = b->auto_kernel();
     if (hipEventCreate(&b->ev0) != hipSuccess || hipEventCreate(&b->ev1) != hipSuccess) {
         delete b;
@@ -814,24 +740,6 @@ int batch_create(Plan* plan, const thesia_batch_desc& d, Batch** out) {
     }
     *out = b;
     return THESIA_OK;
-}
-
-StftLaunch Batch::launch6() const {
-    StftLaunch L = launch;
-    const int idx = mel_path >= 2 ? mel_path - 2 : plan->melp6_best;
-    L.tw6 = plan->tw6.as<float2>();
-    if (idx < 0 || plan->melp6[idx].chunks == 0) {
-        L.melp_chunks = 0;
-        return L;
-    }
-    const Plan::Melp& m = plan->melp6[idx];
-    L.melp_chunks = m.chunks;
-    L.melp_steps = m.steps;
-    L.melp_meta = m.meta.as<int4>();
-    L.melp_wt = m.wt.as<float4>();
-    L.melp_bo = m.bo.as<int>();
-    L.melp_v4 = plan->n_mels % 4 == 0 && plan->n_mels <= 128 && (reinterpret_cast<uintptr_t>(L.out) & 15) == 0;
-    return L;
 }
 
 void Batch::apply_mel_path() {
@@ -858,7 +766,6 @@ int batch_set_option(Batch* b, int option, int64_t value) {
             else if (value == 2 && stft2_supports((int)b->plan->n_fft)) b->kernel = 2;
             else if (value == 3 && b->k3_ok) b->kernel = 3;
             else if (value == 5 && b->k5_ok) b->kernel = 5;
-            else if (value == 6 && b->k6_ok && b->mel_path != 1) b->kernel = 6;
             else if (value == 9 && stftx_lds_bytes((int)b->plan->n_fft) <= 163840) b->kernel = 9;
             else return set_error(THESIA_ERR_UNSUPPORTED, "kernel " + std::to_string(value) +
                                                              " does not run this batch's geometry");
@@ -881,19 +788,6 @@ int batch_set_option(Batch* b, int option, int64_t value) {
             return THESIA_OK;
         case THESIA_BATCH_OPT_MEL_PATH: {
             if (value < 0 || value > 3) return set_error(THESIA_ERR_INVALID_ARG, "mel_path must be 0..3");
-            if (b->kernel == 6) {  // stft6: its own 64-lane packed streams only
-                const int idx = value >= 2 ? (int)value - 2 : b->plan->melp6_best;
-                if (value == 1 || idx < 0 || b->plan->melp6[idx].chunks == 0)
-                    return set_error(THESIA_ERR_UNSUPPORTED, "no packed mel stream of stft6 for this path");
-                const int prev = b->mel_path;
-                b->mel_path = (int)value;
-                if (stft6_lds_bytes(b->launch6()) > 163840) {
-                    b->mel_path = prev;
-                    return set_error(THESIA_ERR_UNSUPPORTED, "the mel tables of that path do not fit LDS");
-                }
-                b->apply_mel_path();
-                return THESIA_OK;
-            }
             if (value >= 2 && b->plan->melp[value - 2].chunks == 0)
                 return set_error(THESIA_ERR_UNSUPPORTED, "no packed mel stream for this plan");
             const int prev = b->mel_path;
@@ -930,8 +824,7 @@ int batch_run(Batch* b, hipStream_t s) {
         rc = launch_stftx(b->launch, s);
         if (rc) return set_error(rc == -2 ? THESIA_ERR_UNSUPPORTED : THESIA_ERR_DEVICE, "stftx launch failed");
     } else {
-        if (b->kernel == 6) rc = launch_stft6(b->launch6(), s);
-        if (b->kernel == 5 || (rc == -2 && b->kernel == 6 && b->k5_ok)) rc = launch_stft5(b->launch, s);
+        if (b->kernel == 5) rc = launch_stft5(b->launch, s);
         if (rc == -2 && b->kernel >= 3) {
             const bool fold = b->range && lin && b->launch.row_alt == 0;
             b->launch.trk_range = fold ? b->range : nullptr;

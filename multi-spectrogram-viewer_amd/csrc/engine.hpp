@@ -83,17 +83,13 @@ struct Plan {
     float xw8[4] = {0.f, 0.f, 0.f, 0.f};
     int mel_chunks = 0;
     size_t mel4_wt_rows = 0;
-    // stft5's packed mel stream (32 lanes per frame), built for 2 and 3 float4 steps per chunk
-    // (build_melp); melp6: the same for stft6's 64 lanes, wide filters in two pieces (bo: the
-    // second piece's slot per mel)
+    // stft5's packed mel stream, built for 2 and 3 float4 steps per chunk (build_melp)
     struct Melp {
-        DevBuf meta, wt, bo;
+        DevBuf meta, wt;
         int chunks = 0;  // 0: not available for this filterbank
         int steps = 0;
-    } melp[2], melp6[2];
+    } melp[2];
     int melp_best = -1;  // index into melp of the default (fewest estimated instructions), -1 none
-    int melp6_best = -1;
-    DevBuf tw6;  // stft6's twiddle tables (kernels.hpp StftLaunch::tw6), n_fft 2048 only
     bool use_v2 = false;  // stft2_kernel runs this plan (n_fft 256..2048)
     size_t row_bins() const;
     size_t out_elem_bytes() const { return out_kind == OUT_COMPLEX ? 8 : 4; }
@@ -108,14 +104,11 @@ struct Batch {
     DevBuf d_in_off, d_len, d_frame0;
     uint64_t total_frames = 0;
     StftLaunch launch{};
-    // 1 stft_kernel, 2 stft2_kernel, 3 stft3_kernel, 5 stft5_kernel, 6 stft6_kernel (streaming),
-    // 9 stftx_kernel (reference operation order)
+    // 1 stft_kernel, 2 stft2_kernel, 3 stft3_kernel, 5 stft5_kernel (streaming), 9 stftx_kernel
+    // (reference operation order)
     int kernel = 1;
     bool k3_ok = false;  // the streaming kernel supports this batch's geometry
     bool k5_ok = false;  // ... and so does its n_fft 2048 variant (stft5_kernel)
-    bool k6_ok = false;  // ... and the one-frame-per-wave variant (stft6_kernel, mel kinds)
-    // the launch descriptor with stft6's mel tables (packed for 64 lanes) in place of stft5's
-    StftLaunch launch6() const;
     // automatic choice: stft5 for the mel kinds at n_fft 2048 and for linear rows without the
     // range option (measured faster there: stereo power dB 5.64 vs 6.22 ms in round 3; slower for
     // complex rows, 9.0 vs 6.98 ms, and stft3 folds the per-track range into its row epilogue;

@@ -82,12 +82,6 @@ struct StftLaunch {
     int melp_v4 = 0;  // n_mels % 4 == 0 and 16-byte aligned rows: float4 row stores
     const int4* melp_meta = nullptr;
     const float4* melp_wt = nullptr;
-    // stft6 (64 lanes per frame): filters wider than the plan's cap run as two pieces whose
-    // sums land in slots A (kMelpOut + m) and B; melp_bo[m] = B's float offset in the region
-    // (region[F] = +0 for the unsplit mels)
-    const int* melp_bo = nullptr;
-    // stft6 twiddles: [64][16] W_1024^{j k1}, then [4][16] W_64^{b c} (f64-rounded)
-    const float2* tw6 = nullptr;
     // output
     void* out = nullptr;  // packed rows: frame g at out + g * row_elems
     // scheduling / named alternatives (thesia_batch_set_option)
@@ -114,7 +108,6 @@ struct StftLaunch {
 // stft5 stream region (floats) and where the packed mel stream stages a frame's mels in it:
 // behind the |X| row of F4 = 1028 floats; dummy slots follow the n_mels slots
 constexpr int kStft5Region = 1184, kMelpOut = 1028, kMelpDummies = 16;
-constexpr int kStft6Region = 2244;  // stft6's region per wave (17 transpose rows of 132 floats)
 
 // f32 <-> int32 with the order of the floats (max / min by integer atomics); NaN excluded
 __host__ __device__ inline int range_ord(float x) {
@@ -154,11 +147,6 @@ int launch_irfftx(const float* in, uint64_t n_frames, int length, const int* xpo
 int launch_stft5(const StftLaunch& a, hipStream_t stream);
 bool stft5_supports(int n_fft, int win, int hop, int in_format, int channels);
 int stft5_lds_bytes(const StftLaunch& a);
-// stft6_kernel (streaming, n_fft 2048, mel kinds: one 64-lane frame per wave, 3 waves/SIMD;
-// stft6_kernels.hip): -2 when the geometry / kind is not its own or its tables are missing
-int launch_stft6(const StftLaunch& a, hipStream_t stream);
-bool stft6_supports(int n_fft, int win, int hop, int in_format, int channels, int out_kind);
-int stft6_lds_bytes(const StftLaunch& a);
 // LDS bytes / frames per block pass / lanes per frame of the kernel for n_fft.
 int stft_kernel_info(int n_fft, int* lds_bytes, int* tile_frames, int* lanes_per_frame);
 
