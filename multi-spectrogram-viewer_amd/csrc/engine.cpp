@@ -766,7 +766,7 @@ int batch_set_option(Batch* b, int option, int64_t value) {
             else if (value == 2 && stft2_supports((int)b->plan->n_fft)) b->kernel = 2;
             else if (value == 3 && b->k3_ok) b->kernel = 3;
             else if (value == 5 && b->k5_ok) b->kernel = 5;
-            else if (value == 9 && stftx_lds_bytes((int)b->plan->n_fft) <= 163840) b->kernel = 9;
+            else if (value == 9 && stftx_lds_bytes((int)b->plan->n_fft, true) <= 163840) b->kernel = 9;
             else return set_error(THESIA_ERR_UNSUPPORTED, "kernel " + std::to_string(value) +
                                                              " does not run this batch's geometry");
             b->kernel_forced = value != 0;

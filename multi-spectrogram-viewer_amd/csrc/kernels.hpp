@@ -137,7 +137,7 @@ bool stft3_supports(int n_fft, int win, int hop, int in_format, int channels);
 int stft3_lds_bytes(const StftLaunch& a);  // dynamic LDS of the launch (> 163840: cannot run)
 // stftx_kernel (every n_fft: the reference's operation order, bit-exact with the oracle)
 int launch_stftx(const StftLaunch& a, hipStream_t stream);
-int stftx_lds_bytes(int n_fft);
+int stftx_lds_bytes(int n_fft, bool mel);
 // InvRealFFT (realfft.rs:167-241) in the reference's operation order: n_frames spectra of
 // length/2+1 complex (re, im interleaved) -> n_frames rows of `length` reals; tables of the
 // length's Plan (xpos, forward twiddles, sin_cos, base butterfly_8 twiddles)

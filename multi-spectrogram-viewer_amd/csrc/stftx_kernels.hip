@@ -79,6 +79,7 @@ stftx_kernel(StftLaunch a) {
     extern __shared__ __attribute__((aligned(16))) float xs[];
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     Cx* buf = reinterpret_cast<Cx*>(xs) + (size_t)wave * bufl;
+    // the |X| row (mel kinds only: the other kinds' launches carry no room for it)
     float* mag = xs + (size_t)kXWaves * bufl * 2 + (size_t)wave * ((F + 3) & ~3);
     const uint64_t g = (uint64_t)blockIdx.x * kXWaves + wave;
     if (g >= a.total_frames) return;  // wave-uniform; no block barrier below
@@ -312,15 +313,17 @@ int launch_irfftx(const float* in, uint64_t n_frames, int length, const int* xpo
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
-int stftx_lds_bytes(int n_fft) {
+int stftx_lds_bytes(int n_fft, bool mel) {
     const int NC = n_fft / 2, F = NC + 1;
     const int bufl = (NC + 1 + 3) & ~3;
-    return kXWaves * (bufl * 8 + ((F + 3) & ~3) * 4);
+    return kXWaves * (bufl * 8 + (mel ? ((F + 3) & ~3) * 4 : 0));
 }
 
 int launch_stftx(const StftLaunch& a, hipStream_t s) {
     if (a.n_fft < 2 || (a.n_fft & (a.n_fft - 1))) return -2;
-    const int lds = stftx_lds_bytes(a.n_fft);
+    // the |X| row only for the mel kinds: without it a frame's wave takes 8 KiB at n_fft 2048
+    // (16 waves per CU instead of 12)
+    const int lds = stftx_lds_bytes(a.n_fft, a.out_kind == OUT_MEL || a.out_kind == OUT_MEL_AMP_DB);
     if (lds > 163840) return -2;
     auto kern = a.in_format == IN_S16 ? stftx_kernel<IN_S16> : stftx_kernel<IN_F32>;
     if (hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
