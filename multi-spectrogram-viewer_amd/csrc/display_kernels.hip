@@ -903,6 +903,165 @@ __global__ void __launch_bounds__(256) grey_vert_kernel(const float* spec, uint3
     }
 }
 
+// K4+K5v, wide: grey_vert_kernel with FPL consecutive frames per lane (a block owns 64 * FPL
+// frames x `band` output rows). A tap reads the lane's FPL grey values of one tile row with one
+// ds_read_b64 / ds_read_b128 (256 B/clk, against 128 for the narrow kernel's ds_read_b32) and an
+// output row leaves as one FPL * 4-byte store per lane: 512 B / 1 KiB contiguous per wave
+// instead of 256 B. Same staging, zero-padded weights and per-element summation order as
+// grey_vert_kernel (identical bytes). Lanes whose frames start past T store nothing; frames past
+// T inside a stored vector land in the row padding [T, ts) as finite values (their tile columns
+// are grey(+0)), which the horizontal pass only ever multiplies by zero weights.
+template <int FPL>
+struct FVec;
+template <>
+struct FVec<2> {
+    using T = float2;
+};
+template <>
+struct FVec<4> {
+    using T = float4;
+};
+template <int FPL>
+__device__ __forceinline__ float& fv(typename FVec<FPL>::T& v, int c) {
+    return reinterpret_cast<float*>(&v)[c];
+}
+template <int FPL>
+__global__ void __launch_bounds__(256) grey_vert_wide_kernel(const float* spec, uint32_t bins, float max,
+                                                             float min, uint32_t nh, const RenderDesc* d,
+                                                             float* tmp, int tile_cap, int kv, uint32_t band) {
+    using VT = typename FVec<FPL>::T;
+    constexpr int FW = 64 * FPL;  // frames per block
+    constexpr int TS = FW + 4;    // tile row stride (16-byte aligned rows)
+    extern __shared__ __attribute__((aligned(16))) float vsm[];
+    const RenderDesc r = d[blockIdx.z];
+    const uint32_t x0 = blockIdx.x * FW, ob = blockIdx.y * band;
+    const uint32_t oy1 = ob + band < nh ? ob + band : nh;
+    const uint32_t oy0 = ob > r.oz ? ob : r.oz;  // rows below oz: +0, never formed (RenderDesc)
+    if (x0 >= r.T || oy0 >= oy1) return;         // block-uniform
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int32_t ya = r.vl[oy0];
+    const int32_t rows = r.vl[oy1 - 1] - ya + kv;  // <= tile_cap (host)
+    const uint32_t nb = oy1 - oy0;
+    const int mrows = ((int)band + 3) & ~3;
+    int* meta = reinterpret_cast<int*>(vsm);
+    float* tile = vsm + mrows;                      // [tile_cap][TS]
+    float* wl = tile + tile_cap * TS;               // [band][kv], zero-padded per row
+    const int32_t H = (int32_t)r.H, top = (int32_t)r.H - (int32_t)bins;
+    const float* sp = spec + r.spec_off;
+    {
+        // (frame, row) pairs in quads of frames: element e = (quad q, row k, frame 4q + c), c
+        // fastest. A wave reads 16 consecutive bins of 4 frames (4 x 64 B) and its LDS stores
+        // k * TS + 4q + c (TS = 4 mod 32) fall on 32 distinct banks; THESIA_VDEPTH loads in
+        // flight per thread. The zero fill above the track's band, rows past the image and
+        // frames past T are never loaded.
+        constexpr int D = THESIA_VDEPTH;
+        const int total = FW * rows;
+        const uint32_t r4 = 4u * (uint32_t)rows;
+        const uint32_t mrec = (uint32_t)((0x100000000ull + r4 - 1) / r4);
+        auto split = [&](uint32_t e, uint32_t& f, int32_t& k) {
+            const uint32_t q = __umulhi(e, mrec), rem = e - q * r4;
+            k = (int32_t)(rem >> 2);
+            f = 4 * q + (rem & 3);
+        };
+        for (int e0 = 0; e0 < total; e0 += 256 * D) {
+            float v[D];
+#pragma unroll
+            for (int i = 0; i < D; ++i) {
+                const uint32_t e = (uint32_t)(e0 + 256 * i + tid);
+                uint32_t f;
+                int32_t k;
+                split(e, f, k);
+                const int32_t y = ya + k;
+                v[i] = 0.0f;
+                if ((int)e < total && y >= top && y < H && x0 + f < r.T)
+                    v[i] = sp[(uint64_t)(x0 + f) * bins + (uint32_t)(H - 1 - y)];
+            }
+#pragma unroll
+            for (int i = 0; i < D; ++i) {
+                const uint32_t e = (uint32_t)(e0 + 256 * i + tid);
+                uint32_t f;
+                int32_t k;
+                split(e, f, k);
+                const int32_t y = ya + k;
+                if ((int)e < total) tile[k * TS + f] = (y >= top && y < H) ? grey_of(v[i], max, min) : 0.0f;
+            }
+        }
+        for (uint32_t e = tid; e < nb * (uint32_t)kv; e += 256) {
+            const uint32_t j = e / (uint32_t)kv, i = e - j * (uint32_t)kv;
+            const int32_t n = r.vc[oy0 + j];
+            wl[e] = (int32_t)i < n ? r.vw[r.vo[oy0 + j] + i] : 0.0f;
+        }
+        for (uint32_t j = tid; j < nb; j += 256) meta[j] = r.vl[oy0 + j] - ya;
+    }
+    __syncthreads();
+    const uint32_t xl = x0 + (uint32_t)(FPL * lane);
+    const bool st = xl < r.T;  // (no block barrier below)
+    float* out = tmp + r.tmp_off + xl;
+    const float4* wl4 = reinterpret_cast<const float4*>(wl);
+    const int kv4 = kv >> 2;
+    const float* col = tile + FPL * lane;
+    auto tap = [&](VT& t, const float* c, float w) {
+        const VT g = *reinterpret_cast<const VT*>(c);
+        const float* gp = reinterpret_cast<const float*>(&g);
+#pragma unroll
+        for (int u = 0; u < FPL; ++u) fv<FPL>(t, u) += gp[u] * w;
+    };
+    uint32_t oy = oy0 + wave;
+    // four output rows per wave step (four independent chains per frame, each in its own order)
+    for (; oy + 12 < oy1; oy += 16) {
+        int lq[4];
+        const float4* wq[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const uint32_t j = oy - oy0 + 4 * q;
+            lq[q] = __builtin_amdgcn_readfirstlane(meta[j]);
+            wq[q] = wl4 + j * kv4;
+        }
+        VT t[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+#pragma unroll
+            for (int u = 0; u < FPL; ++u) fv<FPL>(t[q], u) = 0.0f;
+        for (int i4 = 0; i4 < kv4; ++i4) {
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const float4 w = wq[q][i4];
+                const float* c = col + (lq[q] + 4 * i4) * TS;
+                tap(t[q], c, w.x);
+                tap(t[q], c + TS, w.y);
+                tap(t[q], c + 2 * TS, w.z);
+                tap(t[q], c + 3 * TS, w.w);
+            }
+        }
+        if (st) {
+#pragma unroll
+            for (int q = 0; q < 4; ++q) *reinterpret_cast<VT*>(out + (uint64_t)(oy + 4 * q) * r.ts) = t[q];
+        }
+    }
+    for (; oy < oy1; oy += 4) {
+        const uint32_t j = oy - oy0;
+        const int l = __builtin_amdgcn_readfirstlane(meta[j]);
+        const float4* w4 = wl4 + j * kv4;
+        VT t;
+#pragma unroll
+        for (int u = 0; u < FPL; ++u) fv<FPL>(t, u) = 0.0f;
+        for (int i4 = 0; i4 < kv4; ++i4) {
+            const float4 w = w4[i4];
+            const float* c = col + (l + 4 * i4) * TS;
+            tap(t, c, w.x);
+            tap(t, c + TS, w.y);
+            tap(t, c + 2 * TS, w.z);
+            tap(t, c + 3 * TS, w.w);
+        }
+        if (st) *reinterpret_cast<VT*>(out + (uint64_t)oy * r.ts) = t;
+    }
+}
+
+int grey_vert_wide_lds_bytes(int fpl, uint32_t band, int tile_cap, int kv) {
+    return ((((int)band + 3) & ~3) + tile_cap * (64 * fpl + 4) + (int)band * kv) * 4;
+}
+
 // The horizontal pass with its row spans staged by LDS-DMA (global_load_lds_dwordx4, no VGPRs):
 // NB row buffers per block, NB - 1 rows in flight while a row is summed, one barrier per row.
 // A block owns 256 output columns of one image (thread = column, <= KT zero-padded register
@@ -1026,22 +1185,35 @@ int launch_render_batch2(const float* spec, uint32_t bins, float max, float min,
                          const RenderDesc* d_desc, uint32_t n, uint32_t T_max, uint32_t H_max,
                          uint32_t nw_max, uint32_t nh, int h_taps, int h_span, uint32_t v_band,
                          int v_rows, int v_kv, float* tmp, const uint8_t* cmap, uint8_t* rgb,
-                         hipStream_t s, bool h_dma) {
+                         hipStream_t s, bool h_dma, int v_fpl) {
     if (n == 0 || nh == 0 || v_band == 0) return 0;
     if (n > 65535) return -2;
     (void)H_max;
-    // K4+K5v: the band's grey tile, meta and zero-padded weights in LDS (a band whose tile does
-    // not fit reads HBM directly)
     const int kv = (v_kv + 3) & ~3;
-    const int tile_cap = v_rows < 256 ? v_rows : 256;
-    const int lds1 = ((((int)v_band + 3) & ~3) + ((tile_cap * 65 + 3) & ~3) + (int)v_band * kv) * 4;
-    if (lds1 > 163840) return -2;
-    if (hipFuncSetAttribute(reinterpret_cast<const void*>(grey_vert_kernel),
-                            hipFuncAttributeMaxDynamicSharedMemorySize, lds1) != hipSuccess)
-        return -1;
-    dim3 g1((T_max + 63) / 64, (nh + v_band - 1) / v_band, n);
-    hipLaunchKernelGGL(grey_vert_kernel, g1, dim3(256), lds1, s, spec, bins, max, min, nh, d_desc, tmp,
-                       tile_cap, kv, v_band);
+    if (v_fpl == 4) {
+        // K4+K5v wide: every band's grey rows fit the tile (host: v_rows <= the FPL's cap)
+        const int lds1 = grey_vert_wide_lds_bytes(v_fpl, v_band, v_rows, kv);
+        if (lds1 > 163840) return -2;
+        const void* kern = reinterpret_cast<const void*>(grey_vert_wide_kernel<4>);
+        if (hipFuncSetAttribute(kern, hipFuncAttributeMaxDynamicSharedMemorySize, lds1) != hipSuccess) return -1;
+        const uint32_t fw = 64u * (uint32_t)v_fpl;
+        dim3 g1((T_max + fw - 1) / fw, (nh + v_band - 1) / v_band, n);
+        int tile_cap = v_rows;
+        void* args[] = {&spec, &bins, &max, &min, &nh, &d_desc, &tmp, &tile_cap, const_cast<int*>(&kv), &v_band};
+        if (hipLaunchKernel(kern, g1, dim3(256), args, lds1, s) != hipSuccess) return -1;
+    } else {
+        // K4+K5v: the band's grey tile, meta and zero-padded weights in LDS (a band whose tile
+        // does not fit reads HBM directly)
+        const int tile_cap = v_rows < 256 ? v_rows : 256;
+        const int lds1 = ((((int)v_band + 3) & ~3) + ((tile_cap * 65 + 3) & ~3) + (int)v_band * kv) * 4;
+        if (lds1 > 163840) return -2;
+        if (hipFuncSetAttribute(reinterpret_cast<const void*>(grey_vert_kernel),
+                                hipFuncAttributeMaxDynamicSharedMemorySize, lds1) != hipSuccess)
+            return -1;
+        dim3 g1((T_max + 63) / 64, (nh + v_band - 1) / v_band, n);
+        hipLaunchKernelGGL(grey_vert_kernel, g1, dim3(256), lds1, s, spec, bins, max, min, nh, d_desc, tmp,
+                           tile_cap, kv, v_band);
+    }
     // K5h + K6: the three-stage path's horizontal pass (same intermediate layout [nh][T])
     // row blocks per image: THESIA_RYH, more when few images would leave CUs idle
     uint32_t ry_h = THESIA_RYH;  // (8 rows blocks: same time with the LDS-DMA pass; 32: +4 %)

@@ -1180,6 +1180,7 @@ struct FusedGroup {
     uint64_t tmp_tot = 0;         // intermediate floats ([nheight][T] per track)
     uint32_t T_max = 0, H_max = 0, nw_max = 0, v_band = 1;
     int h_taps = 0, h_span = 0, v_rows = 1, v_kv = 4;
+    int v_fpl = 1;  // frames per lane of the vertical pass (4: grey_vert_wide_kernel)
 };
 
 // Host planning of one group: a RenderDesc per non-empty track (appended to `desc`), the
@@ -1187,7 +1188,7 @@ struct FusedGroup {
 // tile for every track of the group) and the horizontal pass's tap / span bounds.
 int plan_fused_group(const float* d_spec, const uint64_t* row0, size_t bins, size_t n,
                      const float* up_ratio, const uint32_t* nwidth, uint32_t nheight,
-                     const uint64_t* rgb_off, std::vector<RenderDesc>& desc, FusedGroup& g) {
+                     const uint64_t* rgb_off, std::vector<RenderDesc>& desc, FusedGroup& g, bool wide) {
     g.spec = d_spec;
     g.bins = (uint32_t)bins;
     g.desc0 = desc.size();
@@ -1234,7 +1235,7 @@ int plan_fused_group(const float* d_spec, const uint64_t* row0, size_t bins, siz
     int kv = 4;
     for (const auto& [vt, oz] : vts) kv = std::max(kv, (vt->max_taps + 3) & ~3);
     g.v_kv = kv;
-    auto band_need = [&](uint32_t band, int* rows_out) {
+    auto band_need = [&](uint32_t band, int* rows_out, int cap) {
         int rows = 1;
         for (const auto& [vt, oz] : vts)
             for (uint32_t ob = 0; ob < nheight; ob += band) {
@@ -1243,10 +1244,27 @@ int plan_fused_group(const float* d_spec, const uint64_t* row0, size_t bins, siz
                 rows = std::max(rows, vt->h_left[o1] - vt->h_left[o0] + kv);
             }
         *rows_out = rows;
-        return rows <= THESIA_VROWS && (int)band * kv <= 4096;
+        return rows <= cap && (int)band * kv <= 4096;
     };
     g.v_band = THESIA_VBAND;
-    while (!band_need(g.v_band, &g.v_rows) && g.v_band > 1) g.v_band /= 2;
+    while (!band_need(g.v_band, &g.v_rows, THESIA_VROWS) && g.v_band > 1) g.v_band /= 2;
+    g.v_fpl = 1;
+    if (wide && g.H_max <= nheight) {
+        // the wide vertical pass (4 frames per lane; its tile rows are 260 floats, so it holds
+        // at most 40 of them, ~42 KiB) for groups that upsample vertically (H <= nheight: few
+        // grey rows per band) where a band of at least 16 output rows fits. Measured per group
+        // (C5, profiles/r03_s2_display): 44.1 kHz / n_fft 256 470 -> 381 us, 22.05 kHz / 256
+        // 176 -> 159, 48 kHz / 512 310 -> 295; the downsampling groups ran slower (their bands
+        // shrink to 16 rows of 40 tile rows). Display per C5 step 3.285 -> 3.232 ms (in process).
+        uint32_t band = THESIA_VBAND;
+        int rows = 1;
+        while (!band_need(band, &rows, 40) && band > 1) band /= 2;
+        if (band >= 16 && band_need(band, &rows, 40)) {
+            g.v_fpl = 4;
+            g.v_band = band;
+            g.v_rows = rows;
+        }
+    }
     return THESIA_OK;
 }
 
@@ -1303,7 +1321,7 @@ int render_rgb_fused(size_t n_groups, const float* const* d_specs, const uint64_
         size_t t0 = 0;
         for (size_t k = 0; k < n_groups; ++k) {
             rc = plan_fused_group(d_specs[k], row0s[k], bins[k], ns[k], up_ratio + t0, nwidth + t0, nheight,
-                                  rgb_off + t0, desc, groups[k]);
+                                  rgb_off + t0, desc, groups[k], true);
             if (rc) return rc;
             tmp_max = std::max<uint64_t>(tmp_max, groups[k].tmp_tot);
             t0 += ns[k];
@@ -1334,7 +1352,8 @@ int render_rgb_fused(size_t n_groups, const float* const* d_specs, const uint64_
             const uint32_t nb = (uint32_t)std::min<size_t>(65535, g.ndesc - b);
             if (launch_render_batch2(g.spec, g.bins, max, min, ws.desc.as<RenderDesc>() + g.desc0 + b, nb,
                                      g.T_max, g.H_max, g.nw_max, nheight, g.h_taps, g.h_span, g.v_band,
-                                     g.v_rows, g.v_kv, ws.tmp.as<float>(), cmap_ptr, d_rgb, s, h_dma))
+                                     g.v_rows, g.v_kv, ws.tmp.as<float>(), cmap_ptr, d_rgb, s, h_dma,
+                                     g.v_fpl))
                 return set_error(THESIA_ERR_DEVICE, "render batch launch failed");
         }
     // stream-ordered: the images are complete for every later library call (copies included)

@@ -190,7 +190,10 @@ int launch_render_batch2(const float* spec, uint32_t bins, float max, float min,
                          const RenderDesc* d_desc, uint32_t n, uint32_t T_max, uint32_t H_max,
                          uint32_t nw_max, uint32_t nh, int h_taps, int h_span, uint32_t v_band,
                          int v_rows, int v_kv, float* tmp, const uint8_t* cmap, uint8_t* rgb,
-                         hipStream_t s, bool h_dma = true);  // h_dma: the LDS-DMA horizontal pass
+                         hipStream_t s, bool h_dma = true,  // h_dma: the LDS-DMA horizontal pass
+                         int v_fpl = 1);  // frames per lane of the vertical pass (1, or 4: wide)
+// LDS bytes of the wide vertical pass (grey_vert_wide_kernel<fpl>) for a band / tile / kv
+int grey_vert_wide_lds_bytes(int fpl, uint32_t band, int tile_cap, int kv);
 int launch_spec_to_grey(const float* spec, uint32_t T, uint32_t bins, uint32_t H, float max,
                         float min, float* grey, hipStream_t s);
 int launch_resize_v(const float* in, uint32_t w, uint32_t h, uint32_t nh, const int32_t* left,

@@ -310,9 +310,9 @@ stft3_kernel(StftLaunch a, uint64_t fps) {
             }
             untangle2<NC, kBatch>(v, j, partner, ub, [&](int k, float xr, float xi) {
                 const float p2 = __builtin_fmaf(xr, xr, xi * xi);
-                float val = power ? p2 : __builtin_amdgcn_sqrtf(p2);
-                if (db) val = power ? db_of(val, a.log_amin, 1e-36f, 10.0f)
-                                    : db_of(val, a.log_amin, 1e-18f, 20.0f);
+                // amp dB from |X|^2 (amp_db_of: no v_sqrt); amp / power as is
+                const float val = db ? (power ? db_of(p2, a.log_amin, 1e-36f, 10.0f) : amp_db_of(p2, a.log_amin))
+                                     : (power ? p2 : __builtin_amdgcn_sqrtf(p2));
                 st[k] = val;
                 if (rng) {
                     r_max = fmaxf(r_max, val);

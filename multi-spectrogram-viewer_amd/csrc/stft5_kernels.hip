@@ -545,10 +545,9 @@ stft5_kernel(StftLaunch a, uint64_t fps, int rs) {
             float* stg = region + sh;
             auto val_of = [&](float xr, float xi) {
                 const float p2 = __builtin_fmaf(xr, xr, xi * xi);
-                float val = power ? p2 : __builtin_amdgcn_sqrtf(p2);
-                if (db) val = power ? db_of(val, a.log_amin, 1e-36f, 10.0f)
-                                    : db_of(val, a.log_amin, 1e-18f, 20.0f);
-                return val;
+                // amp dB from |X|^2 (amp_db_of: no v_sqrt); amp / power as is
+                return db ? (power ? db_of(p2, a.log_amin, 1e-36f, 10.0f) : amp_db_of(p2, a.log_amin))
+                          : (power ? p2 : __builtin_amdgcn_sqrtf(p2));
             };
             untangle5<0, 16>(v, lane0, rot, wkb, wj, [&](int k, float xr, float xi, auto) {
                 stg[k] = val_of(xr, xi);

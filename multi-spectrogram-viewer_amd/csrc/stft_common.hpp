@@ -108,6 +108,15 @@ __device__ __forceinline__ float db_of(float x, float log_amin, float amin, floa
     return factor * (l - 0.0f);
 }
 
+// Amp dB of a bin from its |X|^2 p (fast kernels): 20 log10(sqrt(p)) = 10 log10(p), and
+// |X| > amin = 1e-18 <=> p > 1e-36 (a normal float), the clamp 20 log10(amin) = 10 (2 log10(amin))
+// exactly (log_amin is the plan's log10(1e-18)). One v_log_f32 instead of v_sqrt + v_log: the
+// rounding differs from db_of(sqrt(p)) by a few ulp of the log, inside tests/tolerances.py.
+__device__ __forceinline__ float amp_db_of(float p, float log_amin) {
+    const float l = p > 1e-36f ? __builtin_amdgcn_logf(p) * 0.30102999566398119521f : 2.0f * log_amin;
+    return 10.0f * (l - 0.0f);
+}
+
 // Output row stores. Plain stores: non-temporal ones (THESIA_NT_STORES, experiment) measured
 // slower and bimodal on the complex-output kernel (7.6 / 10.1 ms vs 6.24 ms).
 #ifdef THESIA_NT_STORES

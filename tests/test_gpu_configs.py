@@ -103,7 +103,7 @@ def test_c5_mixed_rate_render_pipeline():
         assert r.rgb.tobytes() == img.tobytes(), (t.sr, t.n_fft)  # display path bit-exact
 
 
-@pytest.mark.parametrize("path", [0, 1, 2])  # two-kernel (LDS-DMA horizontal) / per-track / three-stage
+@pytest.mark.parametrize("path", [0, 1, 2])  # two-kernel (LDS-DMA horizontal; wide vertical pass for upsampling groups) / per-track / three-stage
 @pytest.mark.parametrize("px_per_sec", [73.0, 30.0, 9.0, 2.0])  # 30: 17-64 taps; 9, 2: wider spans
 @pytest.mark.parametrize("nheight", [90, 400, 600])  # 400, 600: H -> nheight downsampling ~2.5, taller
 def test_render_batch_ragged_groups(path, px_per_sec, nheight):
