@@ -52,6 +52,8 @@ def parse():
     p.add_argument("--input", choices=["f32", "s16"], default="f32")
     p.add_argument("--n-fft", type=int, default=2048)
     p.add_argument("--hop", type=int, default=512)
+    p.add_argument("--win", type=int, default=None,
+                   help="window length (default n_fft; the viewer geometries: e.g. 1920 with --hop 480)")
     p.add_argument("--n-mels", type=int, default=128)
     p.add_argument("--output", choices=["mel_db", "amp_db", "power_db", "complex"], default="mel_db")
     p.add_argument("--no-cpu-baseline", action="store_true")
@@ -81,6 +83,8 @@ def parse():
                    help="launcher / reduction plumbing only: no GPU, no thesia (CPU tests)")
     p.add_argument("--selftest-fail-rank", type=int, default=-1, help=argparse.SUPPRESS)
     a = p.parse_args()
+    if a.win is None:
+        a.win = a.n_fft
     if a.seconds is None:
         a.seconds = 30.0 if a.workload == "c4" else 10.0
     if a.channels is None:
@@ -231,7 +235,7 @@ def cpu_baseline(args, n_samples):
            for i in range(n_tracks)]
 
     def one(x):
-        return O.track_spec(x, args.n_fft, args.hop, args.n_fft, kind, fb).shape[0]
+        return O.track_spec(x, args.win, args.hop, args.n_fft, kind, fb).shape[0]
 
     t0 = time.perf_counter()
     with ThreadPoolExecutor(threads) as ex:
@@ -338,7 +342,7 @@ def rfft_roofline(args, din, offs, lens, fmt, n_local, n_samples):
     output byte written once, coalesced float4). Reported beside the headline roofline, never as
     `value`."""
     from thesia import engine
-    plan = engine.Plan(args.n_fft, args.n_fft, args.hop, engine.OUT_COMPLEX, sr=args.sr)
+    plan = engine.Plan(args.n_fft, args.win, args.hop, engine.OUT_COMPLEX, sr=args.sr)
     frames = engine.Batch.frames_for(plan, lens)
     out_bytes = frames * plan.row_bins * 8
     dout = engine.DeviceBuffer(out_bytes)
@@ -368,6 +372,7 @@ def workload_params(args, kernel):
     """Every parameter that changes what one launch moves or issues (the key of a stored PMC
     record: a record applies to this run only if all of them are equal)."""
     return {"output": args.output, "input": args.input, "channels": args.channels, "n_fft": args.n_fft,
+            **({"win": args.win} if args.win != args.n_fft else {}),
             "hop": args.hop, "tracks_per_gpu": args.tracks, "seconds": args.seconds, "sr": args.sr,
             "n_mels": args.n_mels if args.output == "mel_db" else 0, "kernel": kernel, "mel_path": 0}
 
@@ -754,13 +759,13 @@ def main_worker(args):
     kind = {"mel_db": engine.OUT_MEL_AMP_DB, "amp_db": engine.OUT_AMP_DB,
             "power_db": engine.OUT_POWER_DB, "complex": engine.OUT_COMPLEX}[args.output]
     fmt = engine.IN_F32 if args.input == "f32" else engine.IN_S16
-    plan = engine.Plan(args.n_fft, args.n_fft, args.hop, kind, sr=args.sr,
+    plan = engine.Plan(args.n_fft, args.win, args.hop, kind, sr=args.sr,
                        n_mels=args.n_mels if kind == engine.OUT_MEL_AMP_DB else 0)
     el = 4 if fmt == engine.IN_F32 else 2
     per_track = n_samples * args.channels
     # the job's tracks (tracks-per-GPU x ranks) are partitioned per file by LPT
     # (thesia.shard); every rank computes the same partition, no exchange
-    mine = shard.plan_shards([n_samples] * (args.tracks * ws), args.n_fft, args.hop, args.n_fft,
+    mine = shard.plan_shards([n_samples] * (args.tracks * ws), args.win, args.hop, args.n_fft,
                              args.n_mels if kind == engine.OUT_MEL_AMP_DB else 0, ws, rank)
     n_local = len(mine)
     din = engine.DeviceBuffer(n_local * per_track * el)
@@ -850,7 +855,8 @@ def main_worker(args):
         "config": {
             "workload": f"{args.workload.upper()} per-GPU shard: {n_local} x {args.sr/1000:g} kHz {args.seconds:g} s "
                         f"{'stereo' if args.channels == 2 else str(args.channels) + '-ch'} tracks per GPU "
-                        f"({args.input} interleaved), n_fft {args.n_fft} hop {args.hop} Hann, "
+                        f"({args.input} interleaved), n_fft {args.n_fft} "
+                        f"{'' if args.win == args.n_fft else 'win ' + str(args.win) + ' '}hop {args.hop} Hann, "
                         f"sum-downmix, {'mel-' + str(args.n_mels) + ' + amp dB' if kind == engine.OUT_MEL_AMP_DB else args.output}",
             "tracks_per_gpu": n_local,
             "tracks_total": args.tracks * ws,

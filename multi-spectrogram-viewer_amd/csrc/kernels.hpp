@@ -135,6 +135,11 @@ int stft2_kernel_info(int n_fft, int* lds_bytes, int* tile_frames, int* lanes_pe
 int launch_stft3(const StftLaunch& a, hipStream_t stream);
 bool stft3_supports(int n_fft, int win, int hop, int in_format, int channels);
 int stft3_lds_bytes(const StftLaunch& a);  // dynamic LDS of the launch (> 163840: cannot run)
+// the streaming kernel at the viewer geometries (stft3v_kernels.hip: win = 4 hop < n_fft, even
+// hop; launch_stft3 / stft3_supports / stft3_lds_bytes dispatch to these)
+int launch_stft3v(const StftLaunch& a, hipStream_t stream);
+bool stft3v_supports(int n_fft, int win, int hop, int in_format, int channels);
+int stft3v_lds_bytes(const StftLaunch& a);
 // stftx_kernel (every n_fft: the reference's operation order, bit-exact with the oracle)
 int launch_stftx(const StftLaunch& a, hipStream_t stream);
 int stftx_lds_bytes(int n_fft, bool mel);

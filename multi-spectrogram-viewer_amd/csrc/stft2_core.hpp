@@ -121,7 +121,11 @@ constexpr int fft2_stride(bool wide) { return Geo2<NC>::L + (wide ? 4 : 2); }
 // TPRIO > 0: the twiddle reads and the LDS transpose run at wave priority TPRIO, the register
 // DFT stages at 0 (stft3 priority phases).
 template <int NC, class TwF, bool WIDE = false, int TPRIO = 0>
-__device__ __forceinline__ void fft2(float2 (&v)[Geo2<NC>::P], float* region, int j, const TwF& twf) {
+__device__ __forceinline__ void fft2(float2 (&v)[Geo2<NC>::P], float* region, int j, const TwF& twf,
+                                     int jw = -1) {
+    // jw: the transpose column this lane's stage-1 outputs go to (default j; stft3's viewer
+    // geometries write the frame's column and read row j)
+    if (jw < 0) jw = j;
     using G = Geo2<NC>;
     constexpr int L = G::L, P = G::P, S = fft2_stride<NC>(WIDE), CPL = G::CPL;
     pin(v);
@@ -150,7 +154,7 @@ __device__ __forceinline__ void fft2(float2 (&v)[Geo2<NC>::P], float* region, in
         static_for<0, P>([&](auto kc) {
             constexpr int k1 = decltype(kc)::value;
             constexpr int pk = ce_pos(P, k1);
-            region[k1 * S + j] = e == 0 ? v[pk].x : v[pk].y;
+            region[k1 * S + jw] = e == 0 ? v[pk].x : v[pk].y;
         });
         wave_lds_sync();
         static_for<0, CPL>([&](auto cc) {

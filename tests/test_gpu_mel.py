@@ -157,8 +157,15 @@ def test_kernel_choice_and_unsupported_force():
     x = np.zeros((4096, 2), np.float32)
     _run(engine.OUT_MEL_AMP_DB, [x], 2, engine.IN_F32, n_mels=128, kernel=5)
     _run(engine.OUT_MEL_AMP_DB, [x], 2, engine.IN_F32, n_mels=128, kernel=3)
-    plan = engine.Plan(2048, 1920, 480, engine.OUT_AMP_DB)  # viewer geometry: not streaming
+    plan = engine.Plan(2048, 1920, 480, engine.OUT_AMP_DB)  # the 48 kHz viewer geometry streams
     din = engine.DeviceBuffer.from_host(x[:, 0].copy())
+    dout = engine.DeviceBuffer(engine.Batch.frames_for(plan, [4096]) * plan.row_bins * 4)
+    b = engine.Batch(plan, din, [0], [4096], dout)
+    assert b.kernel == 3
+    import thesia
+    with pytest.raises(thesia.ThesiaError):
+        b.set_option(engine.OPT_KERNEL, 5)  # stft5: the canonical geometry only
+    plan = engine.Plan(2048, 1764, 441, engine.OUT_AMP_DB)  # 44.1 kHz viewer geometry: odd hop
     dout = engine.DeviceBuffer(engine.Batch.frames_for(plan, [4096]) * plan.row_bins * 4)
     b = engine.Batch(plan, din, [0], [4096], dout)
     assert b.kernel == 2

@@ -1,0 +1,154 @@
+"""The streaming kernel at the viewer's own geometries (stft3v_kernels.hip; lib.rs:43-46,93-99:
+win = round(40 ms sr / 4) 4, hop = win / 4, n_fft = next_pow2(win), so win < n_fft and the hop is
+not a whole number of a lane's rows) against the oracle: streams across track ends, tracks at odd
+element offsets (per-frame reloads), the shortest legal tracks (n = win - 1, lib.rs:413), reflect
+at both ends, mono / stereo, f32 / s16, every output kind, and a grid small enough that each
+stream walks hundreds of frames through the ring's per-lane select shift."""
+import numpy as np
+import pytest
+
+import oracle_ffi as O
+from thesia import engine
+from tolerances import DB_MAX, DB_P9999, STFT_REL, db_clamped_err, stft_frame_err
+
+pytestmark = pytest.mark.gpu
+
+# (n_fft, win, hop) of the viewer at 48 / 24 / 16 / 8 kHz (SURVEY.md §8 viewer-defaults row)
+VIEW = [(2048, 1920, 480), (1024, 960, 240), (1024, 640, 160), (512, 320, 80)]
+
+
+def _mono_fold(t):  # lib.rs:42 channel sum, (0 + c0) + c1 ...
+    acc = np.zeros(t.shape[0], np.float32)
+    for c in range(t.shape[1]):
+        acc = (acc + t[:, c]).astype(np.float32)
+    return acc
+
+
+def _tracks(rng, lens, channels, fmt):
+    out = []
+    for n in lens:
+        if fmt == engine.IN_S16:
+            out.append(rng.integers(-30000, 30000, size=(n, channels)).astype(np.int16))
+        else:
+            out.append((rng.standard_normal((n, channels)) * 0.3).astype(np.float32))
+    return out
+
+
+def _run(plan, tracks, channels, fmt, gap, max_blocks=3, kernel=0, row_floats=None):
+    parts, offs, off = [], [], 0
+    for t in tracks:
+        offs.append(off)
+        parts.append(t.reshape(-1))
+        off += t.size
+        if gap:
+            parts.append(np.zeros(gap, t.dtype))
+            off += gap
+    flat = np.concatenate(parts)
+    lens = [t.shape[0] for t in tracks]
+    din = engine.DeviceBuffer.from_host(flat)
+    T = engine.Batch.frames_for(plan, lens)
+    fl = row_floats if row_floats is not None else plan.row_bins
+    dout = engine.DeviceBuffer(T * fl * 4)
+    b = engine.Batch(plan, din, offs, lens, dout, input_format=fmt, channels=channels,
+                     kernel=kernel, max_blocks=max_blocks)
+    k = b.kernel
+    b.run()
+    engine.synchronize()
+    res = dout.to_host(np.float32)
+    rows = [res[int(b.frame0[i]) * fl:int(b.frame0[i + 1]) * fl] for i in range(len(tracks))]
+    b.close()
+    dout.close()
+    din.close()
+    return k, rows
+
+
+def _x(t, fmt):
+    x = t.astype(np.float32) / np.float32(32768.0) if fmt == engine.IN_S16 else t
+    return _mono_fold(x.astype(np.float32))
+
+
+@pytest.mark.parametrize("n_fft,win,hop", VIEW)
+@pytest.mark.parametrize("channels,fmt", [(1, engine.IN_F32), (2, engine.IN_F32), (2, engine.IN_S16),
+                                          (1, engine.IN_S16)])
+@pytest.mark.parametrize("gap", [0, 3])
+def test_viewer_geometry_complex_streams(n_fft, win, hop, channels, fmt, gap):
+    rng = np.random.default_rng(n_fft * 7 + hop + channels * 3 + fmt + gap)
+    lens = [win - 1, win, n_fft, n_fft + 1, 3 * n_fft + 7, 37 * hop, 10 * n_fft + 3, 60 * hop + 5,
+            2 * n_fft, 211 * hop + 11]
+    tracks = _tracks(rng, lens, channels, fmt)
+    plan = engine.Plan(n_fft, win, hop, engine.OUT_COMPLEX)
+    k, rows = _run(plan, tracks, channels, fmt, gap, row_floats=2 * plan.row_bins)
+    plan.close()
+    assert k == 3  # the streaming kernel is the automatic choice at this geometry
+    for t, r in zip(tracks, rows):
+        ref = O.perform_stft(_x(t, fmt), win, hop, n_fft)
+        got = r.view(np.complex64).reshape(ref.shape)
+        assert stft_frame_err(got, ref) <= STFT_REL, (len(t), stft_frame_err(got, ref))
+
+
+_KINDS = [engine.OUT_MAG, engine.OUT_POWER, engine.OUT_AMP_DB, engine.OUT_POWER_DB]
+
+
+@pytest.mark.parametrize("n_fft,win,hop", VIEW)
+@pytest.mark.parametrize("kind", _KINDS)
+@pytest.mark.parametrize("max_blocks", [0, 2])
+def test_viewer_geometry_linear_kinds(n_fft, win, hop, kind, max_blocks):
+    rng = np.random.default_rng(n_fft + hop + 11 * kind + max_blocks)
+    lens = [win - 1, 5 * n_fft + 3, 33 * hop + 1, 97 * hop + 2]
+    tracks = _tracks(rng, lens, 2, engine.IN_F32)
+    plan = engine.Plan(n_fft, win, hop, kind)
+    k, rows = _run(plan, tracks, 2, engine.IN_F32, 0, max_blocks=max_blocks)
+    plan.close()
+    assert k == 3
+    for t, r in zip(tracks, rows):
+        ref = O.perform_stft(_x(t, engine.IN_F32), win, hop, n_fft)
+        g = r.reshape(ref.shape[0], -1)
+        if kind == engine.OUT_MAG:
+            want = O.norm(ref)
+        elif kind == engine.OUT_POWER:
+            want = O.norm_sqr(ref)
+        elif kind == engine.OUT_AMP_DB:
+            want = O.amp_to_db_default(O.norm(ref))
+        else:
+            want = O.power_to_db_default(O.norm_sqr(ref))
+        if kind in (engine.OUT_AMP_DB, engine.OUT_POWER_DB):
+            mx, p = db_clamped_err(g, want)
+            assert mx <= DB_MAX and p <= DB_P9999, (mx, p)
+        else:
+            scale = np.abs(want).max(axis=1, keepdims=True)
+            rel = 4e-6 if kind == engine.OUT_MAG else 8e-6
+            assert np.all(np.abs(g - want) <= rel * np.maximum(scale, 1e-30)), float(np.abs(g - want).max())
+
+
+@pytest.mark.parametrize("n_fft,win,hop,sr", [(2048, 1920, 480, 48000), (1024, 960, 240, 24000),
+                                              (1024, 640, 160, 16000), (512, 320, 80, 8000)])
+@pytest.mark.parametrize("n_mels", [128, 40])
+def test_viewer_geometry_mel_db(n_fft, win, hop, sr, n_mels):
+    rng = np.random.default_rng(n_fft + n_mels + sr)
+    lens = [win - 1, 4 * n_fft + 5, 71 * hop + 3]
+    tracks = _tracks(rng, lens, 1, engine.IN_S16)
+    plan = engine.Plan(n_fft, win, hop, engine.OUT_MEL_AMP_DB, sr=sr, n_mels=n_mels)
+    k, rows = _run(plan, tracks, 1, engine.IN_S16, 0, max_blocks=2)
+    plan.close()
+    assert k == 3
+    fb = O.calc_mel_fb(sr, n_fft, n_mels)
+    for t, r in zip(tracks, rows):
+        ref = O.perform_stft(_x(t, engine.IN_S16), win, hop, n_fft)
+        want = O.amp_to_db_default(O.dot(O.norm(ref), fb))
+        mx, p = db_clamped_err(r.reshape(ref.shape[0], -1), want)
+        assert mx <= DB_MAX and p <= DB_P9999, (mx, p)
+
+
+def test_odd_hop_viewer_geometry_stays_general():
+    """44.1 kHz viewer geometry (1764 / 441 / 2048): an odd hop starts every other frame between
+    two complex points; the general kernel runs it, within tolerance."""
+    rng = np.random.default_rng(441)
+    n_fft, win, hop = 2048, 1764, 441
+    tracks = _tracks(rng, [win - 1, 20 * hop + 3], 1, engine.IN_F32)
+    plan = engine.Plan(n_fft, win, hop, engine.OUT_COMPLEX)
+    k, rows = _run(plan, tracks, 1, engine.IN_F32, 0, row_floats=2 * plan.row_bins)
+    plan.close()
+    assert k != 3
+    for t, r in zip(tracks, rows):
+        ref = O.perform_stft(_x(t, engine.IN_F32), win, hop, n_fft)
+        assert stft_frame_err(r.view(np.complex64).reshape(ref.shape), ref) <= STFT_REL
