@@ -1070,9 +1070,10 @@ int grey_vert_wide_lds_bytes(int fpl, uint32_t band, int tile_cap, int kv) {
 // (m * 4 + w) * 64 + lane, m < K; chunks past the span re-read the span's last chunk (finite
 // values in the buffer's tail, summed with zero weights: bits unchanged, as in the staged pass;
 // the intermediate's row padding is zeroed when its workspace is allocated). Each wave waits for
-// its own chunks of row k (a counted vmcnt: the only vector-memory ops after them are the next
-// NB - 2 rows' K chunks and this wave's byte stores, which only add to the count), then the
-// barrier makes the whole row visible and frees the buffer of row k - 1 for row k + NB - 1.
+// its own chunks of row k (vmcnt((NB - 2) K): all but the wave's (NB - 2) K youngest
+// vector-memory ops retire, in issue order; the RGB stores interleaved with the DMAs make that
+// wait stricter than row k alone — counting them exactly measured no faster), then
+// the barrier makes the whole row visible and frees the buffer of row k - 1 for row k + NB - 1.
 // Same sums and colormap as resize_h_rgb_batch_kernel (identical bytes).
 template <int N>
 __device__ __forceinline__ void wait_vm() {
