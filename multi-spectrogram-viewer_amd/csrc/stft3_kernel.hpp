@@ -36,7 +36,14 @@ namespace thesia {
 // repeats the ring's last row where the shift is HQ). The window row and the stage-1 twiddles
 // are the column's; the transpose writes column jc and reads row j, so from stage 2 on (bins,
 // untangle partners, outputs) the lane is j as in the canonical geometry.
-template <int NC, int OK, int C, int INF, int VAR = 0, int WV = kWaves, int HQ = 0>
+// VODD: an odd hop (22.05 / 44.1 kHz: 221 / 441 samples), where every other frame starts between
+// two complex points of the previous one. The streams then come in pairs that interleave the
+// frames (stream 2s takes frames g, g + 2, ..., 2s + 1 the ones between), so a stream's hop is
+// 2 hop samples = HQ L + rem points, and a frame starting at an odd sample reads the track on
+// the point grid shifted by one sample (base + C elements): the same ring, on that grid. Its
+// vector loads are then only dword-aligned (f32, or s16 stereo). Complex rows are stored per row
+// (a stream's rows are not contiguous).
+template <int NC, int OK, int C, int INF, int VAR = 0, int WV = kWaves, int HQ = 0, int VODD = 0>
 __global__ void __launch_bounds__(64 * WV, WV / 4)
 stft3_kernel(StftLaunch a, uint64_t fps) {
     constexpr int kBlock = 64 * WV;
@@ -48,6 +55,8 @@ stft3_kernel(StftLaunch a, uint64_t fps) {
     using ET = typename std::conditional<INF == IN_S16, int16_t, float>::type;
     constexpr int P = G::P, L = G::L, FPW = G::FPW, F = G::F, SH = G3::SH;
     constexpr bool VIEW = HQ > 0;
+    constexpr bool ODD = VODD != 0;
+    static_assert(!ODD || (VIEW && !line_rows(OK, VAR) && !(C == 1 && INF == IN_S16)), "odd-hop streams");
     constexpr int NPRE = VIEW ? HQ + 1 : SH;  // rows prefetched per frame
     constexpr int KEEP = P - NPRE;            // ring rows carried into the next frame
     static_assert(KEEP > 0, "hop shorter than the frame");
@@ -86,15 +95,19 @@ stft3_kernel(StftLaunch a, uint64_t fps) {
 
     const uint64_t total = a.total_frames;
     const uint64_t stream = ((uint64_t)blockIdx.x * WV + wave) * FPW + slot;
-    const uint64_t g0 = stream * fps;
-    const uint64_t g1 = g0 + fps < total ? g0 + fps : total;
+    // a stream's frames: g0 + GS it (ODD: a stream pair shares 2 fps frames, interleaved)
+    constexpr uint64_t GS = ODD ? 2 : 1;
+    const uint64_t g0 = (ODD ? (stream >> 1) * 2 * fps : stream * fps);
+    const uint64_t g1 = g0 + GS * fps < total ? g0 + GS * fps : total;
+    const uint64_t gpar = ODD ? (stream & 1) : 0;
     const int hop = a.hop;
+    const int hop_s = ODD ? 2 * hop : hop;  // samples between a stream's frames
     float* region = work + (wave * FPW + slot) * G3::RS_OK(stage_rows(OK, VAR), OK);
     const ET* in = static_cast<const ET*>(a.in);
 
     float2 raw[P];
     CT pre[NPRE];
-    const int rem = VIEW ? (a.hop >> 1) & (L - 1) : 0;
+    const int rem = VIEW ? (hop_s >> 1) & (L - 1) : 0;
     bool pre_ok = false;
     int hint = -1;
     // the stream's current track, cached across frames (looked up again only past its end)
@@ -129,28 +142,12 @@ stft3_kernel(StftLaunch a, uint64_t fps) {
         // bound chains (bpermute batch, |X| row, mel rounds) then issues first whenever it is
         // ready and the other wave's FFT (high ILP) fills the gaps: mel-128 5.13 -> 4.67 ms.
         if constexpr ((VAR & 4096) == 0) __builtin_amdgcn_s_setprio(0);
-        const uint64_t g = g0 + it;
+        const uint64_t g = g0 + gpar + GS * it;
         const bool valid = g < g1;
         // opaque per frame: keeps the untangle rotations (from ub) and the window reads (from
         // wj) inside the loop instead of hoisted as loop invariants into 100+ VGPRs
 #pragma unroll
         for (int c = 0; c < G::CPL; ++c) asm volatile("" : "+v"(ub[c].x), "+v"(ub[c].y));
-        int jc = j;  // the frame's column (HQ > 0)
-        if constexpr (VIEW) {
-            if (valid) {
-                if (g >= g_end || g < g_beg) {
-                    hint = find_track(a.trk_frame0, a.n_tracks, g, hint);
-                    g_beg = a.trk_frame0[hint];
-                    g_end = a.trk_frame0[hint + 1];
-                    n = (int64_t)a.trk_len[hint];
-                    base = a.trk_in_off[hint];
-                }
-                jc = (j - (int)(((g - g_beg) * (uint64_t)rem) & (L - 1))) & (L - 1);
-            }
-        }
-        int wj = jc;
-        asm volatile("" : "+v"(wj));
-        const float4* wrow = reinterpret_cast<const float4*>(wtl + wj * G3::WL_STRIDE);
         int64_t start = 0;
         if (valid) {
             if (g >= g_end || g < g_beg) {
@@ -162,6 +159,32 @@ stft3_kernel(StftLaunch a, uint64_t fps) {
             }
             start = (int64_t)(g - g_beg) * hop - NC;  // half_win = NC, pad_left = 0
         }
+        // the frame's point grid (ODD: shifted by one sample for an odd start) and its column
+        const int par = ODD ? (int)(start & 1) : 0;
+        const uint64_t bse = base + (uint64_t)(par * C);
+        const int64_t st = start - par;
+        int jc = j;  // the frame's column (HQ > 0): (j - frame start in points) mod L
+        if constexpr (VIEW) {
+            if (valid) jc = (j - (int)((st >> 1) & (L - 1))) & (L - 1);
+        }
+        int wj = jc;
+        asm volatile("" : "+v"(wj));
+        const float4* wrow = reinterpret_cast<const float4*>(wtl + wj * G3::WL_STRIDE);
+        // the vector loads of a frame at element offset e: naturally aligned (CT = 2 samples x C
+        // channels), or on ODD grids dword-aligned (4-byte-aligned memcpy loads; s16 tracks at an
+        // odd element offset take the generic loader)
+        auto aligned = [&](uint64_t e) {
+            return ODD ? (e * sizeof(ET)) % 4 == 0 : e % (2 * C) == 0;
+        };
+        auto ldc = [](const CT* p) -> CT {
+            if constexpr (ODD) {
+                CT v;
+                __builtin_memcpy(&v, __builtin_assume_aligned(p, 4), sizeof(CT));
+                return v;
+            } else {
+                return *p;
+            }
+        };
         // ---- the frame's raw samples (a hop: shift by SH points + the prefetched new ones) ----
         // (a rotating slot map instead of the shift was measured 1.05 ms slower: the switch
         // over four slot maps keeps all P raw points live and spills in the hot loop)
@@ -179,13 +202,13 @@ stft3_kernel(StftLaunch a, uint64_t fps) {
             }
 #pragma unroll
             for (int q = 0; q < NPRE; ++q) raw[KEEP + q] = CK::mix(pre[q]);
-        } else if (valid && start >= 0 && start + 2 * NC <= n && ((base + (uint64_t)start * C) % (2 * C)) == 0) {
-            const CT* src = reinterpret_cast<const CT*>(in + base + (uint64_t)start * C) + jc;
+        } else if (valid && start >= 0 && start + 2 * NC <= n && aligned(bse + (uint64_t)st * C)) {
+            const CT* src = reinterpret_cast<const CT*>(in + bse + (uint64_t)st * C) + jc;
             static_for<0, P / 8>([&](auto gc) {  // 8 loads in flight per chunk
                 constexpr int g8 = decltype(gc)::value;
                 static_for<0, 8>([&](auto ic) {
                     constexpr int n1 = 8 * g8 + decltype(ic)::value;
-                    raw[n1] = CK::mix(src[L * n1]);
+                    raw[n1] = CK::mix(ldc(src + L * n1));
                 });
                 pin_range<8 * g8, 8 * g8 + 8>(raw);
             });
@@ -206,16 +229,16 @@ stft3_kernel(StftLaunch a, uint64_t fps) {
         });
         // ---- prefetch the next frame's hop of new samples (its points P-SH .. P-1) ----
         {
-            const int64_t nstart = start + hop;
-            const bool nxt = valid && g + 1 < g1 && g + 1 < g_end && nstart + 2 * NC <= n &&
-                             nstart + 2 * L * KEEP >= 0 &&
-                             ((base + (uint64_t)(nstart + 2 * L * KEEP) * C) % (2 * C)) == 0;
+            const int64_t nstart = start + hop_s, nst = st + hop_s;
+            const bool nxt = valid && g + GS < g1 && g + GS < g_end && nstart + 2 * NC <= n &&
+                             nst + 2 * L * KEEP >= 0 &&
+                             aligned(bse + (uint64_t)(nst + 2 * L * KEEP) * C);
             if constexpr ((VAR & 65536) != 0) __builtin_amdgcn_s_setprio(3);  // experiment
             if (nxt) {
                 const int jn = (jc - rem) & (L - 1);  // the next frame's column (= j unless HQ > 0)
-                const CT* src = reinterpret_cast<const CT*>(in + base + (uint64_t)(nstart + 2 * L * KEEP) * C) + jn;
+                const CT* src = reinterpret_cast<const CT*>(in + bse + (uint64_t)(nst + 2 * L * KEEP) * C) + jn;
 #pragma unroll
-                for (int q = 0; q < NPRE; ++q) pre[q] = src[L * q];
+                for (int q = 0; q < NPRE; ++q) pre[q] = ldc(src + L * q);
             }
             pre_ok = nxt;
             if constexpr ((VAR & 65536) != 0) __builtin_amdgcn_s_setprio(0);

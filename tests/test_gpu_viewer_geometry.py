@@ -15,6 +15,8 @@ pytestmark = pytest.mark.gpu
 
 # (n_fft, win, hop) of the viewer at 48 / 24 / 16 / 8 kHz (SURVEY.md §8 viewer-defaults row)
 VIEW = [(2048, 1920, 480), (1024, 960, 240), (1024, 640, 160), (512, 320, 80)]
+# and at 44.1 / 22.05 kHz: odd hops (streams in pairs interleaving the frames)
+VIEW_ODD = [(2048, 1764, 441), (1024, 884, 221)]
 
 
 def _mono_fold(t):  # lib.rs:42 channel sum, (0 + c0) + c1 ...
@@ -67,7 +69,7 @@ def _x(t, fmt):
     return _mono_fold(x.astype(np.float32))
 
 
-@pytest.mark.parametrize("n_fft,win,hop", VIEW)
+@pytest.mark.parametrize("n_fft,win,hop", VIEW + VIEW_ODD)
 @pytest.mark.parametrize("channels,fmt", [(1, engine.IN_F32), (2, engine.IN_F32), (2, engine.IN_S16),
                                           (1, engine.IN_S16)])
 @pytest.mark.parametrize("gap", [0, 3])
@@ -79,7 +81,9 @@ def test_viewer_geometry_complex_streams(n_fft, win, hop, channels, fmt, gap):
     plan = engine.Plan(n_fft, win, hop, engine.OUT_COMPLEX)
     k, rows = _run(plan, tracks, channels, fmt, gap, row_floats=2 * plan.row_bins)
     plan.close()
-    assert k == 3  # the streaming kernel is the automatic choice at this geometry
+    # the streaming kernel is the automatic choice at this geometry (odd hops: not for s16 mono,
+    # whose 2-byte samples give vector loads below dword alignment on the shifted grid)
+    assert k == (2 if hop % 2 and fmt == engine.IN_S16 and channels == 1 else 3)
     for t, r in zip(tracks, rows):
         ref = O.perform_stft(_x(t, fmt), win, hop, n_fft)
         got = r.view(np.complex64).reshape(ref.shape)
@@ -89,7 +93,7 @@ def test_viewer_geometry_complex_streams(n_fft, win, hop, channels, fmt, gap):
 _KINDS = [engine.OUT_MAG, engine.OUT_POWER, engine.OUT_AMP_DB, engine.OUT_POWER_DB]
 
 
-@pytest.mark.parametrize("n_fft,win,hop", VIEW)
+@pytest.mark.parametrize("n_fft,win,hop", VIEW + VIEW_ODD)
 @pytest.mark.parametrize("kind", _KINDS)
 @pytest.mark.parametrize("max_blocks", [0, 2])
 def test_viewer_geometry_linear_kinds(n_fft, win, hop, kind, max_blocks):
@@ -121,34 +125,41 @@ def test_viewer_geometry_linear_kinds(n_fft, win, hop, kind, max_blocks):
 
 
 @pytest.mark.parametrize("n_fft,win,hop,sr", [(2048, 1920, 480, 48000), (1024, 960, 240, 24000),
-                                              (1024, 640, 160, 16000), (512, 320, 80, 8000)])
+                                              (1024, 640, 160, 16000), (512, 320, 80, 8000),
+                                              (2048, 1764, 441, 44100), (1024, 884, 221, 22050)])
 @pytest.mark.parametrize("n_mels", [128, 40])
 def test_viewer_geometry_mel_db(n_fft, win, hop, sr, n_mels):
     rng = np.random.default_rng(n_fft + n_mels + sr)
     lens = [win - 1, 4 * n_fft + 5, 71 * hop + 3]
-    tracks = _tracks(rng, lens, 1, engine.IN_S16)
+    fmt = engine.IN_F32 if hop % 2 else engine.IN_S16
+    tracks = _tracks(rng, lens, 1, fmt)
     plan = engine.Plan(n_fft, win, hop, engine.OUT_MEL_AMP_DB, sr=sr, n_mels=n_mels)
-    k, rows = _run(plan, tracks, 1, engine.IN_S16, 0, max_blocks=2)
+    k, rows = _run(plan, tracks, 1, fmt, 0, max_blocks=2)
     plan.close()
     assert k == 3
     fb = O.calc_mel_fb(sr, n_fft, n_mels)
     for t, r in zip(tracks, rows):
-        ref = O.perform_stft(_x(t, engine.IN_S16), win, hop, n_fft)
+        ref = O.perform_stft(_x(t, fmt), win, hop, n_fft)
         want = O.amp_to_db_default(O.dot(O.norm(ref), fb))
         mx, p = db_clamped_err(r.reshape(ref.shape[0], -1), want)
         assert mx <= DB_MAX and p <= DB_P9999, (mx, p)
 
 
-def test_odd_hop_viewer_geometry_stays_general():
-    """44.1 kHz viewer geometry (1764 / 441 / 2048): an odd hop starts every other frame between
-    two complex points; the general kernel runs it, within tolerance."""
-    rng = np.random.default_rng(441)
-    n_fft, win, hop = 2048, 1764, 441
-    tracks = _tracks(rng, [win - 1, 20 * hop + 3], 1, engine.IN_F32)
-    plan = engine.Plan(n_fft, win, hop, engine.OUT_COMPLEX)
-    k, rows = _run(plan, tracks, 1, engine.IN_F32, 0, row_floats=2 * plan.row_bins)
+@pytest.mark.parametrize("n_fft,win,hop", VIEW_ODD)
+@pytest.mark.parametrize("n_tracks", [1, 2, 7])
+def test_odd_hop_pairs_across_track_ends(n_fft, win, hop, n_tracks):
+    """Odd hops: a stream pair shares its frames (even / odd ones); with tracks of odd and even
+    frame counts the pair's parity relative to each track changes at every track end, and with
+    max_blocks 1 every stream pair crosses several tracks."""
+    rng = np.random.default_rng(n_fft + hop + n_tracks)
+    lens = [int(v) for v in rng.integers(win - 1, 60 * hop, n_tracks)]
+    tracks = _tracks(rng, lens, 2, engine.IN_F32)
+    plan = engine.Plan(n_fft, win, hop, engine.OUT_AMP_DB)
+    for mb in (1, 2, 0):
+        k, rows = _run(plan, tracks, 2, engine.IN_F32, 1, max_blocks=mb)
+        assert k == 3
+        for t, r in zip(tracks, rows):
+            ref = O.perform_stft(_x(t, engine.IN_F32), win, hop, n_fft)
+            mx, p = db_clamped_err(r.reshape(ref.shape[0], -1), O.amp_to_db_default(O.norm(ref)))
+            assert mx <= DB_MAX and p <= DB_P9999, (len(t), mb, mx, p)
     plan.close()
-    assert k != 3
-    for t, r in zip(tracks, rows):
-        ref = O.perform_stft(_x(t, engine.IN_F32), win, hop, n_fft)
-        assert stft_frame_err(r.view(np.complex64).reshape(ref.shape), ref) <= STFT_REL
