@@ -99,11 +99,11 @@ def test_mel_fb_vs_float64_formula(sr, n_fft, n_mel):
 @pytest.mark.parametrize("n_fft", [256, 512, 1024, 2048, 4096])
 def test_default_n_mel_is_the_largest_without_an_empty_filter(sr, n_fft):
     """mel.rs:87-99 independently: starting from floor(2 mel(sr/2) / mel(sr/n_fft) - 1) capped at
-    F, the first n_mel whose float64 filterbank has no empty filter; the library's default table
-    has that n_mel (or, where a filter is empty only by f32 rounding, one less)."""
+    F, the first n_mel whose float64 filterbank has no empty filter: the library's default table
+    has exactly that n_mel at every viewer rate and n_fft 256..4096."""
     got = thesia.mel.calc_mel_fb_default(sr, n_fft).shape[1]
     n = int(2.0 * _hz_to_mel64(sr / 2.0) / _hz_to_mel64(sr / n_fft) - 1.0)
     n = min(n, n_fft // 2 + 1)
     while not (_mel_fb64(sr, n_fft, n).sum(axis=0) > 0).all():
         n -= 1
-    assert got in (n, n - 1), (got, n)
+    assert got == n, (got, n)
