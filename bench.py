@@ -66,6 +66,8 @@ def parse():
     p.add_argument("--variants", default="", help="experiment (needs THESIA_LIB=lib/libthesia_exp.so): "
                    "comma list of THESIA_STFT_VARIANT values to A/B (interleaved rounds, one process)")
     p.add_argument("--kernel", type=int, default=0, help="force a fused kernel (1/2/3/5; 0 = automatic)")
+    p.add_argument("--max-blocks", default="", help="A/B of the launch's block count (thesia_batch_set_option "
+                   "MAX_BLOCKS): comma list, 0 = the occupancy default")
     p.add_argument("--kernels", default="", help="A/B of named kernels on the product library: comma list "
                    "of kernel ids (interleaved rounds, one process), e.g. 3,5")
     p.add_argument("--mel-paths", default="", help="A/B of stft5's mel projections (THESIA_BATCH_OPT_MEL_PATH): "
@@ -817,6 +819,19 @@ def main_worker(args):
         if rank == 0:
             print(json.dumps({"kernels_ms": {str(k): {"median": float(np.median(t)), "min": float(min(t))}
                                              for k, t in res.items()}}), flush=True)
+
+    if args.max_blocks:
+        ms = [int(v) for v in args.max_blocks.split(",")]
+        res = {m: [] for m in ms}
+        for _ in range(5):  # interleaved rounds
+            for m in ms:
+                batch.set_option(engine.OPT_MAX_BLOCKS, m)
+                batch.run_timed(1)
+                res[m].append(batch.run_timed(3) / 3)
+        batch.set_option(engine.OPT_MAX_BLOCKS, 0)
+        if rank == 0:
+            print(json.dumps({"max_blocks_ms": {str(m): {"median": float(np.median(t)), "min": float(min(t))}
+                                                for m, t in res.items()}}), flush=True)
 
     if args.mel_paths:
         ps = [int(v) for v in args.mel_paths.split(",")]
