@@ -845,6 +845,49 @@ int batch_run(Batch* b, hipStream_t s) {
     return THESIA_OK;
 }
 
+// Library streams of the device (created once, kept), forked from and joined back to a caller's
+// stream: the work of independent launches (batches_run's batches, render_rgb_fused's groups)
+// overlaps, so one launch's ramp and tail fill with another's blocks. Callers hold
+// run_pool_mutex() from the fork to the join (the events are shared).
+struct RunPool {
+    static constexpr int kStreams = 4;
+    hipStream_t st[kStreams] = {};
+    hipEvent_t fork = nullptr, join[kStreams] = {};
+    hipError_t fork_from(hipStream_t s, int k) {
+        hipError_t e = hipEventRecord(fork, s);
+        for (int i = 0; i < k && e == hipSuccess; ++i) e = hipStreamWaitEvent(st[i], fork, 0);
+        return e;
+    }
+    int join_into(hipStream_t s, int k) {
+        hipError_t e = hipSuccess;
+        for (int i = 0; i < k; ++i) {
+            hipError_t e1 = hipEventRecord(join[i], st[i]);
+            if (e1 == hipSuccess) e1 = hipStreamWaitEvent(s, join[i], 0);
+            if (e == hipSuccess) e = e1;
+        }
+        return e == hipSuccess ? THESIA_OK : set_error(THESIA_ERR_DEVICE, hipGetErrorString(e));
+    }
+};
+static std::mutex& run_pool_mutex() {
+    static auto& mu = *new std::mutex();  // leaked, see dev_taps
+    return mu;
+}
+static int run_pool(RunPool** out) {  // caller holds run_pool_mutex()
+    static auto& pools = *new std::map<int, RunPool>();  // leaked, see dev_taps
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    RunPool& p = pools[dev];
+    if (!p.fork) {
+        for (int i = 0; i < RunPool::kStreams; ++i) {
+            THESIA_HIP(hipStreamCreateWithFlags(&p.st[i], hipStreamNonBlocking));
+            THESIA_HIP(hipEventCreateWithFlags(&p.join[i], hipEventDisableTiming));
+        }
+        THESIA_HIP(hipEventCreateWithFlags(&p.fork, hipEventDisableTiming));
+    }
+    *out = &p;
+    return THESIA_OK;
+}
+
 // Several batches (e.g. one per geometry group) on up to kRunStreams library streams of the
 // device, forked from and joined back to `s`: a small launch's ramp (the first frame of every
 // stream loaded without prefetch, the tables staged into LDS) overlaps the others' work.
@@ -858,34 +901,15 @@ int batches_run(Batch* const* b, size_t n, hipStream_t s) {
         if (std::adjacent_find(seen.begin(), seen.end()) != seen.end() || seen.front() == nullptr)
             return set_error(THESIA_ERR_INVALID_ARG, "batches_run: a batch handle appears twice (or is null)");
     }
-    constexpr int kRunStreams = 4;
-    struct Pool {
-        hipStream_t st[kRunStreams] = {};
-        hipEvent_t fork = nullptr, join[kRunStreams] = {};
-    };
-    static std::mutex mu;
-    static auto& pools = *new std::map<int, Pool>();  // leaked, see dev_taps
-    int dev = 0;
-    (void)hipGetDevice(&dev);
-    std::lock_guard<std::mutex> lk(mu);
-    Pool& p = pools[dev];
-    if (!p.fork) {
-        for (int i = 0; i < kRunStreams; ++i) {
-            THESIA_HIP(hipStreamCreateWithFlags(&p.st[i], hipStreamNonBlocking));
-            THESIA_HIP(hipEventCreateWithFlags(&p.join[i], hipEventDisableTiming));
-        }
-        THESIA_HIP(hipEventCreateWithFlags(&p.fork, hipEventDisableTiming));
-    }
-    const int k = (int)std::min<size_t>(kRunStreams, n);
-    THESIA_HIP(hipEventRecord(p.fork, s));
-    for (int i = 0; i < k; ++i) THESIA_HIP(hipStreamWaitEvent(p.st[i], p.fork, 0));
-    int rc = THESIA_OK;
-    for (size_t i = 0; i < n && !rc; ++i) rc = batch_run(b[i], p.st[i % k]);
-    for (int i = 0; i < k; ++i) {  // join even after an error: `s` never runs ahead of them
-        THESIA_HIP(hipEventRecord(p.join[i], p.st[i]));
-        THESIA_HIP(hipStreamWaitEvent(s, p.join[i], 0));
-    }
-    return rc;
+    std::lock_guard<std::mutex> lk(run_pool_mutex());
+    RunPool* p = nullptr;
+    int rc = run_pool(&p);
+    if (rc) return rc;
+    const int k = (int)std::min<size_t>(RunPool::kStreams, n);
+    THESIA_HIP(p->fork_from(s, k));
+    for (size_t i = 0; i < n && !rc; ++i) rc = batch_run(b[i], p->st[i % k]);
+    const int jrc = p->join_into(s, k);  // join even after an error: `s` never runs ahead of them
+    return rc ? rc : jrc;
 }
 
 // host side of Batch::range: {ord max, ord min, NaN} -> (max, min, NaN) per track
@@ -1289,6 +1313,12 @@ int render_rgb_fused(size_t n_groups, const float* const* d_specs, const uint64_
     size_t ntr = 0;
     const int rpath = render_path();
     put(&rpath, sizeof rpath);
+    // groups in flight at once (THESIA_RENDER_STREAMS, 1..4; default 4)
+    static const int nst = [] {
+        const char* e = std::getenv("THESIA_RENDER_STREAMS");
+        const int v = e ? std::atoi(e) : RunPool::kStreams;
+        return v < 1 ? 1 : v > RunPool::kStreams ? RunPool::kStreams : v;
+    }();
     put(&n_groups, sizeof n_groups);
     put(&nheight, sizeof nheight);
     put(&d_rgb, sizeof d_rgb);
@@ -1317,15 +1347,23 @@ int render_rgb_fused(size_t n_groups, const float* const* d_specs, const uint64_
         ws.key.clear();
         std::vector<RenderDesc> desc;
         std::vector<FusedGroup> groups(n_groups);
-        uint64_t tmp_max = 1;
         size_t t0 = 0;
         for (size_t k = 0; k < n_groups; ++k) {
             rc = plan_fused_group(d_specs[k], row0s[k], bins[k], ns[k], up_ratio + t0, nwidth + t0, nheight,
                                   rgb_off + t0, desc, groups[k], true);
             if (rc) return rc;
-            tmp_max = std::max<uint64_t>(tmp_max, groups[k].tmp_tot);
             t0 += ns[k];
         }
+        // the groups run on nst streams (group k on stream k % nst): each stream's groups share
+        // an intermediate region of the largest of them, the regions side by side
+        std::vector<uint64_t> slot(nst, 0);
+        for (size_t k = 0; k < n_groups; ++k) slot[k % nst] = std::max(slot[k % nst], groups[k].tmp_tot);
+        std::vector<uint64_t> slot0(nst, 0);
+        for (int i = 1; i < nst; ++i) slot0[i] = slot0[i - 1] + slot[i - 1];
+        const uint64_t tmp_max = std::max<uint64_t>(1, slot0[nst - 1] + slot[nst - 1]);
+        for (size_t k = 0; k < n_groups; ++k)
+            for (size_t i = groups[k].desc0; i < groups[k].desc0 + groups[k].ndesc; ++i)
+                desc[i].tmp_off += slot0[k % nst];
         auto grow = [](DevBuf& b, size_t bytes) {
             if (b.bytes >= bytes && b.p) return 0;
             b.release();
@@ -1347,17 +1385,31 @@ int render_rgb_fused(size_t n_groups, const float* const* d_specs, const uint64_
     // the horizontal pass: LDS-DMA row staging (display_kernels.hip resize_h_dma_kernel; the
     // register-staged pass of the three-stage path where a span does not fit)
     const bool h_dma = true;
-    for (const FusedGroup& g : groups)
+    auto launch_group = [&](const FusedGroup& g, hipStream_t st) {
         for (size_t b = 0; b < g.ndesc; b += 65535) {  // grid.z limit
             const uint32_t nb = (uint32_t)std::min<size_t>(65535, g.ndesc - b);
             if (launch_render_batch2(g.spec, g.bins, max, min, ws.desc.as<RenderDesc>() + g.desc0 + b, nb,
                                      g.T_max, g.H_max, g.nw_max, nheight, g.h_taps, g.h_span, g.v_band,
-                                     g.v_rows, g.v_kv, ws.tmp.as<float>(), cmap_ptr, d_rgb, s, h_dma,
+                                     g.v_rows, g.v_kv, ws.tmp.as<float>(), cmap_ptr, d_rgb, st, h_dma,
                                      g.v_fpl))
                 return set_error(THESIA_ERR_DEVICE, "render batch launch failed");
         }
+        return THESIA_OK;
+    };
+    const int k = (int)std::min<size_t>(nst, groups.size());
+    if (k <= 1) {
+        for (const FusedGroup& g : groups)
+            if ((rc = launch_group(g, s))) return rc;
+        return THESIA_OK;
+    }
+    std::lock_guard<std::mutex> plk(run_pool_mutex());
+    RunPool* p = nullptr;
+    if ((rc = run_pool(&p))) return rc;
+    THESIA_HIP(p->fork_from(s, k));
+    for (size_t i = 0; i < groups.size() && !rc; ++i) rc = launch_group(groups[i], p->st[i % nst]);
+    const int jrc = p->join_into(s, k);
     // stream-ordered: the images are complete for every later library call (copies included)
-    return THESIA_OK;
+    return rc ? rc : jrc;
 }
 
 // InvRealFFT (realfft.rs:167-241) over device buffers: the length's tables come from a Plan
