@@ -1205,6 +1205,8 @@ struct FusedGroup {
     uint32_t T_max = 0, H_max = 0, nw_max = 0, v_band = 1;
     int h_taps = 0, h_span = 0, v_rows = 1, v_kv = 4;
     int v_fpl = 1;  // frames per lane of the vertical pass (4: grey_vert_wide_kernel)
+    uint64_t cost = 0;  // HBM floats its two passes move (spectrogram, intermediate twice, RGB / 4)
+    int stream = 0;     // render_rgb_fused: the library stream it runs on
 };
 
 // Host planning of one group: a RenderDesc per non-empty track (appended to `desc`), the
@@ -1246,6 +1248,7 @@ int plan_fused_group(const float* d_spec, const uint64_t* row0, size_t bins, siz
         r.oz = oz;
         if (std::find(vts.begin(), vts.end(), std::make_pair(vt, oz)) == vts.end()) vts.emplace_back(vt, oz);
         g.tmp_tot += (uint64_t)r.ts * nheight;
+        g.cost += (uint64_t)T * bins + 2ull * r.ts * nheight + (3ull * nwidth[i] * nheight) / 4;
         g.h_taps = std::max(g.h_taps, ht->max_taps);
         g.h_span = std::max<int>(g.h_span, (int)((256.0 * T + nwidth[i] - 1) / nwidth[i]) + ht->max_taps + 8);
         g.T_max = std::max(g.T_max, T);
@@ -1354,16 +1357,26 @@ int render_rgb_fused(size_t n_groups, const float* const* d_specs, const uint64_
             if (rc) return rc;
             t0 += ns[k];
         }
-        // the groups run on nst streams (group k on stream k % nst): each stream's groups share
-        // an intermediate region of the largest of them, the regions side by side
-        std::vector<uint64_t> slot(nst, 0);
-        for (size_t k = 0; k < n_groups; ++k) slot[k % nst] = std::max(slot[k % nst], groups[k].tmp_tot);
-        std::vector<uint64_t> slot0(nst, 0);
+        // the groups run on nst streams, the largest first, each to the least loaded stream
+        // (by the HBM floats it moves); a stream's groups share an intermediate region of the
+        // largest of them, the regions side by side; ws.groups in launch order
+        std::vector<size_t> ord(n_groups);
+        for (size_t k = 0; k < n_groups; ++k) ord[k] = k;
+        std::stable_sort(ord.begin(), ord.end(), [&](size_t a, size_t b) { return groups[a].cost > groups[b].cost; });
+        std::vector<uint64_t> load(nst, 0), slot(nst, 0), slot0(nst, 0);
+        for (size_t k : ord) {
+            const int i = (int)(std::min_element(load.begin(), load.end()) - load.begin());
+            groups[k].stream = i;
+            load[i] += groups[k].cost;
+            slot[i] = std::max(slot[i], groups[k].tmp_tot);
+        }
         for (int i = 1; i < nst; ++i) slot0[i] = slot0[i - 1] + slot[i - 1];
         const uint64_t tmp_max = std::max<uint64_t>(1, slot0[nst - 1] + slot[nst - 1]);
-        for (size_t k = 0; k < n_groups; ++k)
-            for (size_t i = groups[k].desc0; i < groups[k].desc0 + groups[k].ndesc; ++i)
-                desc[i].tmp_off += slot0[k % nst];
+        for (const FusedGroup& g : groups)
+            for (size_t i = g.desc0; i < g.desc0 + g.ndesc; ++i) desc[i].tmp_off += slot0[g.stream];
+        std::vector<FusedGroup> sorted;
+        for (size_t k : ord) sorted.push_back(groups[k]);
+        groups = std::move(sorted);
         auto grow = [](DevBuf& b, size_t bytes) {
             if (b.bytes >= bytes && b.p) return 0;
             b.release();
@@ -1406,7 +1419,7 @@ int render_rgb_fused(size_t n_groups, const float* const* d_specs, const uint64_
     RunPool* p = nullptr;
     if ((rc = run_pool(&p))) return rc;
     THESIA_HIP(p->fork_from(s, k));
-    for (size_t i = 0; i < groups.size() && !rc; ++i) rc = launch_group(groups[i], p->st[i % nst]);
+    for (size_t i = 0; i < groups.size() && !rc; ++i) rc = launch_group(groups[i], p->st[groups[i].stream]);
     const int jrc = p->join_into(s, k);
     // stream-ordered: the images are complete for every later library call (copies included)
     return rc ? rc : jrc;
