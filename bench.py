@@ -482,7 +482,8 @@ def main_c5(args, ws, rank, pg, device):
     engine.synchronize()
     dt_host = max_over_ranks(pg, (time.perf_counter() - t0) / 3)
     # spectrogram kernels alone (HIP events per group launch)
-    kms = sum(b.run_timed(3) / 3 for _, _, _, b in p.groups)
+    kms_batches = [(pl.n_fft, b.total_frames, b.run_timed(3) / 3) for pl, _, _, b in p.groups]
+    kms = sum(t for _, _, t in kms_batches)
     # the step's spectrogram phase as it runs: the batches overlapped on the library streams
     engine.synchronize()
     p.run_spectrograms()
@@ -530,6 +531,7 @@ def main_c5(args, ws, rank, pg, device):
                          "kernel_ms": kms, "algorithmic_bytes_per_launch": in_bytes + out_bytes,
                          "kernel_ms_note": "sum of the batches' launches, each timed alone",
                          "overlapped_ms": kms_overlap,
+                         "per_batch": [{"n_fft": nf, "frames": fr, "kernel_ms": t} for nf, fr, t in kms_batches],
                          "overlapped_note": "the step's spectrogram phase: the batches on the library "
                                             "streams (thesia_batches_run), HIP events on the library stream"},
             "roofline_display": disp,
