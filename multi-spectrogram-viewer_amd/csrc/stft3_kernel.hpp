@@ -166,6 +166,11 @@ stft3_kernel(StftLaunch a, uint64_t fps) {
         int jc = j;  // the frame's column (HQ > 0): (j - frame start in points) mod L
         if constexpr (VIEW) {
             if (valid) jc = (j - (int)((st >> 1) & (L - 1))) & (L - 1);
+        } else {
+            // opaque per frame here too: the addresses derived from the column are then formed
+            // per frame instead of hoisted as loop invariants (which spilled 21-65 VGPRs at
+            // NC 512 / 1024; the viewer instances, whose column varies, never did)
+            asm volatile("" : "+v"(jc));
         }
         int wj = jc;
         asm volatile("" : "+v"(wj));
