@@ -40,13 +40,13 @@ stft2_kernel(StftLaunch a, uint64_t tiles_per_block) {
     float* wtab = lds;
     float* work = lds + G::WIN_FLOATS;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    const int slot = lane / L, j = lane % L;
-    const int partner = slot * L + ((L - j) % L);
+    const int slot = lane / L, j0 = lane % L;
+    const int partner0 = slot * L + ((L - j0) % L);
 
     for (int i = threadIdx.x; i < 2 * NC; i += kBlock) wtab[i] = a.wpad[i] * 0.5f;  // exact
     float2 ub[G::CPL];  // untangle bases (sin, cos)(pi (j + cL) / NC), realfft.rs:88-93
 #pragma unroll
-    for (int c = 0; c < G::CPL; ++c) ub[c] = a.sincos[j + c * L];
+    for (int c = 0; c < G::CPL; ++c) ub[c] = a.sincos[j0 + c * L];
     __syncthreads();
 
     const uint64_t total = a.total_frames;
@@ -67,6 +67,10 @@ stft2_kernel(StftLaunch a, uint64_t tiles_per_block) {
         // loop instead of hoisted (and spilled) as loop invariants
 #pragma unroll
         for (int c = 0; c < G::CPL; ++c) asm volatile("" : "+v"(ub[c].x), "+v"(ub[c].y));
+        // the lane's column and partner opaque per pass too: the addresses derived from them
+        // are formed per pass instead of hoisted (the complex / NC 512-1024 instances spilled)
+        int j = j0, partner = partner0;
+        asm volatile("" : "+v"(j), "+v"(partner));
         float2 v[P];
         if (valid) {
             hint = find_track(a.trk_frame0, a.n_tracks, g, hint);
