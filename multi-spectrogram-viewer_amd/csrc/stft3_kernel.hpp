@@ -41,7 +41,8 @@ namespace thesia {
 // frames (stream 2s takes frames g, g + 2, ..., 2s + 1 the ones between), so a stream's hop is
 // 2 hop samples = HQ L + rem points, and a frame starting at an odd sample reads the track on
 // the point grid shifted by one sample (base + C elements): the same ring, on that grid. Its
-// vector loads are then only dword-aligned (f32, or s16 stereo). Complex rows are stored per row
+// vector loads are then only dword-aligned (f32, s16 stereo) or, for int16 mono, 2-byte-aligned
+// (a sample pair straddling two dwords). Complex rows are stored per row
 // (a stream's rows are not contiguous).
 template <int NC, int OK, int C, int INF, int VAR = 0, int WV = kWaves, int HQ = 0, int VODD = 0>
 __global__ void __launch_bounds__(64 * WV, WV / 4)
@@ -56,7 +57,9 @@ stft3_kernel(StftLaunch a, uint64_t fps) {
     constexpr int P = G::P, L = G::L, FPW = G::FPW, F = G::F, SH = G3::SH;
     constexpr bool VIEW = HQ > 0;
     constexpr bool ODD = VODD != 0;
-    static_assert(!ODD || (VIEW && !line_rows(OK, VAR) && !(C == 1 && INF == IN_S16)), "odd-hop streams");
+    static_assert(!ODD || (VIEW && !line_rows(OK, VAR)), "odd-hop streams");
+    // odd-hop vector loads: dword-aligned, or 2-byte-aligned for int16 mono (a sample pair)
+    constexpr int OALIGN = C == 1 && INF == IN_S16 ? 2 : 4;
     constexpr int NPRE = VIEW ? HQ + 1 : SH;  // rows prefetched per frame
     constexpr int KEEP = P - NPRE;            // ring rows carried into the next frame
     static_assert(KEEP > 0, "hop shorter than the frame");
@@ -176,15 +179,15 @@ stft3_kernel(StftLaunch a, uint64_t fps) {
         asm volatile("" : "+v"(wj));
         const float4* wrow = reinterpret_cast<const float4*>(wtl + wj * G3::WL_STRIDE);
         // the vector loads of a frame at element offset e: naturally aligned (CT = 2 samples x C
-        // channels), or on ODD grids dword-aligned (4-byte-aligned memcpy loads; s16 tracks at an
-        // odd element offset take the generic loader)
+        // channels), or on ODD grids OALIGN-aligned memcpy loads (dword: f32, s16 stereo at an even
+        // element offset, else the generic loader; int16 mono: 2-byte, every offset)
         auto aligned = [&](uint64_t e) {
-            return ODD ? (e * sizeof(ET)) % 4 == 0 : e % (2 * C) == 0;
+            return ODD ? (e * sizeof(ET)) % OALIGN == 0 : e % (2 * C) == 0;
         };
         auto ldc = [](const CT* p) -> CT {
             if constexpr (ODD) {
                 CT v;
-                __builtin_memcpy(&v, __builtin_assume_aligned(p, 4), sizeof(CT));
+                __builtin_memcpy(&v, __builtin_assume_aligned(p, C == 1 && INF == IN_S16 ? 2 : 4), sizeof(CT));
                 return v;
             } else {
                 return *p;

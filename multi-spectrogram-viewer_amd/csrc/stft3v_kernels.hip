@@ -10,7 +10,7 @@
 // odd frames on the point grid shifted by one sample):
 //   44.1 kHz  1764 / 441 / 2048: NC 1024, L 32, 441 points a stream hop = 13 rows + 25
 //   22.05 kHz  884 / 221 / 1024: NC  512, L 16, 221 points = 13 rows + 13
-// (odd hops need dword-aligned vector loads at every sample: f32, or s16 stereo). Any geometry
+// (odd hops: vector loads at every sample, dword-aligned or, int16 mono, 2-byte). Any geometry
 // with an even win <= n_fft and one of these row counts runs here.
 #include "stft3_kernel.hpp"
 
@@ -64,7 +64,7 @@ int launch3v_nc(const StftLaunch& a, hipStream_t s) {
 template <int NC, int HQ>
 int launch3v_nc_odd(const StftLaunch& a, hipStream_t s) {
     if (a.in_format == IN_S16)
-        return a.channels == 2 ? launch3v_c<NC, HQ, 2, IN_S16, 1>(a, s) : -2;
+        return a.channels == 2 ? launch3v_c<NC, HQ, 2, IN_S16, 1>(a, s) : launch3v_c<NC, HQ, 1, IN_S16, 1>(a, s);
     return a.channels == 2 ? launch3v_c<NC, HQ, 2, IN_F32, 1>(a, s) : launch3v_c<NC, HQ, 1, IN_F32, 1>(a, s);
 }
 
@@ -89,7 +89,7 @@ bool stft3v_supports(int n_fft, int win, int hop, int in_format, int channels) {
     // n_fft / 2, i.e. an even win (lib.rs:400-401); the canonical geometry is stft3's own
     return view_rows(n_fft, hop) > 0 && win <= n_fft && win % 2 == 0 && win >= 2 &&
            !(win == n_fft && hop * 4 == n_fft) && (in_format == IN_F32 || in_format == IN_S16) &&
-           (channels == 1 || channels == 2) && !(hop % 2 && in_format == IN_S16 && channels == 1);
+           (channels == 1 || channels == 2);
 }
 
 int stft3v_lds_bytes(const StftLaunch& a) {

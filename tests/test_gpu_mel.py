@@ -166,12 +166,17 @@ def test_kernel_choice_and_unsupported_force():
     with pytest.raises(thesia.ThesiaError):
         b.set_option(engine.OPT_KERNEL, 5)  # stft5: the canonical geometry only
     plan = engine.Plan(2048, 1764, 441, engine.OUT_AMP_DB)  # 44.1 kHz viewer geometry: odd hop,
-    x16 = np.zeros(4096, np.int16)                          # s16 mono: not dword-aligned -> stft2
+    x16 = np.zeros(4096, np.int16)                          # s16 mono (2-byte-aligned loads) streams
     din = engine.DeviceBuffer.from_host(x16)
     dout = engine.DeviceBuffer(engine.Batch.frames_for(plan, [4096]) * plan.row_bins * 4)
     b = engine.Batch(plan, din, [0], [4096], dout, input_format=engine.IN_S16)
+    assert b.kernel == 3
+    with pytest.raises(thesia.ThesiaError):
+        b.set_option(engine.OPT_KERNEL, 5)
+    plan = engine.Plan(2048, 1763, 441, engine.OUT_AMP_DB)  # odd win: no streaming start rule
+    dout = engine.DeviceBuffer(engine.Batch.frames_for(plan, [4096]) * plan.row_bins * 4)
+    b = engine.Batch(plan, din, [0], [4096], dout, input_format=engine.IN_S16)
     assert b.kernel == 2
-    import thesia
     with pytest.raises(thesia.ThesiaError):
         b.set_option(engine.OPT_KERNEL, 3)
     with pytest.raises(thesia.ThesiaError):

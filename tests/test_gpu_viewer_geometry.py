@@ -81,9 +81,9 @@ def test_viewer_geometry_complex_streams(n_fft, win, hop, channels, fmt, gap):
     plan = engine.Plan(n_fft, win, hop, engine.OUT_COMPLEX)
     k, rows = _run(plan, tracks, channels, fmt, gap, row_floats=2 * plan.row_bins)
     plan.close()
-    # the streaming kernel is the automatic choice at this geometry (odd hops: not for s16 mono,
-    # whose 2-byte samples give vector loads below dword alignment on the shifted grid)
-    assert k == (2 if hop % 2 and fmt == engine.IN_S16 and channels == 1 else 3)
+    # the streaming kernel is the automatic choice at this geometry (odd hops with s16 mono too:
+    # 2-byte-aligned sample-pair loads on the shifted grid)
+    assert k == 3
     for t, r in zip(tracks, rows):
         ref = O.perform_stft(_x(t, fmt), win, hop, n_fft)
         got = r.view(np.complex64).reshape(ref.shape)
@@ -131,7 +131,7 @@ def test_viewer_geometry_linear_kinds(n_fft, win, hop, kind, max_blocks):
 def test_viewer_geometry_mel_db(n_fft, win, hop, sr, n_mels):
     rng = np.random.default_rng(n_fft + n_mels + sr)
     lens = [win - 1, 4 * n_fft + 5, 71 * hop + 3]
-    fmt = engine.IN_F32 if hop % 2 else engine.IN_S16
+    fmt = engine.IN_S16
     tracks = _tracks(rng, lens, 1, fmt)
     plan = engine.Plan(n_fft, win, hop, engine.OUT_MEL_AMP_DB, sr=sr, n_mels=n_mels)
     k, rows = _run(plan, tracks, 1, fmt, 0, max_blocks=2)
