@@ -299,6 +299,10 @@ int thesia_render_rgb_batch_device(const float* d_spec, const uint64_t* row0, si
 int thesia_minmax_segments_multi(size_t n_groups, const float* const* d_specs,
                                  const uint64_t* const* row0s, const size_t* bins, const size_t* ns,
                                  float* max, float* min, int* has_nan);
+/* render_rgb_multi runs its groups concurrently on the library's stream pool (largest first;
+ * THESIA_RENDER_STREAMS=1 in the environment keeps them serial), still stream-ordered on the
+ * library stream as a whole: the tracks' RGB ranges (rgb_off, nwidth x nheight x 3 bytes) must
+ * not overlap, as two tracks writing the same bytes would race. */
 int thesia_render_rgb_multi(size_t n_groups, const float* const* d_specs, const uint64_t* const* row0s,
                             const size_t* bins, const size_t* ns, const float* up_ratio,
                             const uint32_t* nwidth, uint32_t nheight, float max, float min,
