@@ -1348,6 +1348,15 @@ int render_rgb_fused(size_t n_groups, const float* const* d_specs, const uint64_
     Ws& ws = ws_map[dev];
     if (ws.key != key) {
         ws.key.clear();
+        {  // the tracks' RGB ranges are written concurrently: they must not overlap
+            std::vector<std::pair<uint64_t, uint64_t>> rr;
+            for (size_t i = 0; i < ntr; ++i)
+                if (nwidth[i]) rr.emplace_back(rgb_off[i], rgb_off[i] + (uint64_t)nwidth[i] * nheight * 3);
+            std::sort(rr.begin(), rr.end());
+            for (size_t i = 1; i < rr.size(); ++i)
+                if (rr[i].first < rr[i - 1].second)
+                    return set_error(THESIA_ERR_INVALID_ARG, "render: two tracks' RGB ranges overlap");
+        }
         std::vector<RenderDesc> desc;
         std::vector<FusedGroup> groups(n_groups);
         size_t t0 = 0;

@@ -151,3 +151,25 @@ def test_render_pinned_readback_matches_pageable():
         finally:
             p.close()
     assert outs[0] == outs[1]
+
+
+def test_render_rejects_overlapping_rgb_ranges():
+    """render_rgb_multi runs its groups concurrently: two tracks whose RGB ranges overlap would
+    race, so the call is refused (thesia.h) instead of leaving either image."""
+    import ctypes as C
+    from thesia._lib import lib, _fp, _u64p
+    p = pipeline.RenderPipeline(pipeline.c5_tracks(6, seconds=0.5), px_per_sec=50.0, nheight=64)
+    try:
+        p.run_spectrograms()
+        p.render(want_rgb=False)
+        up = next(iter(p._up.values()))
+        off = p._off.copy()
+        args = lambda o: (p._n_disp, p._c_specs, p._c_row0, p._c_bins, p._c_ns, up.ctypes.data_as(_fp),
+                          p._nw.ctypes.data_as(C.POINTER(C.c_uint32)), p.nheight, 0.0, -100.0,
+                          p._rgb.ptr, o.ctypes.data_as(_u64p))
+        assert lib.thesia_render_rgb_multi(*args(off)) == 0
+        off[1] = off[0] + 1
+        assert lib.thesia_render_rgb_multi(*args(off)) != 0
+        assert "overlap" in lib.thesia_last_error().decode()
+    finally:
+        p.close()
