@@ -618,11 +618,22 @@ int thesia_mt_add_tracks(thesia_mt* mt, const uint64_t* ids, size_t n_ids, const
     std::vector<WavData> wavs(n);
     std::vector<uint64_t> idv(ids, ids + n);
     std::vector<PcmIn> pcm(n);
+    // the files are read straight into the handle's page-locked staging (one read per file, no
+    // copy of the samples on the host; the uploads then run as DMA), sized from the files
+    std::vector<size_t> fsz(n, 0), foff(n + 1, 0);
     for (size_t i = 0; i < n; ++i) {
         std::string err;
-        int rc = read_wav(pl[i], &wavs[i], &err);
+        int rc = wav_file_size(pl[i], &fsz[i], &err);
         if (rc) return set_error(rc, err);
-        pcm[i].data = wavs[i].raw.data();
+        foff[i + 1] = foff[i] + ((fsz[i] + 63) & ~size_t(63));
+    }
+    uint8_t* stage = M(mt)->staging(foff[n]);
+    for (size_t i = 0; i < n; ++i) {
+        std::string err;
+        int rc = stage && fsz[i] ? read_wav_into(pl[i], stage + foff[i], fsz[i], &wavs[i], &err)
+                                 : read_wav(pl[i], &wavs[i], &err);
+        if (rc) return set_error(rc, err);
+        pcm[i].data = wavs[i].samples();
         pcm[i].kind = wavs[i].kind;
         pcm[i].scale = pcm_scale(wavs[i].kind, wavs[i].bits);
         pcm[i].channels = wavs[i].channels;
@@ -746,7 +757,7 @@ int thesia_open_audio_file(const char* path, float* out, size_t cap, size_t* n_f
     if (channels) *channels = w.channels;
     if (!out) return THESIA_OK;
     if (cap < n) return set_error(THESIA_ERR_BUFFER_TOO_SMALL, "sample buffer too small");
-    decode_pcm_f32(w.raw.data(), w.kind, pcm_scale(w.kind, w.bits), n, out);
+    decode_pcm_f32(w.samples(), w.kind, pcm_scale(w.kind, w.bits), n, out);
     return THESIA_OK;
     GUARD_END
 }

@@ -17,6 +17,23 @@ MultiTrack::MultiTrack() = default;
 
 MultiTrack::~MultiTrack() {
     for (auto& kv : plans_) delete kv.second;
+    if (stage_) (void)hipHostFree(stage_);
+}
+
+uint8_t* MultiTrack::staging(size_t bytes) {
+    // an add_tracks that failed after enqueuing its uploads returned before its synchronisation:
+    // its copies may still read the staging (the stream is idle otherwise)
+    if (hipStreamSynchronize(default_stream()) != hipSuccess) return nullptr;
+    if (bytes <= stage_bytes_) return stage_;
+    if (stage_) (void)hipHostFree(stage_);
+    stage_ = nullptr;
+    stage_bytes_ = 0;
+    const size_t want = bytes + bytes / 4;  // headroom: a session adds files of similar sizes
+    void* p = nullptr;
+    if (hipHostMalloc(&p, want, hipHostMallocDefault) != hipSuccess) return nullptr;
+    stage_ = static_cast<uint8_t*>(p);
+    stage_bytes_ = want;
+    return stage_;
 }
 
 int MultiTrack::set_setting(float win_ms, size_t t_overlap, size_t f_overlap, int freq_scale,

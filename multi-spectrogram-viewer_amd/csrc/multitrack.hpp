@@ -72,6 +72,9 @@ class MultiTrack {
     size_t size() const { return tracks_.size(); }
     // device bytes the tracks hold: their wav / spectrogram buffers (shared ones once) and greys
     size_t device_bytes() const;
+    // page-locked host staging for add_tracks' file reads (grow-only, this handle's; free again
+    // once add_tracks returns, which synchronises its uploads): nullptr if it cannot be had
+    uint8_t* staging(size_t bytes);
 
   private:
     int make_plan(const Track& tr, Plan** out) const;
@@ -85,6 +88,8 @@ class MultiTrack {
     uint64_t id_max_sec_ = 0;
     uint32_t max_sr_ = 0;
     DevBuf img_;  // image scratch (grow-only)
+    uint8_t* stage_ = nullptr;  // hipHostMalloc'd, stage_bytes_
+    size_t stage_bytes_ = 0;
 };
 
 }  // namespace thesia

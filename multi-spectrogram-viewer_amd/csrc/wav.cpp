@@ -38,25 +38,79 @@ void decode_pcm_f32(const uint8_t* raw, int kind, float scale, uint64_t n, float
     }
 }
 
+static int io_error(std::string* err) {
+    const int e = errno;
+    *err = std::string(std::strerror(e)) + " (os error " + std::to_string(e) + ")";
+    return THESIA_ERR_IO;
+}
+
+int wav_file_size(const std::string& path, size_t* size, std::string* err) {
+    FILE* f = std::fopen(path.c_str(), "rb");
+    if (!f) return io_error(err);
+    long sz = -1;
+    if (std::fseek(f, 0, SEEK_END) == 0) sz = std::ftell(f);
+    std::fclose(f);
+    *size = sz > 0 ? (size_t)sz : 0;
+    return THESIA_OK;
+}
+
+int read_wav_into(const std::string& path, uint8_t* dst, size_t cap, WavData* out, std::string* err) {
+    FILE* f = std::fopen(path.c_str(), "rb");
+    if (!f) return io_error(err);
+    size_t len = 0;
+    while (len < cap) {
+        const size_t n = std::fread(dst + len, 1, cap - len, f);
+        if (n == 0) break;
+        len += n;
+    }
+    uint8_t probe;
+    const bool more = len == cap && std::fread(&probe, 1, 1, f) == 1;
+    std::fclose(f);
+    if (more) return read_wav(path, out, err);  // the file grew since it was sized
+    return parse_wav(dst, len, out, err);
+}
+
 int read_wav(const std::string& path, WavData* out, std::string* err) {
     FILE* f = std::fopen(path.c_str(), "rb");
-    if (!f) {
-        const int e = errno;
-        *err = std::string(std::strerror(e)) + " (os error " + std::to_string(e) + ")";
-        return THESIA_ERR_IO;
-    }
-    std::vector<uint8_t> buf;
+    if (!f) return io_error(err);
+    // one read into an uninitialised buffer of the file's size (growing only if the file grew)
+    size_t cap = 0, len = 0;
     if (std::fseek(f, 0, SEEK_END) == 0) {
         const long sz = std::ftell(f);
-        if (sz > 0) buf.reserve((size_t)sz);
+        if (sz > 0) cap = (size_t)sz;
         std::fseek(f, 0, SEEK_SET);
     }
-    {
-        uint8_t tmp[1 << 16];
-        size_t n;
-        while ((n = std::fread(tmp, 1, sizeof(tmp), f)) > 0) buf.insert(buf.end(), tmp, tmp + n);
+    std::unique_ptr<uint8_t[]> file(new uint8_t[std::max<size_t>(cap, 1)]);
+    while (true) {
+        if (len == cap) {  // full: at the end, or the size was unknown / the file grew
+            uint8_t probe;
+            if (std::fread(&probe, 1, 1, f) == 0) break;
+            const size_t ncap = std::max<size_t>(2 * cap, 1 << 16);
+            std::unique_ptr<uint8_t[]> nf(new uint8_t[ncap]);
+            if (len) std::memcpy(nf.get(), file.get(), len);
+            file = std::move(nf);
+            cap = ncap;
+            file[len++] = probe;
+        }
+        const size_t n = std::fread(file.get() + len, 1, cap - len, f);
+        len += n;
+        if (n == 0) break;
     }
     std::fclose(f);
+    const int rc = parse_wav(file.get(), len, out, err);
+    if (rc) return rc;
+    out->file = std::move(file);
+    out->file_len = len;
+    return THESIA_OK;
+}
+
+int parse_wav(const uint8_t* file, size_t len, WavData* out, std::string* err) {
+    struct View {
+        const uint8_t* p;
+        size_t n;
+        size_t size() const { return n; }
+        const uint8_t* data() const { return p; }
+    } buf{file, len};
     if (buf.size() < 12 || std::memcmp(buf.data(), "RIFF", 4) || std::memcmp(buf.data() + 8, "WAVE", 4)) {
         *err = "not a WAV file: the reference's rodio fallback (FLAC/Vorbis) is not supported";
         return THESIA_ERR_UNSUPPORTED;
@@ -116,7 +170,8 @@ int read_wav(const std::string& path, WavData* out, std::string* err) {
     out->kind = kind;
     // audio.rs:32-34: truncate to whole frames
     out->n_frames = (data_len / bps) / channels;
-    out->raw.assign(data, data + out->n_frames * channels * bps);
+    out->data_off = (size_t)(data - file);
+    out->base = file;
     return THESIA_OK;
 }
 
