@@ -6,6 +6,8 @@
 #include <cstring>
 #include <new>
 #include <string>
+#include <atomic>
+#include <thread>
 #include <vector>
 
 #include "../../include/thesia.h"
@@ -628,11 +630,28 @@ int thesia_mt_add_tracks(thesia_mt* mt, const uint64_t* ids, size_t n_ids, const
         foff[i + 1] = foff[i] + ((fsz[i] + 63) & ~size_t(63));
     }
     uint8_t* stage = M(mt)->staging(foff[n]);
+    // the files read concurrently (the reference's per-track rayon loop, lib.rs:161-166, reads
+    // and transforms each track on its own worker); errors reported in list order
+    std::vector<int> rcs(n, 0);
+    std::vector<std::string> errs(n);
+    auto read_one = [&](size_t i) {
+        rcs[i] = stage && fsz[i] ? read_wav_into(pl[i], stage + foff[i], fsz[i], &wavs[i], &errs[i])
+                                 : read_wav(pl[i], &wavs[i], &errs[i]);
+    };
+    const size_t nthr = std::min<size_t>(n, std::max(1u, std::min(8u, std::thread::hardware_concurrency())));
+    if (nthr <= 1) {
+        for (size_t i = 0; i < n; ++i) read_one(i);
+    } else {
+        std::atomic<size_t> next{0};
+        std::vector<std::thread> pool;
+        for (size_t t = 0; t < nthr; ++t)
+            pool.emplace_back([&] {
+                for (size_t i; (i = next.fetch_add(1)) < n;) read_one(i);
+            });
+        for (auto& th : pool) th.join();
+    }
     for (size_t i = 0; i < n; ++i) {
-        std::string err;
-        int rc = stage && fsz[i] ? read_wav_into(pl[i], stage + foff[i], fsz[i], &wavs[i], &err)
-                                 : read_wav(pl[i], &wavs[i], &err);
-        if (rc) return set_error(rc, err);
+        if (rcs[i]) return set_error(rcs[i], errs[i]);
         pcm[i].data = wavs[i].samples();
         pcm[i].kind = wavs[i].kind;
         pcm[i].scale = pcm_scale(wavs[i].kind, wavs[i].bits);
