@@ -27,6 +27,7 @@ namespace thesia {
 namespace {
 
 constexpr int kXWaves = 4;
+constexpr int kXMagRegs = 17;  // |X| values per lane held in registers (F <= 1088: n_fft <= 2048)
 
 struct Cx {
     float re, im;
@@ -79,8 +80,11 @@ stftx_kernel(StftLaunch a) {
     extern __shared__ __attribute__((aligned(16))) float xs[];
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     Cx* buf = reinterpret_cast<Cx*>(xs) + (size_t)wave * bufl;
-    // the |X| row (mel kinds only: the other kinds' launches carry no room for it)
-    float* mag = xs + (size_t)kXWaves * bufl * 2 + (size_t)wave * ((F + 3) & ~3);
+    // the |X| row (mel kinds): in the frame's own buffer once the untangle has read it (NC <=
+    // kXMagRegs x 64 - 1: the row goes through registers), else a row of its own after the
+    // buffers (the other kinds' launches carry no room for it)
+    float* mag = NC < 64 * kXMagRegs ? reinterpret_cast<float*>(buf)
+                                     : xs + (size_t)kXWaves * bufl * 2 + (size_t)wave * ((F + 3) & ~3);
     const uint64_t g = (uint64_t)blockIdx.x * kXWaves + wave;
     if (g >= a.total_frames) return;  // wave-uniform; no block barrier below
 
@@ -128,8 +132,9 @@ stftx_kernel(StftLaunch a) {
         for (; cur <= NC; cur *= 4) {
             wave_lds_sync();
             const int q = cur / 4, tstride = NC / cur;
+            const int lq = __builtin_ctz((unsigned)q);  // q, cur: powers of two (no divisions)
             for (int b = lane; b < NC / 4; b += 64) {
-                const int row = b / q, j = b - row * q;
+                const int row = b >> lq, j = b & (q - 1);
                 Cx* d = buf + (size_t)row * cur;
                 // rustfft butterfly_4, forward (oracle cfft_tab)
                 const Cx s0 = xmul(d[j + q], tw[j * 1 * tstride]);
@@ -183,9 +188,25 @@ stftx_kernel(StftLaunch a) {
         }
         return;
     }
-    for (int k = lane; k < F; k += 64) {
-        const Cx x = bin(k);
-        mag[k] = exact::hypotf_glibc(x.re, x.im);
+    if (NC < 64 * kXMagRegs) {
+        float mr[kXMagRegs];
+#pragma unroll
+        for (int i = 0; i < kXMagRegs; ++i) {
+            const int k = lane + 64 * i;
+            if (k < F) {
+                const Cx x = bin(k);
+                mr[i] = exact::hypotf_glibc(x.re, x.im);
+            }
+        }
+        wave_lds_sync();  // every lane's untangle reads are done: the buffer takes the row
+#pragma unroll
+        for (int i = 0; i < kXMagRegs; ++i)
+            if (lane + 64 * i < F) mag[lane + 64 * i] = mr[i];
+    } else {
+        for (int k = lane; k < F; k += 64) {
+            const Cx x = bin(k);
+            mag[k] = exact::hypotf_glibc(x.re, x.im);
+        }
     }
     wave_lds_sync();
     // lib.rs:131: out[m] = fma chain over k ascending of |X|[k] * fb[k][m] (the oracle's dot);
@@ -270,8 +291,9 @@ irfftx_kernel(const float2* in, uint64_t n_frames, int NC, const int* xpos, cons
         for (; cur <= NC; cur *= 4) {
             wave_lds_sync();
             const int q = cur / 4, tstride = NC / cur;
+            const int lq = __builtin_ctz((unsigned)q);  // q, cur: powers of two (no divisions)
             for (int b = lane; b < NC / 4; b += 64) {
-                const int row = b / q, j = b - row * q;
+                const int row = b >> lq, j = b & (q - 1);
                 Cx* d = buf + (size_t)row * cur;
                 // rustfft butterfly_4, inverse
                 const Cx s0 = xmul(d[j + q], xconj(tw[j * 1 * tstride]));
@@ -316,13 +338,13 @@ int launch_irfftx(const float* in, uint64_t n_frames, int length, const int* xpo
 int stftx_lds_bytes(int n_fft, bool mel) {
     const int NC = n_fft / 2, F = NC + 1;
     const int bufl = (NC + 1 + 3) & ~3;
-    return kXWaves * (bufl * 8 + (mel ? ((F + 3) & ~3) * 4 : 0));
+    return kXWaves * (bufl * 8 + (mel && NC >= 64 * kXMagRegs ? ((F + 3) & ~3) * 4 : 0));
 }
 
 int launch_stftx(const StftLaunch& a, hipStream_t s) {
     if (a.n_fft < 2 || (a.n_fft & (a.n_fft - 1))) return -2;
-    // the |X| row only for the mel kinds: without it a frame's wave takes 8 KiB at n_fft 2048
-    // (16 waves per CU instead of 12)
+    // a separate |X| row only for the mel kinds at n_fft 4096: otherwise a frame's wave takes
+    // 8 KiB at n_fft 2048 (16 waves per CU instead of 12)
     const int lds = stftx_lds_bytes(a.n_fft, a.out_kind == OUT_MEL || a.out_kind == OUT_MEL_AMP_DB);
     if (lds > 163840) return -2;
     auto kern = a.in_format == IN_S16 ? stftx_kernel<IN_S16> : stftx_kernel<IN_F32>;
