@@ -76,7 +76,8 @@ __global__ void __launch_bounds__(64 * kXWaves)
 stftx_kernel(StftLaunch a) {
     const int NC = a.n_fft / 2;
     const int F = NC + 1;
-    const int bufl = (NC + 1 + 3) & ~3;  // complex points (+ buf[NC], realfft.rs:140)
+    const int bufl = (NC + 3) & ~3;  // complex points (realfft.rs:140's buf[NC] = buf[0]: read
+                                     // through the index mod NC below)
     extern __shared__ __attribute__((aligned(16))) float xs[];
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     Cx* buf = reinterpret_cast<Cx*>(xs) + (size_t)wave * bufl;
@@ -153,8 +154,6 @@ stftx_kernel(StftLaunch a) {
         }
     }
     wave_lds_sync();
-    if (lane == 0) buf[NC] = buf[0];  // realfft.rs:140
-    wave_lds_sync();
 
     // ---- realfft untangle (realfft.rs:142-157) and the output kind ----
     const int kind = a.out_kind;
@@ -162,7 +161,7 @@ stftx_kernel(StftLaunch a) {
     auto bin = [&](int k) -> Cx {
         if (k == NC) return Cx{buf[0].re - buf[0].im, 0.0f};
         const float s = sc[k].x, c = sc[k].y;
-        const Cx b = buf[k], r = buf[NC - k];
+        const Cx b = buf[k], r = buf[(NC - k) & (NC - 1)];  // k = 0: buf[NC] = buf[0]
         const float xr = 0.5f * (((b.re + r.re) + c * (b.im + r.im)) - s * (b.re - r.re));
         const float xi = 0.5f * (((b.im - r.im) - s * (b.im + r.im)) - c * (b.re - r.re));
         return Cx{xr, xi};
@@ -337,7 +336,7 @@ int launch_irfftx(const float* in, uint64_t n_frames, int length, const int* xpo
 
 int stftx_lds_bytes(int n_fft, bool mel) {
     const int NC = n_fft / 2, F = NC + 1;
-    const int bufl = (NC + 1 + 3) & ~3;
+    const int bufl = (NC + 3) & ~3;
     return kXWaves * (bufl * 8 + (mel && NC >= 64 * kXMagRegs ? ((F + 3) & ~3) * 4 : 0));
 }
 
