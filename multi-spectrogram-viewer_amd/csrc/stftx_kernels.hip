@@ -214,6 +214,8 @@ stftx_kernel(StftLaunch a) {
     for (int m = lane; m < a.n_mels; m += 64) {
         const int4 bd = a.xmel_band[m];  // {first bin, bins, weight offset}
         float acc = 0.0f;
+        // unrolled: the weight reads (global) of 8 taps issue ahead of their fma chain
+#pragma unroll 8
         for (int t = 0; t < bd.y; ++t) acc = __builtin_fmaf(mag[bd.x + t], a.xmel_w[bd.z + t], acc);
         row[m] = db ? xdb(acc, a.log_amin, 1e-18f, 20.0f) : acc;
     }
