@@ -321,7 +321,9 @@ int thesia_mt_set_setting(thesia_mt* mt, float win_ms, size_t t_overlap, size_t 
                           int freq_scale, float db_range);
 /* add_tracks(id_list, path_list) -> Result<bool, JsValue> -- lib.rs:170-191.
  * paths are '\n'-separated; *changed = "global dB range / max sr changed: refetch all
- * images". On error nothing is added (the reference would leave a half-added state). */
+ * images". On error nothing is added (the reference would leave a half-added state).
+ * The files are read concurrently into a page-locked host buffer the handle keeps (grow-only,
+ * about 1.25x the largest call's total file size; freed by thesia_mt_destroy). */
 int thesia_mt_add_tracks(thesia_mt* mt, const uint64_t* ids, size_t n_ids, const char* paths,
                          int* changed);
 /* WAV files keep their sample encoding up to the device: 8/16/24/32-bit integer or f32 samples
