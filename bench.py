@@ -73,8 +73,9 @@ def parse():
     p.add_argument("--mel-paths", default="", help="A/B of stft5's mel projections (THESIA_BATCH_OPT_MEL_PATH): "
                    "comma list, e.g. 1,2,3 (interleaved rounds, one process)")
     p.add_argument("--row-store", type=int, default=0,
-                   help="complex-output row store of the window+rFFT roofline (THESIA_BATCH_OPT_ROW_STORE: "
-                        "0 lane-wise 8-byte, 1 LDS-staged 16-byte, 2 whole 128-byte lines)")
+                   help="complex-output row store of the window+rFFT roofline (THESIA_BATCH_OPT_ROW_STORE, "
+                        "thesia.h: 0 default = whole 128-byte lines, 1 LDS-staged 16-byte, 2 whole 128-byte "
+                        "lines, 3 lane-wise 8-byte)")
     p.add_argument("--row-stores", default="", help="A/B of the complex-output row stores (comma list, "
                    "interleaved rounds, one process), reported in roofline_window_rfft")
     p.add_argument("--render-path", type=int, default=-1, help="c5: the display launch structure "
@@ -448,9 +449,14 @@ def main_c5(args, ws, rank, pg, device):
 
     total = args.tracks * ws
     gen = pipeline.c5_tracks(total, seconds=0.0)  # geometry only (empty PCM) for the partition
-    costs = [shard.track_cost(int(round(args.seconds * t.sr)), t.n_fft, t.n_fft // 4, t.n_fft)
-             for t in gen]
-    mine = shard.assign_tracks(costs, ws)[rank]
+    # both phases balanced (the display waits for every rank's range: a step pays the slowest
+    # rank of each phase), thesia.shard.assign_tracks_2phase
+    lens = [int(round(args.seconds * t.sr)) for t in gen]
+    max_sr = max(t.sr for t in gen)
+    spec_costs = [shard.track_cost(n, t.n_fft, t.n_fft // 4, t.n_fft) for n, t in zip(lens, gen)]
+    disp_costs = [shard.display_cost(n, t.sr, t.n_fft, t.n_fft // 4, t.n_fft, max_sr, 100.0, 500)
+                  for n, t in zip(lens, gen)]
+    mine = shard.assign_tracks_2phase(spec_costs, disp_costs, ws)[rank]
     tracks = []
     for i in mine:  # the generator is indexed by the global track id
         tracks += pipeline.c5_tracks(1, seconds=args.seconds, first=i, channels=args.channels)

@@ -87,6 +87,23 @@ bool num(napi_env env, napi_value v, double* out) {
     return false;
 }
 
+// a whole number in [0, max] (u32 / usize arguments of the reference); RangeError otherwise
+// (a negative, NaN or huge value cast straight to an unsigned type is undefined behaviour or a
+// huge allocation)
+bool uint_arg(napi_env env, napi_value v, double max, const char* name, double* out) {
+    double d = 0;
+    if (!num(env, v, &d)) return false;
+    if (!(d >= 0) || !(d <= max) || d != (double)(uint64_t)d) {
+        napi_throw_range_error(env, "ERR_ARG", (std::string(name) + ": expected a whole number in [0, " +
+                                                std::to_string((uint64_t)max) + "]").c_str());
+        return false;
+    }
+    *out = d;
+    return true;
+}
+constexpr double kU32Max = 4294967295.0;
+constexpr double kLenMax = 268435456.0;  // 2^28 elements: sizes beyond this are refused up front
+
 bool id_arg(napi_env env, napi_value v, uint64_t* id) {
     double d = 0;
     if (!num(env, v, &d)) return false;
@@ -301,7 +318,9 @@ napi_value MtGetSpecImage(napi_env env, napi_callback_info info) {
     thesia_mt* h = self_handle(env, self);
     uint64_t id = 0;
     double pps = 0, nh = 0;
-    if (!h || !id_arg(env, argv[0], &id) || !num(env, argv[1], &pps) || !num(env, argv[2], &nh)) return nullptr;
+    if (!h || !id_arg(env, argv[0], &id) || !num(env, argv[1], &pps) ||
+        !uint_arg(env, argv[2], kU32Max, "nheight", &nh))
+        return nullptr;
     size_t need = 0;
     int rc = thesia_mt_get_spec_image(h, id, (float)pps, (uint32_t)nh, nullptr, 0, &need);
     if (rc != THESIA_OK && rc != THESIA_ERR_BUFFER_TOO_SMALL) return throw_thesia(env, rc);
@@ -317,8 +336,8 @@ napi_value MtGetWavImage(napi_env env, napi_callback_info info) {
     thesia_mt* h = self_handle(env, self);
     uint64_t id = 0;
     double pps = 0, nh = 0, amin = 0, amax = 0;
-    if (!h || !id_arg(env, argv[0], &id) || !num(env, argv[1], &pps) || !num(env, argv[2], &nh) ||
-        !num(env, argv[3], &amin) || !num(env, argv[4], &amax))
+    if (!h || !id_arg(env, argv[0], &id) || !num(env, argv[1], &pps) ||
+        !uint_arg(env, argv[2], kU32Max, "nheight", &nh) || !num(env, argv[3], &amin) || !num(env, argv[4], &amax))
         return nullptr;
     size_t need = 0;
     int rc = thesia_mt_get_wav_image(h, id, (float)pps, (uint32_t)nh, (float)amin, (float)amax, nullptr, 0, &need);
@@ -407,11 +426,12 @@ napi_value Hann(napi_env env, napi_callback_info info) {
     if (!get_args(env, info, 2, argv, nullptr)) return nullptr;
     double size = 0;
     bool sym = false;
-    if (!num(env, argv[0], &size) || napi_get_value_bool(env, argv[1], &sym) != napi_ok) {
+    if (!uint_arg(env, argv[0], kLenMax, "size", &size)) return nullptr;
+    if (napi_get_value_bool(env, argv[1], &sym) != napi_ok) {
         throw_napi(env, "hann(size: number, symmetric: boolean)");
         return nullptr;
     }
-    std::vector<float> w((size_t)(size > 0 ? size : 0));
+    std::vector<float> w((size_t)size);
     const int rc = thesia_hann(w.size(), sym ? 1 : 0, w.data());
     if (rc != THESIA_OK) return throw_thesia(env, rc);
     return f32_array(env, w.data(), w.size());
@@ -432,7 +452,8 @@ napi_value CalcMelFbDefault(napi_env env, napi_callback_info info) {
     napi_value argv[2];
     if (!get_args(env, info, 2, argv, nullptr)) return nullptr;
     double sr = 0, n_fft = 0;
-    if (!num(env, argv[0], &sr) || !num(env, argv[1], &n_fft)) return nullptr;
+    if (!uint_arg(env, argv[0], kU32Max, "sr", &sr) || !uint_arg(env, argv[1], kLenMax, "n_fft", &n_fft))
+        return nullptr;
     size_t n_mel = 0;
     int rc = thesia_calc_mel_fb_default((uint32_t)sr, (size_t)n_fft, &n_mel, nullptr, 0);
     if (rc != THESIA_OK) return throw_thesia(env, rc);
@@ -449,8 +470,9 @@ napi_value CalcMelFb(napi_env env, napi_callback_info info) {
     double sr = 0, n_fft = 0, n_mel = 0, fmin = 0, fmax = -1;
     bool norm = true;
     napi_valuetype t;
-    if (!num(env, argv[0], &sr) || !num(env, argv[1], &n_fft) || !num(env, argv[2], &n_mel) ||
-        !num(env, argv[3], &fmin) || napi_typeof(env, argv[4], &t) != napi_ok)
+    if (!uint_arg(env, argv[0], kU32Max, "sr", &sr) || !uint_arg(env, argv[1], kLenMax, "n_fft", &n_fft) ||
+        !uint_arg(env, argv[2], 65536.0, "n_mel", &n_mel) || !num(env, argv[3], &fmin) ||
+        napi_typeof(env, argv[4], &t) != napi_ok)
         return nullptr;
     if (t != napi_null && t != napi_undefined && !num(env, argv[4], &fmax)) return nullptr;
     if (napi_get_value_bool(env, argv[5], &norm) != napi_ok) {
@@ -477,8 +499,8 @@ napi_value PerformStft(napi_env env, napi_callback_info info) {
     const float* x = nullptr;
     size_t n = 0;
     double win = 0, hop = 0, n_fft = 0;
-    if (!f32_arg(env, argv[0], &x, &n) || !num(env, argv[1], &win) || !num(env, argv[2], &hop) ||
-        !num(env, argv[3], &n_fft))
+    if (!f32_arg(env, argv[0], &x, &n) || !uint_arg(env, argv[1], kLenMax, "win_length", &win) ||
+        !uint_arg(env, argv[2], kLenMax, "hop_length", &hop) || !uint_arg(env, argv[3], kLenMax, "n_fft", &n_fft))
         return nullptr;
     const float* w = nullptr;
     if (argc > 4) {
@@ -523,37 +545,53 @@ napi_value DeviceCount(napi_env env, napi_callback_info) {
     return js_num(env, n);
 }
 
+// every callback behind a C++ exception barrier: an exception escaping into node (std::bad_alloc
+// from a result vector) would call std::terminate and end the Electron main process
+template <napi_value (*F)(napi_env, napi_callback_info)>
+napi_value Guarded(napi_env env, napi_callback_info info) {
+    try {
+        return F(env, info);
+    } catch (const std::bad_alloc&) {
+        napi_throw_range_error(env, "ERR_NOMEM", "out of host memory");
+    } catch (const std::exception& e) {
+        napi_throw_error(env, "ERR_NATIVE", e.what());
+    } catch (...) {
+        napi_throw_error(env, "ERR_NATIVE", "native exception");
+    }
+    return nullptr;
+}
+
 napi_value Init(napi_env env, napi_value exports) {
     napi_property_descriptor mt_methods[] = {
-        {"add_tracks", nullptr, MtAddTracks, nullptr, nullptr, nullptr, napi_default, nullptr},
-        {"remove_track", nullptr, MtRemoveTrack, nullptr, nullptr, nullptr, napi_default, nullptr},
-        {"get_spec_image", nullptr, MtGetSpecImage, nullptr, nullptr, nullptr, napi_default, nullptr},
-        {"get_wav_image", nullptr, MtGetWavImage, nullptr, nullptr, nullptr, napi_default, nullptr},
-        {"get_frequency_hz", nullptr, MtGetFrequencyHz, nullptr, nullptr, nullptr, napi_default, nullptr},
-        {"get_max_db", nullptr, MtGetScalar<thesia_mt_get_max_db>, nullptr, nullptr, nullptr, napi_default, nullptr},
-        {"get_min_db", nullptr, MtGetScalar<thesia_mt_get_min_db>, nullptr, nullptr, nullptr, napi_default, nullptr},
-        {"get_max_sec", nullptr, MtGetScalar<thesia_mt_get_max_sec>, nullptr, nullptr, nullptr, napi_default, nullptr},
-        {"get_sec", nullptr, MtGetSec, nullptr, nullptr, nullptr, napi_default, nullptr},
-        {"get_sr", nullptr, MtGetSr, nullptr, nullptr, nullptr, napi_default, nullptr},
-        {"get_path", nullptr, MtGetString<thesia_mt_get_path>, nullptr, nullptr, nullptr, napi_default, nullptr},
-        {"get_filename", nullptr, MtGetString<thesia_mt_get_filename>, nullptr, nullptr, nullptr, napi_default, nullptr},
-        {"free", nullptr, MtFree, nullptr, nullptr, nullptr, napi_default, nullptr},
+        {"add_tracks", nullptr, Guarded<MtAddTracks>, nullptr, nullptr, nullptr, napi_default, nullptr},
+        {"remove_track", nullptr, Guarded<MtRemoveTrack>, nullptr, nullptr, nullptr, napi_default, nullptr},
+        {"get_spec_image", nullptr, Guarded<MtGetSpecImage>, nullptr, nullptr, nullptr, napi_default, nullptr},
+        {"get_wav_image", nullptr, Guarded<MtGetWavImage>, nullptr, nullptr, nullptr, napi_default, nullptr},
+        {"get_frequency_hz", nullptr, Guarded<MtGetFrequencyHz>, nullptr, nullptr, nullptr, napi_default, nullptr},
+        {"get_max_db", nullptr, Guarded<MtGetScalar<thesia_mt_get_max_db>>, nullptr, nullptr, nullptr, napi_default, nullptr},
+        {"get_min_db", nullptr, Guarded<MtGetScalar<thesia_mt_get_min_db>>, nullptr, nullptr, nullptr, napi_default, nullptr},
+        {"get_max_sec", nullptr, Guarded<MtGetScalar<thesia_mt_get_max_sec>>, nullptr, nullptr, nullptr, napi_default, nullptr},
+        {"get_sec", nullptr, Guarded<MtGetSec>, nullptr, nullptr, nullptr, napi_default, nullptr},
+        {"get_sr", nullptr, Guarded<MtGetSr>, nullptr, nullptr, nullptr, napi_default, nullptr},
+        {"get_path", nullptr, Guarded<MtGetString<thesia_mt_get_path>>, nullptr, nullptr, nullptr, napi_default, nullptr},
+        {"get_filename", nullptr, Guarded<MtGetString<thesia_mt_get_filename>>, nullptr, nullptr, nullptr, napi_default, nullptr},
+        {"free", nullptr, Guarded<MtFree>, nullptr, nullptr, nullptr, napi_default, nullptr},
     };
     napi_value cls;
-    NAPI_OK(napi_define_class(env, "MultiTrack", NAPI_AUTO_LENGTH, MtNew, nullptr,
+    NAPI_OK(napi_define_class(env, "MultiTrack", NAPI_AUTO_LENGTH, Guarded<MtNew>, nullptr,
                               sizeof(mt_methods) / sizeof(mt_methods[0]), mt_methods, &cls));
     // module exports are plain enumerable properties (as a wasm-bindgen package's exports)
     constexpr napi_property_attributes kExport =
         static_cast<napi_property_attributes>(napi_writable | napi_enumerable | napi_configurable);
     napi_property_descriptor fns[] = {
         {"MultiTrack", nullptr, nullptr, nullptr, nullptr, cls, kExport, nullptr},
-        {"get_colormap", nullptr, GetColormap, nullptr, nullptr, nullptr, kExport, nullptr},
-        {"hann", nullptr, Hann, nullptr, nullptr, nullptr, kExport, nullptr},
-        {"calc_mel_fb", nullptr, CalcMelFb, nullptr, nullptr, nullptr, kExport, nullptr},
-        {"calc_mel_fb_default", nullptr, CalcMelFbDefault, nullptr, nullptr, nullptr, kExport, nullptr},
-        {"perform_stft", nullptr, PerformStft, nullptr, nullptr, nullptr, kExport, nullptr},
-        {"version", nullptr, Version, nullptr, nullptr, nullptr, kExport, nullptr},
-        {"device_count", nullptr, DeviceCount, nullptr, nullptr, nullptr, kExport, nullptr},
+        {"get_colormap", nullptr, Guarded<GetColormap>, nullptr, nullptr, nullptr, kExport, nullptr},
+        {"hann", nullptr, Guarded<Hann>, nullptr, nullptr, nullptr, kExport, nullptr},
+        {"calc_mel_fb", nullptr, Guarded<CalcMelFb>, nullptr, nullptr, nullptr, kExport, nullptr},
+        {"calc_mel_fb_default", nullptr, Guarded<CalcMelFbDefault>, nullptr, nullptr, nullptr, kExport, nullptr},
+        {"perform_stft", nullptr, Guarded<PerformStft>, nullptr, nullptr, nullptr, kExport, nullptr},
+        {"version", nullptr, Guarded<Version>, nullptr, nullptr, nullptr, kExport, nullptr},
+        {"device_count", nullptr, Guarded<DeviceCount>, nullptr, nullptr, nullptr, kExport, nullptr},
     };
     NAPI_OK(napi_define_properties(env, exports, sizeof(fns) / sizeof(fns[0]), fns));
     return exports;

@@ -58,6 +58,14 @@ int thesia_host_register(void* host, size_t bytes);
 int thesia_host_unregister(void* host);
 int thesia_memset_device(void* dst_device, int value, size_t bytes);
 int thesia_device_synchronize(void);
+/* The library's own stream-ordered memory pool on the current device (not the device's default
+ * pool): buffers the library frees stay reserved there for its next allocations, without a device
+ * synchronisation. thesia_pool_trim hands the unused reserve back to the device (it also runs in
+ * thesia_mt_destroy, after MultiTrack compaction and before an allocation that ran out of memory
+ * is retried); thesia_pool_bytes reports the pool's reserved and in-use bytes (either may be NULL).
+ * Plumbing, not part of the reference surface. */
+int thesia_pool_trim(void);
+int thesia_pool_bytes(uint64_t* reserved, uint64_t* used);
 /* Device name / CU count of the current device (for reports). */
 int thesia_device_info(char* name, size_t cap, int* n_cu);
 /* HIP events for timing work on a stream (NULL stream => the library's stream of the current
@@ -204,7 +212,8 @@ typedef enum {
      * 0 = default (complex rows as whole 128-byte lines, the line two rows share carried from
      * frame to frame; linear rows LDS-staged 16-byte stores), 1 = the other method (LDS-staged
      * 16-byte for complex / lane-wise for linear rows), 2 = complex whole lines, 3 = complex
-     * lane-wise 8-byte stores; 1 and 3 at n_fft 2048 stereo f32 only */
+     * lane-wise 8-byte stores (2 and 3: complex rows only, THESIA_ERR_INVALID_ARG otherwise);
+     * 1 and 3 at n_fft 2048 stereo f32 only */
     THESIA_BATCH_OPT_ROW_STORE = 3,
     /* a device buffer of 3 int32 per track (value = its address, 0 = off): every run also
      * leaves each track's max / min over its output rows and a NaN flag there (the per-track
@@ -322,8 +331,9 @@ int thesia_mt_set_setting(thesia_mt* mt, float win_ms, size_t t_overlap, size_t 
 /* add_tracks(id_list, path_list) -> Result<bool, JsValue> -- lib.rs:170-191.
  * paths are '\n'-separated; *changed = "global dB range / max sr changed: refetch all
  * images". On error nothing is added (the reference would leave a half-added state).
- * The files are read concurrently into a page-locked host buffer the handle keeps (grow-only,
- * about 1.25x the largest call's total file size; freed by thesia_mt_destroy). */
+ * The files are read concurrently into a page-locked host buffer the handle keeps between calls
+ * (about 1.25x the call's total file size, at most 256 MiB; a call whose files exceed that reads
+ * into a page-locked buffer of its own, freed when the call returns; thesia_mt_destroy frees it). */
 int thesia_mt_add_tracks(thesia_mt* mt, const uint64_t* ids, size_t n_ids, const char* paths,
                          int* changed);
 /* WAV files keep their sample encoding up to the device: 8/16/24/32-bit integer or f32 samples

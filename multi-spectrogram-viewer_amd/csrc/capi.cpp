@@ -61,8 +61,25 @@ int thesia_get_device(int* device) {
     return THESIA_OK;
 }
 int thesia_device_malloc(void** ptr, size_t bytes) {
-    THESIA_HIP(hipMalloc(ptr, bytes ? bytes : 16));
+    if (!ptr) return set_error(THESIA_ERR_INVALID_ARG, "null argument");
+    hipError_t e = hipMalloc(ptr, bytes ? bytes : 16);
+    if (e == hipErrorOutOfMemory || e == hipErrorMemoryAllocation) {
+        // the library pool's idle reserve is not visible to hipMalloc: hand it back, retry once
+        (void)hipGetLastError();
+        if (trim_pool() == THESIA_OK) e = hipMalloc(ptr, bytes ? bytes : 16);
+    }
+    THESIA_HIP(e);
     return THESIA_OK;
+}
+int thesia_pool_trim(void) {
+    GUARD_BEGIN
+    return trim_pool();
+    GUARD_END
+}
+int thesia_pool_bytes(uint64_t* reserved, uint64_t* used) {
+    GUARD_BEGIN
+    return pool_bytes(reserved, used);
+    GUARD_END
 }
 int thesia_device_free(void* ptr) {
     THESIA_HIP(hipFree(ptr));
@@ -587,7 +604,11 @@ int thesia_mt_create(thesia_mt** mt) {
     return THESIA_OK;
     GUARD_END
 }
-void thesia_mt_destroy(thesia_mt* mt) { delete reinterpret_cast<MultiTrack*>(mt); }
+void thesia_mt_destroy(thesia_mt* mt) {
+    if (!mt) return;
+    delete reinterpret_cast<MultiTrack*>(mt);
+    (void)trim_pool();  // the handle's buffers leave the library pool's reserve too
+}
 
 static MultiTrack* M(thesia_mt* mt) { return reinterpret_cast<MultiTrack*>(mt); }
 static const MultiTrack* M(const thesia_mt* mt) { return reinterpret_cast<const MultiTrack*>(mt); }
@@ -629,7 +650,8 @@ int thesia_mt_add_tracks(thesia_mt* mt, const uint64_t* ids, size_t n_ids, const
         if (rc) return set_error(rc, err);
         foff[i + 1] = foff[i] + ((fsz[i] + 63) & ~size_t(63));
     }
-    uint8_t* stage = M(mt)->staging(foff[n]);
+    PinnedTmp big;  // a call larger than the handle's kept staging (freed when the call returns)
+    uint8_t* stage = M(mt)->staging(foff[n], &big);
     // the files read concurrently (the reference's per-track rayon loop, lib.rs:161-166, reads
     // and transforms each track on its own worker); errors reported in list order
     std::vector<int> rcs(n, 0);

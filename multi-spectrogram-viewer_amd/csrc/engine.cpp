@@ -34,24 +34,58 @@ void DevBuf::release() {
     bytes = 0;
 }
 
-// the device's default memory pool keeps what is freed into it (release threshold: unlimited)
-static bool pool_ready() {
+// The library's own stream-ordered memory pool per device (hipMemPoolCreate, not the device's
+// default pool: no other allocator in the process is affected). Its release threshold is
+// unlimited, so a block freed by hipFreeAsync stays reserved for the library's next allocation
+// without a device synchronisation; trim_pool() hands the unused reserve back to the device
+// (MultiTrack destroy / compaction, thesia_pool_trim, and before an allocation is retried
+// after running out of memory). nullptr where pools are unavailable.
+static hipMemPool_t lib_pool() {
     static std::mutex mu;
-    static std::map<int, bool> ready;
+    static std::map<int, hipMemPool_t> pools;
     int dev = 0;
     (void)hipGetDevice(&dev);
     std::lock_guard<std::mutex> lk(mu);
-    auto it = ready.find(dev);
-    if (it != ready.end()) return it->second;
-    bool ok = false;
+    auto it = pools.find(dev);
+    if (it != pools.end()) return it->second;
     hipMemPool_t pool = nullptr;
-    if (hipDeviceGetDefaultMemPool(&pool, dev) == hipSuccess && pool) {
+    hipMemPoolProps props{};
+    props.allocType = hipMemAllocationTypePinned;
+    props.handleTypes = hipMemHandleTypeNone;
+    props.location.type = hipMemLocationTypeDevice;
+    props.location.id = dev;
+    if (hipMemPoolCreate(&pool, &props) == hipSuccess && pool) {
         uint64_t thr = ~uint64_t(0);
-        ok = hipMemPoolSetAttribute(pool, hipMemPoolAttrReleaseThreshold, &thr) == hipSuccess;
+        if (hipMemPoolSetAttribute(pool, hipMemPoolAttrReleaseThreshold, &thr) != hipSuccess) {
+            (void)hipMemPoolDestroy(pool);
+            pool = nullptr;
+        }
+    } else {
+        pool = nullptr;
     }
     (void)hipGetLastError();
-    ready[dev] = ok;
-    return ok;
+    pools[dev] = pool;  // never destroyed: library buffers may outlive any owner object
+    return pool;
+}
+
+int trim_pool() {
+    hipMemPool_t pool = lib_pool();
+    if (!pool) return THESIA_OK;
+    // frees are stream-ordered on the library stream: let them complete first
+    THESIA_HIP(hipStreamSynchronize(default_stream()));
+    THESIA_HIP(hipMemPoolTrimTo(pool, 0));
+    return THESIA_OK;
+}
+
+int pool_bytes(uint64_t* reserved, uint64_t* used) {
+    uint64_t r = 0, u = 0;
+    if (hipMemPool_t pool = lib_pool()) {
+        THESIA_HIP(hipMemPoolGetAttribute(pool, hipMemPoolAttrReservedMemCurrent, &r));
+        THESIA_HIP(hipMemPoolGetAttribute(pool, hipMemPoolAttrUsedMemCurrent, &u));
+    }
+    if (reserved) *reserved = r;
+    if (used) *used = u;
+    return THESIA_OK;
 }
 
 int DevBuf::alloc(size_t n) {
@@ -59,10 +93,19 @@ int DevBuf::alloc(size_t n) {
     if (n == 0) n = 16;
     hipStream_t s = default_stream();
     hipError_t e = hipErrorNotSupported;
-    if (pool_ready()) e = hipMallocAsync(&p, n, s);
+    hipMemPool_t pool = lib_pool();
+    if (pool) {
+        e = hipMallocFromPoolAsync(&p, n, pool, s);
+        if (e == hipErrorOutOfMemory || e == hipErrorMemoryAllocation) {
+            // the reserve of other sizes may be what is missing: hand it back and retry once
+            (void)hipGetLastError();
+            if (trim_pool() == THESIA_OK) e = hipMallocFromPoolAsync(&p, n, pool, s);
+        }
+    }
     pooled = e == hipSuccess;
     if (!pooled) {
         (void)hipGetLastError();
+        if (pool) (void)trim_pool();
         e = hipMalloc(&p, n);
     }
     if (e != hipSuccess) {
@@ -802,6 +845,10 @@ int batch_set_option(Batch* b, int option, int64_t value) {
         }
         case THESIA_BATCH_OPT_ROW_STORE:
             if (value < 0 || value > 3) return set_error(THESIA_ERR_INVALID_ARG, "row_store must be 0..3");
+            // 2 and 3 name complex-row methods: on real rows they would change nothing but turn
+            // the in-epilogue range fold off
+            if (value >= 2 && b->launch.out_kind != OUT_COMPLEX)
+                return set_error(THESIA_ERR_INVALID_ARG, "row_store 2 / 3 apply to complex rows only");
             b->launch.row_alt = (int)value;
             return THESIA_OK;
         default:

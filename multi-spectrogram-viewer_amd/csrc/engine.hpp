@@ -28,11 +28,11 @@ const char* last_error();
     } while (0)
 
 // ---- device buffer (move-only RAII) ----
-// Stream-ordered on the library stream of the device it was made on (hipMallocAsync /
-// hipFreeAsync from the device's memory pool, which keeps freed blocks for reuse): a release is
-// ordered after the work already enqueued there and costs no device synchronisation (a hipFree
-// took ~160 us each: 1.5 ms of a 4.4 ms MultiTrack add_tracks call, profiles/r03_viewer). Falls
-// back to hipMalloc / hipFree where the pool allocator is unavailable.
+// Stream-ordered on the library stream of the device it was made on (hipMallocFromPoolAsync /
+// hipFreeAsync from the library's own memory pool, which keeps freed blocks for reuse until
+// trim_pool()): a release is ordered after the work already enqueued there and costs no device
+// synchronisation (a hipFree took ~160 us each: 1.5 ms of a 4.4 ms MultiTrack add_tracks call,
+// profiles/r03_viewer). Falls back to hipMalloc / hipFree where pools are unavailable.
 struct DevBuf {
     void* p = nullptr;
     size_t bytes = 0;
@@ -61,6 +61,10 @@ struct DevBuf {
 };
 
 hipStream_t default_stream();  // library stream of the current device
+// the library pool of the current device: hand its unused reserve back to the device (after the
+// library stream's frees complete); its reserved / in-use bytes
+int trim_pool();
+int pool_bytes(uint64_t* reserved, uint64_t* used);
 hipError_t copy_ordered(void* dst, const void* src, size_t bytes, hipMemcpyKind kind);
 
 // ---- plan ----

@@ -20,7 +20,14 @@ MultiTrack::~MultiTrack() {
     if (stage_) (void)hipHostFree(stage_);
 }
 
-uint8_t* MultiTrack::staging(size_t bytes) {
+PinnedTmp::~PinnedTmp() {
+    if (p) {
+        (void)hipStreamSynchronize(default_stream());  // the call's uploads may still read it
+        (void)hipHostFree(p);
+    }
+}
+
+uint8_t* MultiTrack::staging(size_t bytes, PinnedTmp* tmp) {
     // an add_tracks that failed after enqueuing its uploads returned before its synchronisation:
     // its copies may still read the staging (the stream is idle otherwise)
     if (hipStreamSynchronize(default_stream()) != hipSuccess) return nullptr;
@@ -28,8 +35,16 @@ uint8_t* MultiTrack::staging(size_t bytes) {
     if (stage_) (void)hipHostFree(stage_);
     stage_ = nullptr;
     stage_bytes_ = 0;
-    const size_t want = bytes + bytes / 4;  // headroom: a session adds files of similar sizes
     void* p = nullptr;
+    if (bytes > kStageKeep) {
+        // a call larger than the handle keeps pinned between calls: a buffer of its own, freed
+        // (after the stream drains) when the call returns
+        if (!tmp || hipHostMalloc(&p, bytes, hipHostMallocDefault) != hipSuccess) return nullptr;
+        tmp->p = p;
+        return static_cast<uint8_t*>(p);
+    }
+    // headroom: a session adds files of similar sizes
+    const size_t want = std::min(bytes + bytes / 4, kStageKeep);
     if (hipHostMalloc(&p, want, hipHostMallocDefault) != hipSuccess) return nullptr;
     stage_ = static_cast<uint8_t*>(p);
     stage_bytes_ = want;
@@ -368,8 +383,9 @@ void MultiTrack::compact_pools() {
     };
     move_out(wav_use, true);
     move_out(spec_use, false);
-    // the old pools are released once the last shared_ptr goes; the copies read them first
-    if (copied) (void)hipStreamSynchronize(s);
+    // the old pools are released once the last shared_ptr goes (stream-ordered frees behind the
+    // copies); their bytes then leave the library pool's reserve too (trim_pool synchronises)
+    if (copied) (void)trim_pool();
 }
 
 size_t MultiTrack::device_bytes() const {

@@ -41,6 +41,15 @@ struct PcmIn {
     std::string path;
 };
 
+// a page-locked host buffer for one add_tracks call (hipHostFree after the library stream drains)
+struct PinnedTmp {
+    void* p = nullptr;
+    PinnedTmp() = default;
+    PinnedTmp(const PinnedTmp&) = delete;
+    PinnedTmp& operator=(const PinnedTmp&) = delete;
+    ~PinnedTmp();
+};
+
 class MultiTrack {
   public:
     struct Setting {  // SpecSetting, lib.rs:64-70 / defaults lib.rs:93-99
@@ -72,9 +81,11 @@ class MultiTrack {
     size_t size() const { return tracks_.size(); }
     // device bytes the tracks hold: their wav / spectrogram buffers (shared ones once) and greys
     size_t device_bytes() const;
-    // page-locked host staging for add_tracks' file reads (grow-only, this handle's; free again
-    // once add_tracks returns, which synchronises its uploads): nullptr if it cannot be had
-    uint8_t* staging(size_t bytes);
+    // page-locked host staging for add_tracks' file reads (this handle's, kept between calls up
+    // to kStageKeep bytes; a larger call gets a buffer of its own in *tmp, freed when *tmp goes):
+    // nullptr if it cannot be had (the files are then read into pageable memory)
+    static constexpr size_t kStageKeep = size_t(256) << 20;
+    uint8_t* staging(size_t bytes, PinnedTmp* tmp);
 
   private:
     int make_plan(const Track& tr, Plan** out) const;

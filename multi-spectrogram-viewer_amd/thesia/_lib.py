@@ -55,6 +55,8 @@ _SIGS = {
     "thesia_host_unregister": (_i, [_vp]),
     "thesia_memset_device": (_i, [_vp, _i, _sz]),
     "thesia_device_synchronize": (_i, []),
+    "thesia_pool_trim": (_i, []),
+    "thesia_pool_bytes": (_i, [_u64p, _u64p]),
     "thesia_device_info": (_i, [C.c_char_p, _sz, C.POINTER(_i)]),
     "thesia_event_create": (_i, [C.POINTER(_vp)]),
     "thesia_event_destroy": (_i, [_vp]),

@@ -61,11 +61,16 @@ class MultiTrack:
             check(lib.thesia_mt_set_setting(self.h, win_ms, t_overlap, f_overlap, int(freq_scale), db_range))
         self.freq_scale = freq_scale
 
+    def close(self) -> None:
+        """Destroy the handle now (wasm-bindgen's free()): its device buffers return to the
+        library pool, whose unused reserve is then handed back to the device."""
+        if self.h and self.h.value:
+            lib.thesia_mt_destroy(self.h)
+            self.h = C.c_void_p()
+
     def __del__(self):
         try:
-            if self.h and self.h.value:
-                lib.thesia_mt_destroy(self.h)
-                self.h = C.c_void_p()
+            self.close()
         except Exception:
             pass
 

@@ -24,6 +24,36 @@ def track_cost(n_samples: int, win_length: int, hop_length: int, n_fft: int, n_m
     return float(T) * (n_fft * math.log2(max(n_fft, 2)) + 2.0 * F + 2.0 * n_mels)
 
 
+def _lanczos3_taps(src: int, dst: int) -> int:
+    """Most taps of one axis of image 0.23's Lanczos3 resample (src -> dst): 2*ceil(3*ratio)+1
+    where it downsamples, 7 where it does not (display.rs:57; host_tables.cpp lanczos3_taps)."""
+    if src <= 0 or dst <= 0:
+        return 0
+    ratio = max(src / dst, 1.0)
+    return min(src, 2 * math.ceil(3.0 * ratio) + 1)
+
+
+def display_cost(n_samples: int, sr: int, win_length: int, hop_length: int, n_fft: int, max_sr: int,
+                 px_per_sec: float = 100.0, nheight: int = 500, n_mels: int = 0,
+                 freq_scale_mel: bool = False) -> float:
+    """Cost model of one track's display (grey + Lanczos3 + colormap, lib.rs:193-298 /
+    display.rs:44-61), in HBM-byte equivalents: the dB rows read once (4*T*bins), the f32
+    intermediate of the separable resize written and read ([nheight, T], 8*T*nheight), the RGB
+    bytes written (3*nwidth*nheight), and the taps' arithmetic at the MI355X ridge of ~20 flop per
+    byte (2 flop per tap: the vertical pass T*nheight*vtaps, the horizontal one
+    nwidth*nheight*htaps). bins = n_mels or n_fft/2+1; H = round(bins*up_ratio)."""
+    T = stft_n_frames(n_samples, win_length, hop_length)
+    if T == 0 or nheight == 0:
+        return 0.0
+    bins = n_mels or n_fft // 2 + 1
+    H = max(int(round(bins * up_ratio(sr, max_sr, freq_scale_mel))), bins)
+    nwidth = int(px_per_sec * n_samples / sr)
+    vt, ht = _lanczos3_taps(H, nheight), _lanczos3_taps(T, nwidth)
+    bytes_ = 4.0 * T * bins + 8.0 * T * nheight + 3.0 * nwidth * nheight
+    flops = 2.0 * (T * nheight * vt + nwidth * nheight * ht)
+    return bytes_ + flops / 20.0
+
+
 def assign_tracks(costs: Sequence[float], world_size: int) -> List[List[int]]:
     """Greedy LPT: tracks in decreasing cost (ties: lower index first) go to the least-loaded
     rank (ties: lower rank). Deterministic, so every rank computes the same partition without
@@ -37,6 +67,35 @@ def assign_tracks(costs: Sequence[float], world_size: int) -> List[List[int]]:
         r = min(range(world_size), key=lambda k: (load[k], k))
         shards[r].append(i)
         load[r] += float(costs[i])
+    return [sorted(s) for s in shards]
+
+
+def assign_tracks_2phase(spec_costs: Sequence[float], disp_costs: Sequence[float],
+                         world_size: int) -> List[List[int]]:
+    """Greedy LPT over two phases that a step runs one after the other, with the range exchange
+    between them (lib.rs:193-263: the display needs every rank's range first): a step takes the
+    slowest rank's spectrogram phase plus the slowest rank's display phase, so each phase is
+    balanced on its own. Each phase's costs are normalised by their total; tracks go in
+    decreasing normalised sum (ties: lower index) to the rank whose larger normalised load after
+    adding the track is smallest (ties: smaller sum, then lower rank). Deterministic on every
+    rank. Returns, per rank, its track indices in increasing order."""
+    if world_size < 1:
+        raise ValueError("world_size must be >= 1")
+    if len(spec_costs) != len(disp_costs):
+        raise ValueError("one spectrogram and one display cost per track")
+    A = float(sum(spec_costs)) or 1.0
+    B = float(sum(disp_costs)) or 1.0
+    a = [float(c) / A for c in spec_costs]
+    b = [float(c) / B for c in disp_costs]
+    order = sorted(range(len(a)), key=lambda i: (-(a[i] + b[i]), i))
+    la = [0.0] * world_size
+    lb = [0.0] * world_size
+    shards: List[List[int]] = [[] for _ in range(world_size)]
+    for i in order:
+        r = min(range(world_size), key=lambda k: (max(la[k] + a[i], lb[k] + b[i]), la[k] + lb[k], k))
+        shards[r].append(i)
+        la[r] += a[i]
+        lb[r] += b[i]
     return [sorted(s) for s in shards]
 
 

@@ -143,3 +143,28 @@ def test_remove_frees_shared_pools():
     assert left < full / 5
     assert np.array_equal(mt.get_spec(9).view(np.uint32), spec9.view(np.uint32))
     assert len(mt.get_spec_image(9, 100.0, 64)) == int(np.float32(100.0) * np.float32(len(pcm[9])) / np.float32(24000)) * 64 * 3
+
+
+def test_destroy_hands_the_pool_reserve_back(excerpts, tmp_path):
+    """Library buffers come from the library's own stream-ordered pool (not the device default
+    pool); thesia_mt_destroy trims it, so a destroyed handle's HBM leaves the pool's
+    reserve (thesia_pool_bytes) instead of staying reserved for the process's life."""
+    import ctypes as C
+    from thesia._lib import lib, check
+    res, used = C.c_uint64(), C.c_uint64()
+    check(lib.thesia_pool_trim())
+    check(lib.thesia_pool_bytes(C.byref(res), C.byref(used)))
+    base = res.value
+    paths = []
+    for t in ("44k1", "48k"):
+        p = str(tmp_path / f"s_{t}.wav")
+        _write_wav(p, *excerpts[t])
+        paths.append(p)
+    mt = thesia.MultiTrack()
+    mt.add_tracks([0, 1], "\n".join(paths))
+    check(lib.thesia_pool_bytes(C.byref(res), C.byref(used)))
+    assert used.value > 0 and res.value >= used.value
+    mt.remove_track(0)  # compaction moves track 1 out of the shared buffers and trims
+    mt.close()
+    check(lib.thesia_pool_bytes(C.byref(res), C.byref(used)))
+    assert res.value <= base, (base, res.value, used.value)

@@ -83,3 +83,29 @@ console.log(JSON.stringify(out));
     assert r["io"][0] == -2 and "No such file" in r["io"][1]
     assert r["badids"] is not None and r["freed"][0] == "ERR_FREED" and r["ctor"] is not None
     assert r["empty"] == [0]
+
+
+def test_numeric_arguments_are_range_checked():
+    """Sizes / rates / heights from JavaScript are checked before any cast: a negative,
+    fractional, NaN or oversized value throws a RangeError instead of reaching a size_t / uint32_t
+    conversion or a huge allocation; the process survives."""
+    r = run_node("""
+const out = {};
+const grab = (k, f) => { try { f(); out[k] = null; } catch (e) { out[k] = [e.constructor.name, e.code]; } };
+grab('hann_neg', () => t.hann(-4, false));
+grab('hann_nan', () => t.hann(NaN, false));
+grab('hann_frac', () => t.hann(4.5, false));
+grab('hann_huge', () => t.hann(1e15, false));
+grab('mel_sr', () => t.calc_mel_fb_default(-48000, 2048));
+grab('mel_nmel', () => t.calc_mel_fb(48000, 2048, 1e12, 0, null, true));
+grab('stft_win', () => t.perform_stft(new Float32Array(16), -1, 4, 8));
+const mt = new t.MultiTrack();
+grab('nheight', () => mt.get_spec_image(0, 100, -5));
+grab('nheight_big', () => mt.get_wav_image(0, 100, 2 ** 40, -1, 1));
+out.alive = t.hann(4, false).length;
+console.log(JSON.stringify(out));
+""")
+    for k in ("hann_neg", "hann_nan", "hann_frac", "hann_huge", "mel_sr", "mel_nmel", "stft_win",
+              "nheight", "nheight_big"):
+        assert r[k] == ["RangeError", "ERR_ARG"], (k, r[k])
+    assert r["alive"] == 4

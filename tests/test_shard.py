@@ -149,3 +149,61 @@ def test_non_gloo_group_without_shadow_is_an_error():
     import pytest as _pt
     with _pt.raises(RuntimeError, match="init_host_groups"):
         shard._host_group(FakeDist(), None)
+
+
+def test_display_cost_grows_with_each_term():
+    base = dict(n_samples=480000, sr=48000, win_length=2048, hop_length=512, n_fft=2048, max_sr=48000)
+    c = shard.display_cost(**base)
+    assert c > 0
+    assert shard.display_cost(**{**base, "n_samples": 960000}) > 1.9 * c  # T and nwidth double
+    assert shard.display_cost(**base, nheight=1000) > 1.3 * c              # the image rows
+    assert shard.display_cost(**base, px_per_sec=400.0) > c                # more columns
+    # a lower-rate track of the same length: grey image taller (up_ratio), fewer frames
+    lo = shard.display_cost(**{**base, "sr": 8000, "n_samples": 80000})
+    assert 0 < lo < c
+    assert shard._lanczos3_taps(6891, 1000) == 43 and shard._lanczos3_taps(140, 500) == 7
+
+
+def _mixed_workload(n=1000, seed=7):
+    """Mixed durations (1-60 s), rates, n_fft and image heights (the display phase is 72 % of a
+    C5 step)."""
+    rng = np.random.default_rng(seed)
+    rates = [8000, 16000, 22050, 24000, 44100, 48000]
+    ffts = [256, 512, 1024, 2048]
+    heights = [200, 500, 800]
+    spec, disp = [], []
+    for _ in range(n):
+        sr = int(rng.choice(rates))
+        nf = int(rng.choice(ffts))
+        nh = int(rng.choice(heights))
+        ns = int(sr * rng.uniform(1.0, 60.0))
+        spec.append(shard.track_cost(ns, nf, nf // 4, nf))
+        disp.append(shard.display_cost(ns, sr, nf, nf // 4, nf, 48000, 100.0, nh))
+    return spec, disp
+
+
+@pytest.mark.parametrize("ws", [2, 4, 8])
+def test_two_phase_partition_balances_both_phases(ws):
+    """Both phases' per-rank loads within 5 % of their mean on a mixed workload (a scalar-cost
+    LPT balances only the sum, and a step pays the slowest rank of each phase)."""
+    spec, disp = _mixed_workload()
+    shards = shard.assign_tracks_2phase(spec, disp, ws)
+    assert sorted(i for s in shards for i in s) == list(range(len(spec)))
+    assert shards == shard.assign_tracks_2phase(spec, disp, ws)  # deterministic on every rank
+    for costs in (spec, disp):
+        loads = [sum(costs[i] for i in s) for s in shards]
+        mean = sum(loads) / ws
+        assert max(abs(l - mean) for l in loads) <= 0.05 * mean, (ws, loads)
+
+
+def test_two_phase_beats_spectrogram_only_lpt_on_display():
+    """The spectrogram-only cost model (round 3) leaves the display phase unbalanced on a workload
+    whose image heights vary; the two-phase partition does not."""
+    spec, disp = _mixed_workload(400, seed=3)
+    def spread(shards, costs):
+        loads = [sum(costs[i] for i in s) for s in shards]
+        return max(loads) / (sum(loads) / len(loads)) - 1.0
+    old = shard.assign_tracks(spec, 8)
+    new = shard.assign_tracks_2phase(spec, disp, 8)
+    assert spread(new, disp) < spread(old, disp)
+    assert spread(new, disp) <= 0.05 and spread(new, spec) <= 0.05
