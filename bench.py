@@ -78,6 +78,8 @@ def parse():
                         "lines, 3 lane-wise 8-byte)")
     p.add_argument("--row-stores", default="", help="A/B of the complex-output row stores (comma list, "
                    "interleaved rounds, one process), reported in roofline_window_rfft")
+    p.add_argument("--spec-policies", default="", help="c5: A/B of thesia_set_batches_policy for the "
+                   "spectrogram phase (comma list, interleaved rounds, one process)")
     p.add_argument("--render-path", type=int, default=-1, help="c5: the display launch structure "
                    "(thesia_set_render_path; -1 = the library default)")
     p.add_argument("--render-paths", default="", help="c5: A/B of the display launch structures "
@@ -498,6 +500,21 @@ def main_c5(args, ws, rank, pg, device):
             p.run_spectrograms()
     kms_overlap = tm.ms / 3
     disp = p.display_timed(3)
+    pol_ms = None
+    if args.spec_policies:
+        import numpy as np
+        pols = [int(v) for v in args.spec_policies.split(",")]
+        res = {q: [] for q in pols}
+        for _ in range(5):  # interleaved rounds
+            for q in pols:
+                engine.set_batches_policy(q)
+                p.run_spectrograms()
+                with engine.EventTimer() as tm:
+                    for _ in range(3):
+                        p.run_spectrograms()
+                res[q].append(tm.ms / 3)
+        engine.set_batches_policy(1)
+        pol_ms = {str(q): {"median": float(np.median(t)), "min": float(min(t))} for q, t in res.items()}
     if args.render_paths:
         import numpy as np
         rp = [int(v) for v in args.render_paths.split(",")]
@@ -537,6 +554,7 @@ def main_c5(args, ws, rank, pg, device):
                          "kernel_ms": kms, "algorithmic_bytes_per_launch": in_bytes + out_bytes,
                          "kernel_ms_note": "sum of the batches' launches, each timed alone",
                          "overlapped_ms": kms_overlap,
+                         "batches_policy_ms": pol_ms,
                          "per_batch": [{"n_fft": nf, "frames": fr, "kernel_ms": t} for nf, fr, t in kms_batches],
                          "overlapped_note": "the step's spectrogram phase: the batches on the library "
                                             "streams (thesia_batches_run), HIP events on the library stream"},

@@ -349,6 +349,23 @@ napi_value MtGetWavImage(napi_env env, napi_callback_info info) {
     return u8_array(env, buf.data(), need);
 }
 
+// set_fast(fast: boolean): not in the wasm-bindgen surface; thesia_mt_set_fast (the streaming
+// kernel for the tracks added afterwards, SURVEY §8c's end-to-end contract)
+napi_value MtSetFast(napi_env env, napi_callback_info info) {
+    napi_value argv[1], self;
+    if (!get_args(env, info, 1, argv, &self)) return nullptr;
+    thesia_mt* h = self_handle(env, self);
+    bool fast = false;
+    if (!h) return nullptr;
+    if (napi_get_value_bool(env, argv[0], &fast) != napi_ok) {
+        napi_throw_type_error(env, "ERR_ARG", "set_fast(fast: boolean)");
+        return nullptr;
+    }
+    const int rc = thesia_mt_set_fast(h, fast ? 1 : 0);
+    if (rc != THESIA_OK) return throw_thesia(env, rc);
+    return nullptr;
+}
+
 napi_value MtGetFrequencyHz(napi_env env, napi_callback_info info) {
     napi_value argv[2], self;
     if (!get_args(env, info, 2, argv, &self)) return nullptr;
@@ -575,6 +592,7 @@ napi_value Init(napi_env env, napi_value exports) {
         {"get_sr", nullptr, Guarded<MtGetSr>, nullptr, nullptr, nullptr, napi_default, nullptr},
         {"get_path", nullptr, Guarded<MtGetString<thesia_mt_get_path>>, nullptr, nullptr, nullptr, napi_default, nullptr},
         {"get_filename", nullptr, Guarded<MtGetString<thesia_mt_get_filename>>, nullptr, nullptr, nullptr, napi_default, nullptr},
+        {"set_fast", nullptr, Guarded<MtSetFast>, nullptr, nullptr, nullptr, napi_default, nullptr},
         {"free", nullptr, Guarded<MtFree>, nullptr, nullptr, nullptr, napi_default, nullptr},
     };
     napi_value cls;

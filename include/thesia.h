@@ -187,6 +187,12 @@ int thesia_batch_run(thesia_batch* batch, void* stream);
  * overlap. Not part of the reference surface (its per-track loop is lib.rs:161-166).
  * Asynchronous. */
 int thesia_batches_run(thesia_batch* const* batches, size_t n, void* stream);
+/* Process-wide block-count policy of thesia_batches_run for batches whose block count is
+ * automatic (THESIA_BATCH_OPT_MAX_BLOCKS 0): 1 (default) = the batches share one occupancy wave
+ * of the device in proportion to their work (frames x n_fft log2 n_fft), so they run side by
+ * side on disjoint CUs and every frame stream walks more frames; 0 = each batch sized for the
+ * whole device, as thesia_batch_run. Same results either way. */
+int thesia_set_batches_policy(int policy);
 /* Runs `iters` passes bracketed by HIP events on the launch stream; returns the elapsed
  * milliseconds of all passes (synchronous). */
 int thesia_batch_run_timed(thesia_batch* batch, void* stream, int iters, float* ms);
@@ -284,13 +290,15 @@ int thesia_grey_to_rgb_device(const float* d_grey, uint32_t width, uint32_t heig
 int thesia_minmax_segments_device(const float* d_spec, const uint64_t* row0, size_t bins,
                                   size_t n, float* max, float* min, int* has_nan);
 /* Process-wide choice of the batched display path's launch structure (all byte-identical):
- * 0 = the fused path (default): per geometry group one kernel for grey + vertical Lanczos3 in
- * one pass over the spectrogram, then one for horizontal Lanczos3 + colormap (row spans staged
- * by LDS-DMA), every track of a call in each launch; 1 = per-track launches (the reference's one
- * image at a time structure); 2 = every track in one launch per stage: grey, vertical,
- * horizontal + colormap. (Single-kernel displays -- the intermediate in LDS, per tile or as a
- * ring walked by a band of rows -- were built, byte-exact, and measured 1.5-4.7x slower on C5:
- * DESIGN.md §4.) */
+ * 0 = the fused path (default): per geometry group, where its geometry allows (at most 16
+ * vertical taps and 16 output columns meeting one 8-frame step: the groups whose images
+ * downsample along time), ONE kernel for grey + vertical Lanczos3 + horizontal Lanczos3 +
+ * colormap whose f32 intermediate never leaves registers (render_stripe_kernel); for the other
+ * groups one kernel for grey + vertical Lanczos3 in one pass over the spectrogram, then one for
+ * horizontal Lanczos3 + colormap (row spans staged by LDS-DMA); every track of a call in each
+ * launch; 1 = per-track launches (the reference's one image at a time structure); 2 = every
+ * track in one launch per stage: grey, vertical, horizontal + colormap; 3 = path 0 with the
+ * two-kernel structure for every group (round 3's default). */
 int thesia_set_render_path(int path);
 int thesia_render_rgb_batch_device(const float* d_spec, const uint64_t* row0, size_t bins,
                                    size_t n, const float* up_ratio, const uint32_t* nwidth,
@@ -328,6 +336,12 @@ void thesia_mt_destroy(thesia_mt* mt);
  * freq_scale: 0 = Linear, 1 = Mel. Must be called before any track is added. */
 int thesia_mt_set_setting(thesia_mt* mt, float win_ms, size_t t_overlap, size_t f_overlap,
                           int freq_scale, float db_range);
+/* Spectrogram kernel of the tracks added from now on (not part of the reference surface):
+ * 0 (default) = the reference-order kernel, whose images equal the oracle pipeline's bytes;
+ * 1 = the batch engine's streaming kernel for the viewer's geometry (3.3x faster behind
+ * add_tracks), held to SURVEY.md §8c's end-to-end contract: at most 1 LSB on at
+ * most 1e-4 of the pixels. */
+int thesia_mt_set_fast(thesia_mt* mt, int fast);
 /* add_tracks(id_list, path_list) -> Result<bool, JsValue> -- lib.rs:170-191.
  * paths are '\n'-separated; *changed = "global dB range / max sr changed: refetch all
  * images". On error nothing is added (the reference would leave a half-added state).

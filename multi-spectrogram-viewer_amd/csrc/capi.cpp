@@ -381,6 +381,7 @@ int thesia_batch_set_option(thesia_batch* batch, int option, int64_t value) {
 }
 
 int thesia_set_render_path(int path) { return set_render_path(path); }
+int thesia_set_batches_policy(int policy) { return set_batches_policy(policy); }
 
 
 int thesia_synth_pcm_device(void* d_out, int format, uint32_t channels, uint64_t n_tracks,
@@ -618,6 +619,13 @@ int thesia_mt_set_setting(thesia_mt* mt, float win_ms, size_t t_overlap, size_t 
     GUARD_BEGIN
     return M(mt)->set_setting(win_ms, t_overlap, f_overlap, freq_scale, db_range);
     GUARD_END
+}
+
+int thesia_mt_set_fast(thesia_mt* mt, int fast) {
+    if (!mt) return set_error(THESIA_ERR_INVALID_ARG, "null handle");
+    if (fast != 0 && fast != 1) return set_error(THESIA_ERR_INVALID_ARG, "fast must be 0 or 1");
+    M(mt)->set_fast(fast == 1);
+    return THESIA_OK;
 }
 
 static std::vector<std::string> split_paths(const char* paths) {

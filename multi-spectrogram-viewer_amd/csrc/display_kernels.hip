@@ -12,6 +12,7 @@
 // All accumulations run in the reference's order with -ffp-contract=off, so given the
 // same f32 input these kernels reproduce the oracle bit for bit.
 #include "kernels.hpp"
+#include "display_common.hpp"
 
 #include <cmath>
 #include <cstdlib>
@@ -365,12 +366,6 @@ int launch_resize_v(const float* in, uint32_t w, uint32_t h, uint32_t nh, const 
 // ------------------------------------------------------------------------------------
 // K5 horizontal pass + K6 colormap (display.rs:24-42): RGB u8 [nh][nw][3]
 // ------------------------------------------------------------------------------------
-__device__ __forceinline__ uint8_t sat_u8(float v) {  // Rust `as u8`
-    if (!(v == v)) return 0;
-    if (v <= 0.0f) return 0;
-    if (v >= 255.0f) return 255;
-    return (uint8_t)v;
-}
 
 __device__ __forceinline__ void resize_h_rgb_px(const float* in, uint32_t w, uint32_t nw,
                                                 const int32_t* left, const int32_t* cnt,
@@ -483,26 +478,6 @@ __global__ void resize_v_batch_kernel(uint32_t nh, const RenderDesc* d, const fl
     }
 }
 
-// the colormap of one horizontal-pass value (display.rs:24-42), as resize_h_rgb_px
-__device__ __forceinline__ void colormap_px(float t, const uint8_t* cmap, uint8_t* o) {
-    float x = t;
-    if (!(x >= 0.0f)) x = 0.0f;
-    const float position = 10.0f * x;
-    const float fl = floorf(position);
-    if (fl >= 9.0f) {
-        o[0] = cmap[27];
-        o[1] = cmap[28];
-        o[2] = cmap[29];
-        return;
-    }
-    const int index = (int)fl;
-    const float ratio = position - (float)index;
-#pragma unroll
-    for (int c = 0; c < 3; ++c) {
-        const float av = (float)cmap[index * 3 + c], bv = (float)cmap[(index + 1) * 3 + c];
-        o[c] = sat_u8(roundf(ratio * bv + (1.0f - ratio) * av));
-    }
-}
 
 // A block owns 256 output columns of one image and walks its rows (blockIdx.y-strided). The
 // block's input span [lb, lb + span) of each row is staged in LDS (one coalesced load per
@@ -762,11 +737,6 @@ int launch_render_batch(const float* spec, uint32_t bins, float max, float min,
 // tmp[oy][x] = sum_i grey[l + i][x] * w[i] in resize_v_px's order (t = 0; t += in * w), stored
 // along frames (coalesced). The grey image itself is never written (7.7 GB of the C5 step's
 // display traffic in the three-stage path).
-__device__ __forceinline__ float grey_of(float db, float max, float min) {  // grey_px
-    float v = (db - min) / (max - min);
-    v = fmaxf(v, 0.0f);
-    return fminf(v, 1.0f);
-}
 __global__ void __launch_bounds__(256) grey_vert_kernel(const float* spec, uint32_t bins, float max,
                                                         float min, uint32_t nh, const RenderDesc* d,
                                                         float* tmp, int tile_cap, int kv, uint32_t band) {

@@ -939,6 +939,7 @@ static int run_pool(RunPool** out) {  // caller holds run_pool_mutex()
 // device, forked from and joined back to `s`: a small launch's ramp (the first frame of every
 // stream loaded without prefetch, the tables staged into LDS) overlaps the others' work.
 // Stream-ordered on `s` like batch_run.
+int batches_policy();
 int batches_run(Batch* const* b, size_t n, hipStream_t s) {
     if (!s) s = default_stream();
     if (n <= 1) return n ? batch_run(b[0], s) : THESIA_OK;
@@ -953,10 +954,38 @@ int batches_run(Batch* const* b, size_t n, hipStream_t s) {
     int rc = run_pool(&p);
     if (rc) return rc;
     const int k = (int)std::min<size_t>(RunPool::kStreams, n);
+    // policy 1: every batch whose block count the caller left automatic gets a share of one
+    // occupancy wave proportional to its work (frames x n_fft log2 n_fft), so the concurrent
+    // batches sit on disjoint CUs and each frame stream walks more frames (a stream's ring
+    // prologue reads 4 hops to produce its first frame); policy 0: each batch takes a whole wave
+    std::vector<float> share(n, 0.f);
+    if (batches_policy() == 1 && n <= (size_t)k) {
+        double tot = 0;
+        std::vector<double> w(n, 0.0);
+        for (size_t i = 0; i < n; ++i) {
+            const double nf = (double)b[i]->plan->n_fft;
+            w[i] = (double)b[i]->total_frames * nf * std::log2(std::max(nf, 2.0));
+            tot += w[i];
+        }
+        for (size_t i = 0; i < n && tot > 0; ++i) share[i] = (float)(w[i] / tot);
+    }
     THESIA_HIP(p->fork_from(s, k));
-    for (size_t i = 0; i < n && !rc; ++i) rc = batch_run(b[i], p->st[i % k]);
+    for (size_t i = 0; i < n && !rc; ++i) {
+        const float keep = b[i]->launch.grid_share;
+        b[i]->launch.grid_share = share[i];
+        rc = batch_run(b[i], p->st[i % k]);
+        b[i]->launch.grid_share = keep;
+    }
     const int jrc = p->join_into(s, k);  // join even after an error: `s` never runs ahead of them
     return rc ? rc : jrc;
+}
+
+static int g_batches_policy = 1;  // thesia_set_batches_policy
+int batches_policy() { return __atomic_load_n(&g_batches_policy, __ATOMIC_RELAXED); }
+int set_batches_policy(int policy) {
+    if (policy < 0 || policy > 1) return set_error(THESIA_ERR_INVALID_ARG, "batches policy must be 0 or 1");
+    __atomic_store_n(&g_batches_policy, policy, __ATOMIC_RELAXED);
+    return THESIA_OK;
 }
 
 // host side of Batch::range: {ord max, ord min, NaN} -> (max, min, NaN) per track
@@ -1011,7 +1040,7 @@ static int g_render_path = 0;  // thesia_set_render_path
 
 int render_path() { return __atomic_load_n(&g_render_path, __ATOMIC_RELAXED); }
 int set_render_path(int path) {
-    if (path < 0 || path > 2) return set_error(THESIA_ERR_INVALID_ARG, "render path must be 0 .. 2");
+    if (path < 0 || path > 3) return set_error(THESIA_ERR_INVALID_ARG, "render path must be 0 .. 3");
     __atomic_store_n(&g_render_path, path, __ATOMIC_RELAXED);
     return THESIA_OK;
 }
@@ -1029,6 +1058,11 @@ struct DevTaps {
     DevBuf left, count, offset, weights;
     int max_taps = 0;
     std::vector<int32_t> h_left, h_count;  // host copies (block spans of the fused render)
+    // the taps regrouped by 8-frame step for render_stripe_kernel (RenderDesc::hst / hsw), built
+    // on first use: per step {ca, na, woff, 0} and the na x 8 weights at woff
+    DevBuf st_hdr, st_w;
+    int st_maxna = 0;  // most columns meeting one step
+    std::vector<int32_t> h_st_hdr;
 };
 
 static int dev_taps(uint32_t n, uint32_t nn, const DevTaps** out) {
@@ -1054,6 +1088,53 @@ static int dev_taps(uint32_t n, uint32_t nn, const DevTaps** out) {
         it = cache.emplace(key, std::move(d)).first;
     }
     *out = it->second.get();
+    return THESIA_OK;
+}
+
+// The stepped form of an (n -> nn) tap table: step s covers frames [8s, 8s + 8); its columns are
+// those whose support [l, l + cnt) meets the step (ca .. ca + na - 1: supports are monotone in
+// the column), each with the 8 weights of the step's frames (the column's weight where the frame
+// is inside its support, +0 elsewhere), in column order.
+static int build_stepped(uint32_t n, uint32_t nn, DevTaps* d) {
+    const Taps t = lanczos3_taps(n, nn);
+    const int nsteps = (int)((n + 7) / 8);
+    std::vector<int32_t> hdr(4 * (size_t)nsteps, 0);
+    std::vector<float> w;
+    int ca = 0, cb = -1, maxna = 0;
+    for (int s = 0; s < nsteps; ++s) {
+        while (ca < (int)nn && ((t.left[ca] + t.count[ca] - 1) >> 3) < s) ++ca;
+        while (cb + 1 < (int)nn && (t.left[cb + 1] >> 3) <= s) ++cb;
+        const int na = cb >= ca ? cb - ca + 1 : 0;
+        hdr[4 * s] = ca;
+        hdr[4 * s + 1] = na;
+        hdr[4 * s + 2] = (int32_t)w.size();
+        for (int k = 0; k < na; ++k) {
+            const int c = ca + k, l = t.left[c], cnt = t.count[c];
+            for (int u = 0; u < 8; ++u) {
+                const int f = 8 * s + u;
+                w.push_back(f >= l && f < l + cnt ? t.weights[t.offset[c] + (f - l)] : 0.0f);
+            }
+        }
+        maxna = std::max(maxna, na);
+    }
+    if (w.empty()) w.push_back(0.0f);
+    int rc = d->st_hdr.upload(hdr.data(), hdr.size() * 4);
+    if (!rc) rc = d->st_w.upload(w.data(), w.size() * 4);
+    if (rc) return rc;
+    d->st_maxna = maxna;
+    d->h_st_hdr = std::move(hdr);
+    return THESIA_OK;
+}
+
+static int dev_taps_stepped(uint32_t n, uint32_t nn, const DevTaps** out) {
+    const DevTaps* t = nullptr;
+    int rc = dev_taps(n, nn, &t);
+    if (rc) return rc;
+    static std::mutex mu;
+    std::lock_guard<std::mutex> lk(mu);
+    DevTaps* d = const_cast<DevTaps*>(t);  // the cache owns it; only this function adds the steps
+    if (!d->st_hdr.p && (rc = build_stepped(n, nn, d))) return rc;
+    *out = d;
     return THESIA_OK;
 }
 
@@ -1254,18 +1335,82 @@ struct FusedGroup {
     int v_fpl = 1;  // frames per lane of the vertical pass (4: grey_vert_wide_kernel)
     uint64_t cost = 0;  // HBM floats its two passes move (spectrogram, intermediate twice, RGB / 4)
     int stream = 0;     // render_rgb_fused: the library stream it runs on
+    // the single-pass display (render_stripe_kernel) where its instances cover the group's
+    // geometry (plan_stripe); then no intermediate is formed
+    bool stripe = false;
+    uint32_t st_strip = 64;
+    int st_kv = 0, st_slots = 0, st_fc = 0, st_tile = 0, st_hdr = 0, st_wts = 0;
+    bool st_dword = false;
 };
 
 // Host planning of one group: a RenderDesc per non-empty track (appended to `desc`), the
 // vertical band (the widest whose grey rows <= THESIA_VROWS and weights <= 4096 fit the LDS
 // tile for every track of the group) and the horizontal pass's tap / span bounds.
+// The single-pass display for a group (render_stripe_kernel): the instance (KV vertical taps,
+// A accumulator slots, FC frames per chunk) and the LDS bounds over every track, strip and row
+// block; g.stripe stays false where no instance covers the group (more than 16 vertical taps, more
+// than 16 columns meeting an 8-frame step, a chunk that does not fit the staging registers).
+struct StripeTrack {
+    const DevTaps *vt, *ht;
+    uint32_t T, H, nw, oz;
+    uint64_t rgb_off;
+};
+void plan_stripe(const std::vector<StripeTrack>& trk, uint32_t bins, uint32_t nheight, FusedGroup& g) {
+    g.stripe = false;
+    if (trk.empty()) return;
+    int kvmax = 0, amax = 0;
+    bool dword = true;
+    for (const StripeTrack& t : trk) {
+        kvmax = std::max(kvmax, t.vt->max_taps);
+        amax = std::max(amax, t.ht->st_maxna);
+        dword = dword && t.nw % 4 == 0 && t.rgb_off % 4 == 0;
+    }
+    const int kv = kvmax <= 8 ? 8 : kvmax <= 12 ? 12 : kvmax <= 16 ? 16 : 0;
+    const int slots = amax <= 8 && kv == 8 ? 8 : amax <= 16 ? 16 : 0;
+    if (!kv || !slots) return;
+    constexpr int kRows = 256, kPfCap = 256 * 16;  // render_stripe.hip kRows, kPf
+    const uint32_t strip = g.st_strip;
+    int tile = 1, nbmax = 0, hdr = 1, wts = 8;
+    for (const StripeTrack& t : trk) {
+        const int top = (int)t.H - (int)bins;
+        for (uint32_t R0 = 0; R0 < nheight; R0 += kRows) {
+            const uint32_t rlo = std::max(R0, t.oz), rhi = std::min(R0 + kRows, nheight);
+            if (rlo >= rhi) continue;
+            const int ya = t.vt->h_left[rlo], nt = t.vt->h_left[rhi - 1] + kv - ya;
+            tile = std::max(tile, nt);
+            nbmax = std::max(nbmax, std::min(ya + nt, (int)t.H) - std::max(ya, top));
+        }
+        const std::vector<int32_t>& sh = t.ht->h_st_hdr;
+        for (uint32_t c0 = 0; c0 < t.nw; c0 += strip) {
+            const uint32_t c1 = std::min(c0 + strip, t.nw);
+            const int s_lo = t.ht->h_left[c0] >> 3;
+            const int s_hi = (t.ht->h_left[c1 - 1] + t.ht->h_count[c1 - 1] - 1) >> 3;
+            hdr = std::max(hdr, s_hi - s_lo + 1);
+            wts = std::max(wts, sh[4 * s_hi + 2] + 8 * sh[4 * s_hi + 1] - sh[4 * s_lo + 2]);
+        }
+    }
+    int fc = 16;
+    if (fc * nbmax > kPfCap || render_stripe_lds_bytes(fc, tile, hdr, wts) > 65536) fc = 8;
+    if (fc * nbmax > kPfCap || render_stripe_lds_bytes(fc, tile, hdr, wts) > 98304) return;
+    g.stripe = true;
+    g.st_kv = kv;
+    g.st_slots = slots;
+    g.st_fc = fc;
+    g.st_tile = tile;
+    g.st_hdr = hdr;
+    g.st_wts = wts;
+    g.st_dword = dword;
+}
+
 int plan_fused_group(const float* d_spec, const uint64_t* row0, size_t bins, size_t n,
                      const float* up_ratio, const uint32_t* nwidth, uint32_t nheight,
-                     const uint64_t* rgb_off, std::vector<RenderDesc>& desc, FusedGroup& g, bool wide) {
+                     const uint64_t* rgb_off, std::vector<RenderDesc>& desc, FusedGroup& g, bool wide,
+                     bool stripe) {
     g.spec = d_spec;
     g.bins = (uint32_t)bins;
     g.desc0 = desc.size();
     std::vector<std::pair<const DevTaps*, uint32_t>> vts;  // (vertical taps, oz)
+    std::vector<StripeTrack> strk;
     for (size_t i = 0; i < n; ++i) {
         const float hf = roundf((float)bins * up_ratio[i]);  // display.rs:46
         const uint32_t H = hf > 0.f ? (uint32_t)hf : 0u;
@@ -1274,7 +1419,7 @@ int plan_fused_group(const float* d_spec, const uint64_t* row0, size_t bins, siz
         if (T == 0 || nwidth[i] == 0) continue;
         const DevTaps *vt = nullptr, *ht = nullptr;
         int rc = dev_taps(H, nheight, &vt);
-        if (!rc) rc = dev_taps(T, nwidth[i], &ht);
+        if (!rc) rc = stripe ? dev_taps_stepped(T, nwidth[i], &ht) : dev_taps(T, nwidth[i], &ht);
         if (rc) return rc;
         RenderDesc r{};
         r.spec_off = row0[i] * bins;
@@ -1288,11 +1433,13 @@ int plan_fused_group(const float* d_spec, const uint64_t* row0, size_t bins, siz
         r.vo = vt->offset.as<int32_t>(); r.vw = vt->weights.as<float>();
         r.hl = ht->left.as<int32_t>(); r.hc = ht->count.as<int32_t>();
         r.ho = ht->offset.as<int32_t>(); r.hw = ht->weights.as<float>();
+        r.hst = ht->st_hdr.as<int32_t>(); r.hsw = ht->st_w.as<float>();
         // oz: output rows whose taps end at or above the band's top row H - bins
         const int32_t top = (int32_t)H - (int32_t)bins;
         uint32_t oz = 0;
         while (oz < nheight && vt->h_left[oz] + vt->h_count[oz] <= top) ++oz;
         r.oz = oz;
+        if (stripe) strk.push_back(StripeTrack{vt, ht, T, H, nwidth[i], oz, rgb_off[i]});
         if (std::find(vts.begin(), vts.end(), std::make_pair(vt, oz)) == vts.end()) vts.emplace_back(vt, oz);
         g.tmp_tot += (uint64_t)r.ts * nheight;
         g.cost += (uint64_t)T * bins + 2ull * r.ts * nheight + (3ull * nwidth[i] * nheight) / 4;
@@ -1304,6 +1451,18 @@ int plan_fused_group(const float* d_spec, const uint64_t* row0, size_t bins, siz
         desc.push_back(r);
     }
     g.ndesc = desc.size() - g.desc0;
+    if (stripe) {
+        plan_stripe(strk, (uint32_t)bins, nheight, g);
+        if (g.stripe) {  // no intermediate: the group's workspace share and its cost change
+            uint64_t cost = 0;
+            for (size_t i = g.desc0; i < g.desc0 + g.ndesc; ++i) {
+                desc[i].tmp_off = 0;
+                cost += (uint64_t)desc[i].T * bins + (3ull * desc[i].nw * nheight) / 4;
+            }
+            g.tmp_tot = 0;
+            g.cost = cost;
+        }
+    }
     // taps per row padded to kv (a multiple of 4, zero weights): the tile holds the band's
     // supports plus kv rows, the weight table band x kv floats
     int kv = 4;
@@ -1409,7 +1568,7 @@ int render_rgb_fused(size_t n_groups, const float* const* d_specs, const uint64_
         size_t t0 = 0;
         for (size_t k = 0; k < n_groups; ++k) {
             rc = plan_fused_group(d_specs[k], row0s[k], bins[k], ns[k], up_ratio + t0, nwidth + t0, nheight,
-                                  rgb_off + t0, desc, groups[k], true);
+                                  rgb_off + t0, desc, groups[k], true, rpath == 0);
             if (rc) return rc;
             t0 += ns[k];
         }
@@ -1457,6 +1616,29 @@ int render_rgb_fused(size_t n_groups, const float* const* d_specs, const uint64_
     auto launch_group = [&](const FusedGroup& g, hipStream_t st) {
         for (size_t b = 0; b < g.ndesc; b += 65535) {  // grid.z limit
             const uint32_t nb = (uint32_t)std::min<size_t>(65535, g.ndesc - b);
+            if (g.stripe) {
+                StripeLaunch L{};
+                L.spec = g.spec;
+                L.bins = g.bins;
+                L.max = max;
+                L.min = min;
+                L.nh = nheight;
+                L.desc = ws.desc.as<RenderDesc>() + g.desc0 + b;
+                L.n = nb;
+                L.nw_max = g.nw_max;
+                L.strip = g.st_strip;
+                L.kv = g.st_kv;
+                L.slots = g.st_slots;
+                L.fc = g.st_fc;
+                L.tile_cap = g.st_tile;
+                L.hdr_cap = g.st_hdr;
+                L.wts_cap = g.st_wts;
+                L.dword_rgb = g.st_dword;
+                L.cmap = cmap_ptr;
+                L.rgb = d_rgb;
+                if (launch_render_stripe(L, st)) return set_error(THESIA_ERR_DEVICE, "render stripe launch failed");
+                continue;
+            }
             if (launch_render_batch2(g.spec, g.bins, max, min, ws.desc.as<RenderDesc>() + g.desc0 + b, nb,
                                      g.T_max, g.H_max, g.nw_max, nheight, g.h_taps, g.h_span, g.v_band,
                                      g.v_rows, g.v_kv, ws.tmp.as<float>(), cmap_ptr, d_rgb, st, h_dma,
@@ -1536,7 +1718,7 @@ int render_rgb_batch_device(const float* d_spec, const uint64_t* row0, size_t bi
     int crc = 0;
     const uint8_t* cmap_ptr = colormap_device(&crc);
     if (crc) return crc;
-    if (render_path() == 0) {
+    if (render_path() == 0 || render_path() == 3) {
         const size_t ns[1] = {n};
         const size_t bs[1] = {bins};
         return render_rgb_fused(1, &d_spec, &row0, bs, ns, up_ratio, nwidth, nheight, max, min, d_rgb,

@@ -135,6 +135,8 @@ struct Batch {
 int batch_create(Plan* plan, const thesia_batch_desc& d, Batch** out);
 int batch_run(Batch* b, hipStream_t s);
 int batches_run(Batch* const* b, size_t n, hipStream_t s);  // thesia_batches_run
+int batches_policy();  // thesia_set_batches_policy
+int set_batches_policy(int policy);
 int batch_set_option(Batch* b, int option, int64_t value);  // thesia_batch_set_option
 int ranges_read(const int* d_range, size_t n, float* mx, float* mn, int* nan, hipStream_t s);
 

@@ -86,6 +86,7 @@ struct StftLaunch {
     void* out = nullptr;  // packed rows: frame g at out + g * row_elems
     // scheduling / named alternatives (thesia_batch_set_option)
     int grid = 0;     // 0 => computed from occupancy, else at most this many blocks
+    float grid_share = 0.f;  // grid 0: this share of the occupancy wave (0 = all of it)
     // row-store method (stft3): 0 default (complex: whole 128-B lines; linear: LDS-
     // staged 16-byte), 1 the other one (complex: LDS-staged 16-byte; linear: lane-wise), 2 complex
     // whole lines, 3 complex lane-wise 8-byte; 1 and 3 at n_fft 2048 stereo f32 only
@@ -181,6 +182,11 @@ struct RenderDesc {
     const float* vw;
     const int32_t *hl, *hc, *ho;
     const float* hw;
+    // the horizontal taps regrouped by 8-frame step (render_stripe_kernel): per step s of the
+    // track, {ca, na, woff, 0} = the columns ca .. ca + na - 1 whose supports meet frames
+    // [8s, 8s + 8), and at hsw + woff their na x 8 weights (zero outside a column's support)
+    const int32_t* hst;
+    const float* hsw;
 };
 int launch_render_batch(const float* spec, uint32_t bins, float max, float min,
                         const RenderDesc* d_desc, uint32_t n, uint32_t T_max, uint32_t H_max,
@@ -197,6 +203,31 @@ int launch_render_batch2(const float* spec, uint32_t bins, float max, float min,
                          int v_rows, int v_kv, float* tmp, const uint8_t* cmap, uint8_t* rgb,
                          hipStream_t s, bool h_dma = true,  // h_dma: the LDS-DMA horizontal pass
                          int v_fpl = 1);  // frames per lane of the vertical pass (1, or 4: wide)
+// The single-pass display (render_stripe_kernel, render_stripe.hip): grey + vertical Lanczos3 +
+// horizontal Lanczos3 + colormap in one kernel, the f32 intermediate never leaving registers.
+// A block owns `strip` output columns x 256 output rows of one track; its geometry bounds
+// (host, plan_stripe_group): kv vertical taps (8, 12 or 16, zero-padded), at most `slots`
+// columns meeting one 8-frame step (8 or 16), fc frames per staged chunk (8 or 16), at most
+// tile_cap grey rows per block, hdr_cap steps and wts_cap step weights per strip. -2 when no
+// instance fits.
+struct StripeLaunch {
+    const float* spec;
+    uint32_t bins;
+    float max, min;
+    uint32_t nh;
+    const RenderDesc* desc;
+    uint32_t n;          // tracks (grid.z)
+    uint32_t nw_max;
+    uint32_t strip;      // output columns per block (multiple of 4)
+    int kv, slots, fc;
+    int tile_cap, hdr_cap, wts_cap;
+    bool dword_rgb;      // every track's nw and rgb_off are multiples of 4 (dword RGB stores)
+    const uint8_t* cmap;
+    uint8_t* rgb;
+};
+int launch_render_stripe(const StripeLaunch& L, hipStream_t s);
+int render_stripe_lds_bytes(int fc, int tile_cap, int hdr_cap, int wts_cap);
+
 // LDS bytes of the wide vertical pass (grey_vert_wide_kernel<fpl>) for a band / tile / kv
 int grey_vert_wide_lds_bytes(int fpl, uint32_t band, int tile_cap, int kv);
 int launch_spec_to_grey(const float* spec, uint32_t T, uint32_t bins, uint32_t H, float max,

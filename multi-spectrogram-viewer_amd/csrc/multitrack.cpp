@@ -174,8 +174,9 @@ int MultiTrack::add_tracks(const std::vector<uint64_t>& ids, const std::vector<P
         if (rc) return rc;
         g.batch.reset(b);
         // the viewer path computes in the reference's operation order (stftx_kernel): its
-        // images are the oracle pipeline's bytes
-        rc = batch_set_option(b, THESIA_BATCH_OPT_KERNEL, 9);
+        // images are the oracle pipeline's bytes; opt-in (set_fast): the automatic streaming
+        // kernel (stft3 at the viewer geometries)
+        rc = batch_set_option(b, THESIA_BATCH_OPT_KERNEL, fast_ ? 0 : 9);
         if (!rc) rc = batch_run(b, s);
         if (rc) return rc;
         g.spec = spec->as<float>();

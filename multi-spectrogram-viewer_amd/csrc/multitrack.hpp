@@ -61,6 +61,11 @@ class MultiTrack {
     MultiTrack();
     ~MultiTrack();
     int set_setting(float win_ms, size_t t_overlap, size_t f_overlap, int freq_scale, float db_range);
+    // 0 (default): spectrograms from the reference-order kernel (images = the oracle pipeline's
+    // bytes); 1: the batch engine's automatic streaming kernel (tolerance contract, SURVEY §8c:
+    // end to end <= 1 LSB on <= 1e-4 of the pixels). Applies to the tracks added afterwards.
+    void set_fast(bool fast) { fast_ = fast; }
+    bool fast() const { return fast_; }
     int add_tracks(const std::vector<uint64_t>& ids, const std::vector<PcmIn>& pcm, int* changed);
     int remove_track(uint64_t id, int* changed);
     // images straight into the caller's buffer: *needed = bytes; THESIA_ERR_BUFFER_TOO_SMALL
@@ -93,6 +98,7 @@ class MultiTrack {
     void compact_pools();
 
     Setting set_;
+    bool fast_ = false;
     std::map<uint64_t, Track> tracks_;
     std::map<uint32_t, Plan*> plans_;  // windows / mel_fbs per sr (lib.rs:76-77)
     float max_db_ = -INFINITY, min_db_ = INFINITY, max_sec_ = 0.f;

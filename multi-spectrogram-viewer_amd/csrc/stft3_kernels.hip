@@ -90,7 +90,7 @@ static int launch3_k(const StftLaunch& a, hipStream_t stream) {
     if (a.total_frames == 0) return 0;
     constexpr uint64_t per_block = Geo3<NC, WV>::STREAMS;
     int grid = grid_for(reinterpret_cast<const void*>(kern), kBlock, lds,
-                        (a.total_frames + per_block - 1) / per_block, a.grid);
+                        (a.total_frames + per_block - 1) / per_block, a.grid, a.grid_share);
     const uint64_t streams = (uint64_t)grid * per_block;
     const uint64_t fps = (a.total_frames + streams - 1) / streams;
     grid = (int)((a.total_frames + fps * per_block - 1) / (fps * per_block));

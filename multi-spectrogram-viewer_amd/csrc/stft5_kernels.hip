@@ -27,6 +27,7 @@
 // two frames of a wave keep their LDS regions on opposite halves of the 64 banks.
 #include "stft3_core.hpp"
 
+#include <cstdlib>
 #include <type_traits>
 
 namespace thesia {
@@ -221,9 +222,14 @@ __device__ __forceinline__ void melp5(const StftLaunch& a, float* region, const 
 }
 
 // OK: 0 complex, 1 linear kinds, 2 mel kinds. C: 1 mono, 2 stereo (interleaved); INF: f32 / s16.
-template <int OK, int C, int INF>
+// VAR bit 0 (experiment): the register ring rotates instead of shifting -- logical point group t
+// (points 8 t .. 8 t + 7 of the lane's 32) lives in physical group (t + ph) & 3, the hop's new
+// samples overwrite the oldest group and ph advances (no 48 v_mov per frame pair); the first
+// radix-4 level, the only reader, is compiled once per phase behind a uniform branch.
+template <int OK, int C, int INF, int VAR = 0>
 __global__ void __launch_bounds__(Geo5::BLOCK, Geo5::WV / 4)
 stft5_kernel(StftLaunch a, uint64_t fps, int rs) {
+    constexpr bool kRot = (VAR & 1) != 0;
     using G = Geo5;
     using CK = Chunk<C, INF>;
     using CT = typename CK::T;
@@ -233,12 +239,13 @@ stft5_kernel(StftLaunch a, uint64_t fps, int rs) {
     constexpr bool kStage = OK == 1;  // linear kinds: LDS-staged 16-byte row stores
 
     extern __shared__ __attribute__((aligned(16))) float lds[];
+    constexpr int kTab = G::TAB_FLOATS + (kRot ? 3 * G::TW_FLOATS : 0);
     float* wtl = lds;
     float2* twtab = reinterpret_cast<float2*>(lds + G::WL_FLOATS);
-    float* work = lds + G::TAB_FLOATS;
+    float* work = lds + kTab;
     // mel tables: the packed stream (meta rows, then weight rows) or the rounds' chunk stream
     const bool packed = OK == 2 && a.melp_chunks > 0;
-    float4* mel_lds = reinterpret_cast<float4*>(lds + G::TAB_FLOATS + G::STREAMS * rs);
+    float4* mel_lds = reinterpret_cast<float4*>(lds + kTab + G::STREAMS * rs);
     int4* pm_lds = reinterpret_cast<int4*>(mel_lds);
     float4* pw_lds = mel_lds + (packed ? (a.melp_chunks + 2) * L : 0);
     int* k0_lds = reinterpret_cast<int*>(mel_lds + (OK == 2 && !packed ? a.mel4_rows * L : 0));
@@ -264,10 +271,16 @@ stft5_kernel(StftLaunch a, uint64_t fps, int rs) {
         for (int i = threadIdx.x; i < a.mel4_rounds; i += kBlock) rd_lds[i] = a.mel4_round[i];
         for (int i = threadIdx.x; i < a.mel_chunks * L; i += kBlock) xo_lds[i] = a.mel_xo[i];
     }
-    // stage-1 twiddles with k1 pairs interleaved: [k1/2][j][k1&1]
-    for (int i = threadIdx.x; i < P * L; i += kBlock) {
-        const int k1 = i / L, jj = i % L;
-        twtab[((k1 >> 1) * L + jj) * 2 + (k1 & 1)] = a.tw3[i];
+    // stage-1 twiddles with k1 pairs interleaved: [k1/2][j][k1&1]; kRot: one table per ring
+    // phase ph, the entries times i^(ph k1) (exact: a swap and negations)
+    for (int i = threadIdx.x; i < (kRot ? 4 : 1) * P * L; i += kBlock) {
+        const int phi = i / (P * L), ii = i % (P * L), k1 = ii / L, jj = ii % L;
+        float2 t = a.tw3[ii];
+        const int r = (phi * k1) & 3;
+        if (r == 1) t = make_float2(-t.y, t.x);
+        else if (r == 2) t = make_float2(-t.x, -t.y);
+        else if (r == 3) t = make_float2(t.y, -t.x);
+        twtab[phi * P * L + ((k1 >> 1) * L + jj) * 2 + (k1 & 1)] = t;
     }
     // untangle bases: slots 0..7 start at bin kb_lo (lane 0: 32), slots 8..15 at bin j
     float2 ub_lo = a.sincos[lane0 ? 32 : j], ub_hi = a.sincos[j];
@@ -293,6 +306,7 @@ stft5_kernel(StftLaunch a, uint64_t fps, int rs) {
     float2 raw[P];
     CT pre[SH];
     bool pre_ok = false;
+    int ph = 0;  // kRot: physical group of logical group 0 (wave-uniform)
     int hint = -1;
     FI g_beg = 1, g_end = 0;
     uint64_t base = 0;
@@ -326,7 +340,21 @@ stft5_kernel(StftLaunch a, uint64_t fps, int rs) {
             start = (SI)(g - g_beg) * hop - NC;  // half_win = NC, pad_left = 0
         }
         // ---- the frame's raw samples: shift by SH points + the prefetched hop ----
-        if (pre_ok) {
+        if (pre_ok && kRot) {
+            // the oldest group takes the new hop; the ring's origin moves one group on
+            static_assert(!kRot || P == 4 * SH, "phase ring: four groups of one hop");
+            const int p0 = __builtin_amdgcn_readfirstlane(ph);
+            auto ins = [&](auto gc) {
+                constexpr int gi = decltype(gc)::value;
+#pragma unroll
+                for (int q = 0; q < SH; ++q) raw[gi * SH + q] = CK::mix(pre[q]);
+            };
+            if (p0 == 0) ins(std::integral_constant<int, 0>{});
+            else if (p0 == 1) ins(std::integral_constant<int, 1>{});
+            else if (p0 == 2) ins(std::integral_constant<int, 2>{});
+            else ins(std::integral_constant<int, 3>{});
+            ph = (p0 + 1) & 3;
+        } else if (pre_ok) {
 #pragma unroll
             for (int n1 = 0; n1 < P - SH; ++n1) raw[n1] = raw[n1 + SH];
 #pragma unroll
@@ -347,6 +375,7 @@ stft5_kernel(StftLaunch a, uint64_t fps, int rs) {
 #pragma unroll
             for (int n1 = 0; n1 < P; ++n1) raw[n1] = make_float2(0.f, 0.f);
         }
+        if (!(pre_ok && kRot)) ph = 0;  // a reloaded ring is in logical order
         MARK5(loaded, 0);
         // ---- prefetch the next frame's hop of new samples (its points P-SH .. P-1) right
         // away: a whole frame to land, as stft3 ----
@@ -369,9 +398,17 @@ stft5_kernel(StftLaunch a, uint64_t fps, int rs) {
         // are formed once and the ones of inputs 0 and 1 ride in the butterfly fmas (12 VALU per
         // butterfly instead of 16)
         float2 v[P];
+        // kRot: the DFT-32 runs over the ring in PHYSICAL order, the window of each physical
+        // group read from its logical row ((g - ph) & 3); the result is the DFT of the frame
+        // rotated by 8 ph points, i.e. Y[k1] (-i)^(ph k1), undone exactly by the stage-1
+        // twiddle table of phase ph (W^{j k1} i^(ph k1): a swap / negation of the entries)
+        const int phs = kRot ? __builtin_amdgcn_readfirstlane(ph) : 0;
+        const float4* wg[4] = {wrow + 4 * ((0 - phs) & 3), wrow + 4 * ((1 - phs) & 3),
+                               wrow + 4 * ((2 - phs) & 3), wrow + 4 * ((3 - phs) & 3)};
+        {
         static_for<0, 4>([&](auto jc) {
             constexpr int jp = decltype(jc)::value;
-            const float4 wq[4] = {wrow[jp], wrow[jp + 4], wrow[jp + 8], wrow[jp + 12]};
+            const float4 wq[4] = {wg[0][jp], wg[1][jp], wg[2][jp], wg[3][jp]};
             static_for<0, 2>([&](auto hc) {
                 constexpr int h = decltype(hc)::value, jj = 2 * jp + h;
                 auto wv = [&](int t) {
@@ -391,6 +428,7 @@ stft5_kernel(StftLaunch a, uint64_t fps, int rs) {
                 v[jj + 24] = twc<32, 3 * jj>(csub(t1, t3));
             });
         });
+        }
         pin(v);
         dif_fft<8, 1, 0, P>(v);
         dif_fft<8, 1, 8, P>(v);
@@ -399,7 +437,7 @@ stft5_kernel(StftLaunch a, uint64_t fps, int rs) {
         pin(v);
         MARK5(stage1, 1);
         {
-            const float4* tp = reinterpret_cast<const float4*>(twtab) + wj;
+            const float4* tp = reinterpret_cast<const float4*>(twtab) + wj + phs * (P / 2 * L);
             static_for<0, P / 2 / G::TWC>([&](auto cc) {
                 constexpr int c0 = decltype(cc)::value * G::TWC;
                 __builtin_amdgcn_sched_barrier(0);
@@ -576,33 +614,40 @@ stft5_kernel(StftLaunch a, uint64_t fps, int rs) {
 // --------------------------------------------------------------------------------------
 // host-side dispatch
 // --------------------------------------------------------------------------------------
-template <int OK>
+template <int OK, int VAR = 0>
 static int lds5_bytes(const StftLaunch& a, int rs) {
     const int mel = OK != 2 ? 0
                     : a.melp_chunks > 0 ? ((a.melp_chunks + 2) + (a.melp_chunks + 1) * a.melp_steps) * Geo5::L * 4
                     : (a.mel4_rows * 4 + a.mel4_rounds + a.mel_chunks) * Geo5::L + 2 * a.mel4_rounds;
-    return (Geo5::TAB_FLOATS + Geo5::STREAMS * rs + mel) * 4;
+    const int tab = Geo5::TAB_FLOATS + ((VAR & 1) ? 3 * Geo5::TW_FLOATS : 0);
+    return (tab + Geo5::STREAMS * rs + mel) * 4;
 }
-template <int OK>
+template <int OK, int VAR = 0>
 static int region_stride5(const StftLaunch& a) {
     // the packed mel stream stages the frame's mels behind the |X| row: full regions only
     if (OK == 2 && a.melp_chunks > 0) return Geo5::RS;
-    return lds5_bytes<OK>(a, Geo5::RS) <= 163840 ? Geo5::RS : Geo5::RS_MIN;
+    return lds5_bytes<OK, VAR>(a, Geo5::RS) <= 163840 ? Geo5::RS : Geo5::RS_MIN;
 }
 
-template <int OK, int C, int INF>
+template <int OK, int C, int INF, int VAR = 0>
 static int launch5_k(const StftLaunch& a, hipStream_t stream) {
-    const int rs = region_stride5<OK>(a);
-    const int lds = lds5_bytes<OK>(a, rs);
+#ifdef THESIA_EXPERIMENTS
+    if constexpr (VAR == 0 && C == 2 && INF == IN_F32) {
+        const char* e = getenv("THESIA_STFT_VARIANT");
+        if (e && atoi(e) == 1) return launch5_k<OK, C, INF, 1>(a, stream);  // phase ring
+    }
+#endif
+    const int rs = region_stride5<OK, VAR>(a);
+    const int lds = lds5_bytes<OK, VAR>(a, rs);
     if (lds > 163840) return -2;
-    auto kern = stft5_kernel<OK, C, INF>;
+    auto kern = stft5_kernel<OK, C, INF, VAR>;
     if (hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
                             hipFuncAttributeMaxDynamicSharedMemorySize, lds) != hipSuccess)
         return -1;
     if (a.total_frames == 0) return 0;
     constexpr uint64_t per_block = Geo5::STREAMS;
     int grid = grid_for(reinterpret_cast<const void*>(kern), Geo5::BLOCK, lds,
-                        (a.total_frames + per_block - 1) / per_block, a.grid);
+                        (a.total_frames + per_block - 1) / per_block, a.grid, a.grid_share);
     const uint64_t streams = (uint64_t)grid * per_block;
     const uint64_t fps = (a.total_frames + streams - 1) / streams;
     grid = (int)((a.total_frames + fps * per_block - 1) / (fps * per_block));

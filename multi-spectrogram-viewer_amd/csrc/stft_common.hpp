@@ -3,6 +3,8 @@
 // sizes). Input decode / downmix, track lookup, dB epilogue.
 #pragma once
 
+#include <algorithm>
+
 #include "device_fft.hpp"
 #include "kernels.hpp"
 
@@ -195,7 +197,10 @@ __device__ __forceinline__ void twiddle_bases(const StftLaunch& a, int j, float2
 }
 
 // Grid for a persistent launch: resident blocks per CU x CUs, capped by the tile count.
-inline int grid_for(const void* kern, int block, int lds, uint64_t n_tiles, int grid_req) {
+// grid_req > 0: at most that many blocks; else one occupancy wave of the device, scaled by
+// share in (0, 1] when several launches run side by side (thesia_batches_run: each batch on its
+// share of the CUs, so its frame streams walk longer)
+inline int grid_for(const void* kern, int block, int lds, uint64_t n_tiles, int grid_req, float share = 0.f) {
     int grid = grid_req;
     if (grid <= 0) {
         int dev = 0, cus = 256, per_cu = 1;
@@ -205,6 +210,7 @@ inline int grid_for(const void* kern, int block, int lds, uint64_t n_tiles, int 
             per_cu < 1)
             per_cu = 1;
         grid = cus * per_cu;
+        if (share > 0.f && share < 1.f) grid = std::max(1, (int)((float)grid * share + 0.5f));
     }
     if ((uint64_t)grid > n_tiles) grid = (int)n_tiles;
     return grid;

@@ -342,7 +342,7 @@ static int launch_k(const StftLaunch& a, hipStream_t stream) {
     }
     const uint64_t n_tiles = (a.total_frames + Geo<NC>::PASS_FRAMES - 1) / Geo<NC>::PASS_FRAMES;
     if (n_tiles == 0) return 0;
-    int grid = grid_for(reinterpret_cast<const void*>(kern), kBlock, lds, n_tiles, a.grid);
+    int grid = grid_for(reinterpret_cast<const void*>(kern), kBlock, lds, n_tiles, a.grid, a.grid_share);
     const uint64_t tpb = (n_tiles + grid - 1) / grid;
     grid = (int)((n_tiles + tpb - 1) / tpb);
     hipLaunchKernelGGL(kern, dim3(grid), dim3(kBlock), lds, stream, a, tpb);

@@ -93,6 +93,7 @@ _SIGS = {
     "thesia_batch_kernel": (_i, [_vp, C.POINTER(C.c_int)]),
     "thesia_batch_set_option": (_i, [_vp, _i, C.c_int64]),
     "thesia_batch_ranges_read": (_i, [C.c_void_p, _sz, _fp, _fp, C.POINTER(C.c_int)]),
+    "thesia_set_batches_policy": (_i, [_i]),
     "thesia_set_render_path": (_i, [_i]),
     "thesia_minmax_device": (_i, [C.c_void_p, C.c_uint64, C.POINTER(C.c_float), C.POINTER(C.c_float),
                                   C.POINTER(C.c_int)]),
@@ -112,6 +113,7 @@ _SIGS = {
     "thesia_open_audio_file": (_i, [C.c_char_p, _fp, _sz, C.POINTER(_sz), C.POINTER(_u32), C.POINTER(_u32)]),
     "thesia_mt_create": (_i, [C.POINTER(_vp)]),
     "thesia_mt_destroy": (None, [_vp]),
+    "thesia_mt_set_fast": (_i, [_vp, _i]),
     "thesia_mt_set_setting": (_i, [_vp, _f, _sz, _sz, _i, _f]),
     "thesia_mt_add_tracks": (_i, [_vp, _u64p, _sz, C.c_char_p, C.POINTER(_i)]),
     "thesia_mt_add_tracks_pcm": (_i, [_vp, _u64p, _sz, C.POINTER(_fp), _u64p, C.POINTER(_u32),

@@ -54,11 +54,15 @@ class MultiTrack:
     """lib.rs:72-365. Tracks, spectrograms and grey images live in HBM."""
 
     def __init__(self, freq_scale: FreqScale = FreqScale.Mel, win_ms: float = 40.0,
-                 t_overlap: int = 4, f_overlap: int = 1, db_range: float = 120.0):
+                 t_overlap: int = 4, f_overlap: int = 1, db_range: float = 120.0, fast: bool = False):
+        """fast: spectrograms from the streaming kernel (thesia_mt_set_fast; SURVEY §8c's
+        end-to-end contract) instead of the reference-order kernel (the oracle's bytes)."""
         self.h = C.c_void_p()
         check(lib.thesia_mt_create(C.byref(self.h)))
         if (freq_scale, win_ms, t_overlap, f_overlap, db_range) != (FreqScale.Mel, 40.0, 4, 1, 120.0):
             check(lib.thesia_mt_set_setting(self.h, win_ms, t_overlap, f_overlap, int(freq_scale), db_range))
+        if fast:
+            check(lib.thesia_mt_set_fast(self.h, 1))
         self.freq_scale = freq_scale
 
     def close(self) -> None:

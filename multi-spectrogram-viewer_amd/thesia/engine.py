@@ -237,6 +237,12 @@ def run_batches(batches, stream=None) -> None:
     check(lib.thesia_batches_run(arr, len(batches), stream))
 
 
+def set_batches_policy(policy: int) -> None:
+    """thesia_set_batches_policy: 1 (default) = concurrent batches share one occupancy wave by
+    work; 0 = each batch sized for the whole device."""
+    check(lib.thesia_set_batches_policy(policy))
+
+
 def set_render_path(path: int) -> None:
     """0: batched display launches (default); 1: per-track launches (cross-check)."""
     check(lib.thesia_set_render_path(path))

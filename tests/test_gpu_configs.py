@@ -145,7 +145,9 @@ def test_c5_mixed_rate_render_pipeline():
         assert r.rgb.tobytes() == img.tobytes(), (t.sr, t.n_fft)  # display path bit-exact
 
 
-@pytest.mark.parametrize("path", [0, 1, 2])  # two-kernel (LDS-DMA horizontal; wide vertical pass for upsampling groups) / per-track / three-stage
+# 0: single-pass stripes where the geometry allows, else two kernels; 1: per-track; 2: three-stage;
+# 3: two kernels for every group (LDS-DMA horizontal; wide vertical pass for upsampling groups)
+@pytest.mark.parametrize("path", [0, 1, 2, 3])
 @pytest.mark.parametrize("px_per_sec", [73.0, 30.0, 9.0, 2.0])  # 30: 17-64 taps; 9, 2: wider spans
 @pytest.mark.parametrize("nheight", [90, 400, 600])  # 400, 600: H -> nheight downsampling ~2.5, taller
 def test_render_batch_ragged_groups(path, px_per_sec, nheight):
@@ -178,6 +180,26 @@ def _ragged(px_per_sec, nheight):
         grey = O.spec_to_grey(r.db, up, gmax, gmin)
         img, _ = O.grey_to_rgb(grey, r.nwidth, nheight)
         assert r.rgb.tobytes() == img.tobytes(), (t.sr, t.n_fft, t.pcm.shape)
+
+
+@pytest.mark.parametrize("path", [0, 3])
+def test_c5_geometry_500_rows(path):
+    """The C5 display geometry (100 px/s x 500 rows, every (rate, n_fft) pair) at 3 s per track:
+    the single-pass stripe kernel runs the 7 groups whose images downsample along time (two row
+    blocks of 256, strips of 64 columns, dword RGB stores: nwidth 300), the others the two-kernel
+    path; bytes equal the oracle display of the device's own dB."""
+    engine.set_render_path(path)
+    try:
+        tracks = pipeline.c5_tracks(12, seconds=3.0)
+        out = pipeline.render_tracks(tracks, px_per_sec=100.0, nheight=500, keep_db=True)
+    finally:
+        engine.set_render_path(0)
+    gmax, gmin, max_sr = shard.global_db_range(max(r.spec_max for r in out), min(r.spec_min for r in out),
+                                               max(t.sr for t in tracks))
+    for t, r in zip(tracks, out):
+        up = shard.up_ratio(t.sr, max_sr, freq_scale_mel=False)
+        img, _ = O.grey_to_rgb(O.spec_to_grey(r.db, up, gmax, gmin), r.nwidth, 500)
+        assert r.rgb.tobytes() == img.tobytes(), (t.sr, t.n_fft)
 
 
 def test_render_pinned_readback_matches_pageable():

@@ -103,15 +103,17 @@ def test_e2e_rgb_c5_generator():
     assert worst <= E2E_MAX_LSB and diff_px / total_px <= E2E_MAX_FRAC, (worst, diff_px, total_px)
 
 
+@pytest.mark.parametrize("fast", [False, True])
 @pytest.mark.parametrize("scale", [thesia.FreqScale.Mel, thesia.FreqScale.Linear])
-def test_e2e_rgb_multitrack_samples(scale):
+def test_e2e_rgb_multitrack_samples(scale, fast):
     """MultiTrack (lib.rs:170-298) on the reference's sample excerpts + the 48 kHz substitute:
-    get_spec_image bytes vs the oracle pipeline from the PCM."""
+    get_spec_image bytes vs the oracle pipeline from the PCM; fast = the streaming kernel at the
+    viewer's geometries (thesia_mt_set_fast) instead of the reference-order one."""
     z = np.load(fixtures.GOLDEN + "/samples_excerpt.npz")
     tags = ["8k", "16k", "22k05", "24k", "44k1"]
     pcm = [fixtures.s16_to_f32(z[f"pcm_{t}"]) for t in tags] + [fixtures.s16_to_f32(fixtures.c1_substitute()[:72000])]
     srs = [int(z[f"sr_{t}"]) for t in tags] + [48000]
-    mt = thesia.MultiTrack(freq_scale=scale)
+    mt = thesia.MultiTrack(freq_scale=scale, fast=fast)
     mt.add_tracks_pcm(list(range(len(pcm))), pcm, srs)
     dbs = []
     for x, sr in zip(pcm, srs):
