@@ -513,7 +513,7 @@ def main_c5(args, ws, rank, pg, device):
                     for _ in range(3):
                         p.run_spectrograms()
                 res[q].append(tm.ms / 3)
-        engine.set_batches_policy(1)
+        engine.set_batches_policy(0)
         pol_ms = {str(q): {"median": float(np.median(t)), "min": float(min(t))} for q, t in res.items()}
     if args.render_paths:
         import numpy as np

@@ -980,7 +980,7 @@ int batches_run(Batch* const* b, size_t n, hipStream_t s) {
     return rc ? rc : jrc;
 }
 
-static int g_batches_policy = 1;  // thesia_set_batches_policy
+static int g_batches_policy = 0;  // thesia_set_batches_policy
 int batches_policy() { return __atomic_load_n(&g_batches_policy, __ATOMIC_RELAXED); }
 int set_batches_policy(int policy) {
     if (policy < 0 || policy > 1) return set_error(THESIA_ERR_INVALID_ARG, "batches policy must be 0 or 1");
@@ -1059,10 +1059,11 @@ struct DevTaps {
     int max_taps = 0;
     std::vector<int32_t> h_left, h_count;  // host copies (block spans of the fused render)
     // the taps regrouped by 8-frame step for render_stripe_kernel (RenderDesc::hst / hsw), built
-    // on first use: per step {ca, na, woff, 0} and the na x 8 weights at woff
-    DevBuf st_hdr, st_w;
-    int st_maxna = 0;  // most columns meeting one step
-    std::vector<int32_t> h_st_hdr;
+    // on first use per slot count A (8, 12, 16): per step its first column ca, and the weights
+    // [step][frame u][slot a] of columns ca + a (+0 outside a column's support and past na)
+    int st_maxna = -1;  // most columns meeting one step (-1: not computed yet)
+    std::vector<int32_t> h_st_ca;
+    DevBuf st_ca[3], st_w[3];
 };
 
 static int dev_taps(uint32_t n, uint32_t nn, const DevTaps** out) {
@@ -1092,48 +1093,52 @@ static int dev_taps(uint32_t n, uint32_t nn, const DevTaps** out) {
 }
 
 // The stepped form of an (n -> nn) tap table: step s covers frames [8s, 8s + 8); its columns are
-// those whose support [l, l + cnt) meets the step (ca .. ca + na - 1: supports are monotone in
-// the column), each with the 8 weights of the step's frames (the column's weight where the frame
-// is inside its support, +0 elsewhere), in column order.
-static int build_stepped(uint32_t n, uint32_t nn, DevTaps* d) {
-    const Taps t = lanczos3_taps(n, nn);
+// those whose support [l, l + cnt) meets the step, ca .. ca + na - 1 (supports are monotone in
+// the column); render_stripe_kernel's slot a of the step holds column ca + a, with the 8 weights
+// of the step's frames (the column's weight where the frame is inside its support, +0 elsewhere
+// and for a >= na), laid out [step][frame][slot].
+static void stepped_cols(const DevTaps& t, uint32_t n, uint32_t nn, std::vector<int32_t>* ca_out, int* maxna) {
     const int nsteps = (int)((n + 7) / 8);
-    std::vector<int32_t> hdr(4 * (size_t)nsteps, 0);
-    std::vector<float> w;
-    int ca = 0, cb = -1, maxna = 0;
+    ca_out->assign(nsteps, 0);
+    int ca = 0, cb = -1, mx = 0;
     for (int s = 0; s < nsteps; ++s) {
-        while (ca < (int)nn && ((t.left[ca] + t.count[ca] - 1) >> 3) < s) ++ca;
-        while (cb + 1 < (int)nn && (t.left[cb + 1] >> 3) <= s) ++cb;
-        const int na = cb >= ca ? cb - ca + 1 : 0;
-        hdr[4 * s] = ca;
-        hdr[4 * s + 1] = na;
-        hdr[4 * s + 2] = (int32_t)w.size();
-        for (int k = 0; k < na; ++k) {
-            const int c = ca + k, l = t.left[c], cnt = t.count[c];
-            for (int u = 0; u < 8; ++u) {
-                const int f = 8 * s + u;
-                w.push_back(f >= l && f < l + cnt ? t.weights[t.offset[c] + (f - l)] : 0.0f);
-            }
-        }
-        maxna = std::max(maxna, na);
+        while (ca < (int)nn && ((t.h_left[ca] + t.h_count[ca] - 1) >> 3) < s) ++ca;
+        while (cb + 1 < (int)nn && (t.h_left[cb + 1] >> 3) <= s) ++cb;
+        (*ca_out)[s] = ca;
+        mx = std::max(mx, cb >= ca ? cb - ca + 1 : 0);
     }
-    if (w.empty()) w.push_back(0.0f);
-    int rc = d->st_hdr.upload(hdr.data(), hdr.size() * 4);
-    if (!rc) rc = d->st_w.upload(w.data(), w.size() * 4);
-    if (rc) return rc;
-    d->st_maxna = maxna;
-    d->h_st_hdr = std::move(hdr);
-    return THESIA_OK;
+    *maxna = mx;
 }
 
-static int dev_taps_stepped(uint32_t n, uint32_t nn, const DevTaps** out) {
+static int dev_taps_stepped(uint32_t n, uint32_t nn, int slots, const DevTaps** out) {
     const DevTaps* t = nullptr;
     int rc = dev_taps(n, nn, &t);
     if (rc) return rc;
     static std::mutex mu;
     std::lock_guard<std::mutex> lk(mu);
     DevTaps* d = const_cast<DevTaps*>(t);  // the cache owns it; only this function adds the steps
-    if (!d->st_hdr.p && (rc = build_stepped(n, nn, d))) return rc;
+    if (d->st_maxna < 0) stepped_cols(*d, n, nn, &d->h_st_ca, &d->st_maxna);
+    const int k = slots / 4 - 2;
+    if (slots > 0 && (k < 0 || k > 2 || slots % 4)) return set_error(THESIA_ERR_INVALID_ARG, "stepped taps: 8, 12 or 16 slots");
+    if (slots > 0 && !d->st_w[k].p) {
+        const Taps tp = lanczos3_taps(n, nn);
+        const int nsteps = (int)d->h_st_ca.size();
+        std::vector<float> w((size_t)nsteps * 8 * slots, 0.0f);
+        for (int s = 0; s < nsteps; ++s)
+            for (int a = 0; a < slots; ++a) {
+                const int c = d->h_st_ca[s] + a;
+                if (c >= (int)nn) break;
+                const int l = tp.left[c], cnt = tp.count[c];
+                for (int u = 0; u < 8; ++u) {
+                    const int f = 8 * s + u;
+                    if (f >= l && f < l + cnt) w[((size_t)s * 8 + u) * slots + a] = tp.weights[tp.offset[c] + (f - l)];
+                }
+            }
+        if (w.empty()) w.push_back(0.0f);
+        rc = d->st_ca[k].upload(d->h_st_ca.data(), std::max<size_t>(d->h_st_ca.size(), 1) * 4);
+        if (!rc) rc = d->st_w[k].upload(w.data(), w.size() * 4);
+        if (rc) return rc;
+    }
     *out = d;
     return THESIA_OK;
 }
@@ -1339,7 +1344,7 @@ struct FusedGroup {
     // geometry (plan_stripe); then no intermediate is formed
     bool stripe = false;
     uint32_t st_strip = 64;
-    int st_kv = 0, st_slots = 0, st_fc = 0, st_tile = 0, st_hdr = 0, st_wts = 0;
+    int st_kv = 0, st_slots = 0, st_fc = 0, st_npf = 0, st_waves = 4, st_tile = 0, st_hdr = 0, st_wts = 0;
     bool st_dword = false;
 };
 
@@ -1361,41 +1366,53 @@ void plan_stripe(const std::vector<StripeTrack>& trk, uint32_t bins, uint32_t nh
     int kvmax = 0, amax = 0;
     bool dword = true;
     for (const StripeTrack& t : trk) {
+        if ((uint64_t)t.T * bins >= (1ull << 32)) return;  // the kernel's 32-bit row offsets
         kvmax = std::max(kvmax, t.vt->max_taps);
         amax = std::max(amax, t.ht->st_maxna);
         dword = dword && t.nw % 4 == 0 && t.rgb_off % 4 == 0;
     }
     const int kv = kvmax <= 8 ? 8 : kvmax <= 12 ? 12 : kvmax <= 16 ? 16 : 0;
-    const int slots = amax <= 8 && kv == 8 ? 8 : amax <= 16 ? 16 : 0;
+    const int slots = amax <= 8 ? 8 : amax <= 12 ? 12 : amax <= 16 ? 16 : 0;
     if (!kv || !slots) return;
-    constexpr int kRows = 256, kPfCap = 256 * 16;  // render_stripe.hip kRows, kPf
+    constexpr int kWaveRows = 64;  // render_stripe.hip: lane = row, a wave's rows stage their own tile
     const uint32_t strip = g.st_strip;
-    int tile = 1, nbmax = 0, hdr = 1, wts = 8;
+    int tile = 1, nbmax = 0, hdr = 1;
     for (const StripeTrack& t : trk) {
         const int top = (int)t.H - (int)bins;
-        for (uint32_t R0 = 0; R0 < nheight; R0 += kRows) {
-            const uint32_t rlo = std::max(R0, t.oz), rhi = std::min(R0 + kRows, nheight);
+        for (uint32_t R0 = 0; R0 < nheight; R0 += kWaveRows) {
+            const uint32_t rlo = std::max(R0, t.oz), rhi = std::min(R0 + kWaveRows, nheight);
             if (rlo >= rhi) continue;
             const int ya = t.vt->h_left[rlo], nt = t.vt->h_left[rhi - 1] + kv - ya;
             tile = std::max(tile, nt);
             nbmax = std::max(nbmax, std::min(ya + nt, (int)t.H) - std::max(ya, top));
         }
-        const std::vector<int32_t>& sh = t.ht->h_st_hdr;
         for (uint32_t c0 = 0; c0 < t.nw; c0 += strip) {
             const uint32_t c1 = std::min(c0 + strip, t.nw);
             const int s_lo = t.ht->h_left[c0] >> 3;
             const int s_hi = (t.ht->h_left[c1 - 1] + t.ht->h_count[c1 - 1] - 1) >> 3;
             hdr = std::max(hdr, s_hi - s_lo + 1);
-            wts = std::max(wts, sh[4 * s_hi + 2] + 8 * sh[4 * s_hi + 1] - sh[4 * s_lo + 2]);
         }
     }
-    int fc = 16;
-    if (fc * nbmax > kPfCap || render_stripe_lds_bytes(fc, tile, hdr, wts) > 65536) fc = 8;
-    if (fc * nbmax > kPfCap || render_stripe_lds_bytes(fc, tile, hdr, wts) > 98304) return;
+    const int wts = hdr * 8 * (kv > 8 ? 16 : slots);
+    // staged values per lane and chunk: fc x (bins per frame) <= 64 x npf; 8 waves per block
+    // (the strip's step table staged once for 512 rows) where two such blocks fit a CU's LDS,
+    // else 4
+    int fc = 16, npf = 8, waves = nheight > 256 ? 8 : 4;
+    if (fc * nbmax > 64 * npf) npf = 16;
+    auto lds = [&]() { return render_stripe_lds_bytes(fc, tile, hdr, wts, waves); };
+    if (fc * nbmax > 64 * npf || lds() > (waves == 8 ? 81920 : 54613)) fc = 8;
+    if (waves == 8 && lds() > 81920) waves = 4;
+    if (fc * nbmax > 64 * npf || lds() > 163840) return;
+    // the instances compiled (render_stripe.hip launch_render_stripe)
+    if (kv > 8) npf = 16;
+    const int slots_run = kv > 8 ? 16 : slots;
+    if (fc == 8) npf = 16;
     g.stripe = true;
     g.st_kv = kv;
-    g.st_slots = slots;
+    g.st_slots = slots_run;
     g.st_fc = fc;
+    g.st_npf = npf;
+    g.st_waves = waves;
     g.st_tile = tile;
     g.st_hdr = hdr;
     g.st_wts = wts;
@@ -1419,7 +1436,7 @@ int plan_fused_group(const float* d_spec, const uint64_t* row0, size_t bins, siz
         if (T == 0 || nwidth[i] == 0) continue;
         const DevTaps *vt = nullptr, *ht = nullptr;
         int rc = dev_taps(H, nheight, &vt);
-        if (!rc) rc = stripe ? dev_taps_stepped(T, nwidth[i], &ht) : dev_taps(T, nwidth[i], &ht);
+        if (!rc) rc = stripe ? dev_taps_stepped(T, nwidth[i], 0, &ht) : dev_taps(T, nwidth[i], &ht);
         if (rc) return rc;
         RenderDesc r{};
         r.spec_off = row0[i] * bins;
@@ -1433,7 +1450,6 @@ int plan_fused_group(const float* d_spec, const uint64_t* row0, size_t bins, siz
         r.vo = vt->offset.as<int32_t>(); r.vw = vt->weights.as<float>();
         r.hl = ht->left.as<int32_t>(); r.hc = ht->count.as<int32_t>();
         r.ho = ht->offset.as<int32_t>(); r.hw = ht->weights.as<float>();
-        r.hst = ht->st_hdr.as<int32_t>(); r.hsw = ht->st_w.as<float>();
         // oz: output rows whose taps end at or above the band's top row H - bins
         const int32_t top = (int32_t)H - (int32_t)bins;
         uint32_t oz = 0;
@@ -1456,6 +1472,12 @@ int plan_fused_group(const float* d_spec, const uint64_t* row0, size_t bins, siz
         if (g.stripe) {  // no intermediate: the group's workspace share and its cost change
             uint64_t cost = 0;
             for (size_t i = g.desc0; i < g.desc0 + g.ndesc; ++i) {
+                const DevTaps* ht = nullptr;  // the step tables for the group's slot count
+                const int rc = dev_taps_stepped(desc[i].T, desc[i].nw, g.st_slots, &ht);
+                if (rc) return rc;
+                const int k = g.st_slots / 4 - 2;
+                desc[i].hst = ht->st_ca[k].as<int32_t>();
+                desc[i].hsw = ht->st_w[k].as<float>();
                 desc[i].tmp_off = 0;
                 cost += (uint64_t)desc[i].T * bins + (3ull * desc[i].nw * nheight) / 4;
             }
@@ -1630,6 +1652,8 @@ int render_rgb_fused(size_t n_groups, const float* const* d_specs, const uint64_
                 L.kv = g.st_kv;
                 L.slots = g.st_slots;
                 L.fc = g.st_fc;
+                L.npf = g.st_npf;
+                L.waves = g.st_waves;
                 L.tile_cap = g.st_tile;
                 L.hdr_cap = g.st_hdr;
                 L.wts_cap = g.st_wts;

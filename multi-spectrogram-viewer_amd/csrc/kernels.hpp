@@ -182,9 +182,10 @@ struct RenderDesc {
     const float* vw;
     const int32_t *hl, *hc, *ho;
     const float* hw;
-    // the horizontal taps regrouped by 8-frame step (render_stripe_kernel): per step s of the
-    // track, {ca, na, woff, 0} = the columns ca .. ca + na - 1 whose supports meet frames
-    // [8s, 8s + 8), and at hsw + woff their na x 8 weights (zero outside a column's support)
+    // the horizontal taps regrouped by 8-frame step (render_stripe_kernel, A slots): per step s
+    // of the track its first column hst[s] (the columns whose supports meet frames [8s, 8s + 8)
+    // are hst[s] ..), and hsw[(s * 8 + u) * A + a] = the weight of column hst[s] + a at frame
+    // 8s + u (+0 outside its support)
     const int32_t* hst;
     const float* hsw;
 };
@@ -205,11 +206,11 @@ int launch_render_batch2(const float* spec, uint32_t bins, float max, float min,
                          int v_fpl = 1);  // frames per lane of the vertical pass (1, or 4: wide)
 // The single-pass display (render_stripe_kernel, render_stripe.hip): grey + vertical Lanczos3 +
 // horizontal Lanczos3 + colormap in one kernel, the f32 intermediate never leaving registers.
-// A block owns `strip` output columns x 256 output rows of one track; its geometry bounds
-// (host, plan_stripe_group): kv vertical taps (8, 12 or 16, zero-padded), at most `slots`
-// columns meeting one 8-frame step (8 or 16), fc frames per staged chunk (8 or 16), at most
-// tile_cap grey rows per block, hdr_cap steps and wts_cap step weights per strip. -2 when no
-// instance fits.
+// A block owns `strip` output columns (a multiple of 16) x 64 `waves` output rows of one track,
+// each wave 64 of the rows; its geometry bounds (host, plan_stripe): kv vertical taps (8, 12 or 16,
+// zero-padded), at most `slots` columns meeting one 8-frame step (8, 12 or 16), fc frames per staged
+// chunk (8 or 16), npf staged values per lane and chunk (8 or 16), at most tile_cap grey rows
+// per wave, hdr_cap steps and wts_cap step weights per strip. -2 when no instance fits.
 struct StripeLaunch {
     const float* spec;
     uint32_t bins;
@@ -218,15 +219,16 @@ struct StripeLaunch {
     const RenderDesc* desc;
     uint32_t n;          // tracks (grid.z)
     uint32_t nw_max;
-    uint32_t strip;      // output columns per block (multiple of 4)
-    int kv, slots, fc;
+    uint32_t strip;      // output columns per block (multiple of 16)
+    int kv, slots, fc, npf;
+    int waves;           // per block (4 or 8: 256 or 512 output rows)
     int tile_cap, hdr_cap, wts_cap;
     bool dword_rgb;      // every track's nw and rgb_off are multiples of 4 (dword RGB stores)
     const uint8_t* cmap;
     uint8_t* rgb;
 };
 int launch_render_stripe(const StripeLaunch& L, hipStream_t s);
-int render_stripe_lds_bytes(int fc, int tile_cap, int hdr_cap, int wts_cap);
+int render_stripe_lds_bytes(int fc, int tile_cap, int hdr_cap, int wts_cap, int waves);
 
 // LDS bytes of the wide vertical pass (grey_vert_wide_kernel<fpl>) for a band / tile / kv
 int grey_vert_wide_lds_bytes(int fpl, uint32_t band, int tile_cap, int kv);

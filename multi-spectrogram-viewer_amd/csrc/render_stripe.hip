@@ -3,19 +3,22 @@
 // horizontal_sample; display.rs:57) + colormap (display.rs:24-42), with the f32 intermediate
 // [nheight, T] of the separable resize never written: it lives in registers for 8 frames.
 //
-// A block owns a strip of output columns [c0, c1) x 256 output rows of one track; lane = output
-// row. It walks the strip's frames in 8-frame steps, ascending:
+// A block owns a strip of output columns [c0, c1) x 256 or 512 output rows of one track; lane =
+// output row, and each wave (64 rows) runs on its own after the block has staged the strip's step
+// table
+// (no block barrier in the frame loop). A wave walks the strip's frames in 8-frame steps,
+// ascending:
 //   * the dB rows of a chunk of FC frames (the bins its rows' taps reach: a contiguous piece of
 //     each frame row) are loaded into registers one chunk ahead, turned into grey values and
-//     stored transposed into an LDS tile [grey row][frame] (double-buffered, one barrier per
-//     chunk);
+//     stored transposed into the wave's LDS tile [grey row][frame] once the chunk before is done;
 //   * vertical: v[u] = sum_i grey[l_row + i][f_u] * wv_row[i] for the step's 8 frames, the row's
-//     taps zero-padded to KV (registers), two ds_read_b128 per tap;
+//     taps zero-padded to KV (registers), ds_read_b128 per tap and 4 frames;
 //   * horizontal: the columns whose supports meet the step (at most A: accumulators acc[k] for
 //     columns cs + k, in registers) take acc[k] += v[u] * w[u] for u ascending, with the step's
 //     weights from LDS (the host regroups each column's taps by step, zero outside its support);
 //   * a column whose support ends in the step is finished: colormap, its 3 bytes packed with
-//     its neighbours', the accumulators shift down one slot.
+//     its neighbours' into the wave's RGB staging in LDS, which leaves as contiguous 48-byte row
+//     pieces every 16 columns; the accumulators shift down one slot.
 // Every sum runs in the reference's order (t = 0; t += x * w, no fused multiply-add: the kernel
 // is built with -ffp-contract=off). The padded terms are (+0 weight) x (finite value) = +-0,
 // which leave a sum's bits unchanged (a sum is never -0: it starts at +0 and x + -x rounds to
@@ -29,30 +32,55 @@ namespace thesia {
 
 namespace {
 
-constexpr int kRows = 256;  // output rows per block (lane = row)
-constexpr int kPf = 16;     // staged dB values per thread and chunk (registers)
+constexpr int kRgbStride = 13;  // dwords per row of a wave's RGB staging (16 columns = 12 dwords)
+constexpr int kSumStride = 17;  // floats per row of a wave's finished sums (16 columns)
+constexpr int kLutFloats = 32;  // the colormap as 10 x {stop i, stop i + 1} (8 bytes each)
+
+// colormap_px (display.rs:24-42) from the paired-stop table: one ds_read_b64 per pixel instead of
+// six byte reads, no branch. Same operations for every value: x < 0 / NaN -> 0; position
+// 10 x; below stop 9 the lerp of stops floor(position) and + 1 with ratio position - index;
+// from stop 9 on, the pair (stop 9, stop 9) with ratio 0, i.e. 0 * b + 1 * a = a exactly.
+__device__ __forceinline__ uint32_t colormap_rgb(float t, const uint2* lut) {
+    float x = t;
+    if (!(x >= 0.0f)) x = 0.0f;
+    const float position = 10.0f * x;
+    const float fl = floorf(position);
+    const bool top = fl >= 9.0f;
+    const int index = top ? 9 : (int)fl;
+    const float ratio = top ? 0.0f : position - (float)index;
+    const uint2 e = lut[index];
+    const float ar = (float)(e.x & 0xFF), ag = (float)((e.x >> 8) & 0xFF), ab = (float)((e.x >> 16) & 0xFF);
+    const float br = (float)(e.y & 0xFF), bg = (float)((e.y >> 8) & 0xFF), bb = (float)((e.y >> 16) & 0xFF);
+    const float om = 1.0f - ratio;
+    const uint32_t r = sat_u8(roundf(ratio * br + om * ar));
+    const uint32_t g = sat_u8(roundf(ratio * bg + om * ag));
+    const uint32_t b = sat_u8(roundf(ratio * bb + om * ab));
+    return r | (g << 8) | (b << 16);
+}
 
 __device__ __forceinline__ int rfl(int x) { return __builtin_amdgcn_readfirstlane(x); }
 
-// the 12 RGB bytes of 4 consecutive columns of one row, packed into 3 dwords
-struct Pack {
-    uint32_t d0 = 0, d1 = 0, d2 = 0;
-    __device__ __forceinline__ void put(int p, const uint8_t* px) {  // p = column & 3 (uniform)
+// the values are formed here (not sunk past this point), and no memory access is moved across
+// it: bounds the LDS reads in flight (their registers) where the compiler would hoist a whole
+// step's worth
+template <int N>
+__device__ __forceinline__ void pin_mem(float (&a)[N]) {
 #pragma unroll
-        for (int ch = 0; ch < 3; ++ch) {
-            const int o = 3 * p + ch;
-            const uint32_t v = (uint32_t)px[ch] << (8 * (o & 3));
-            if ((o >> 2) == 0) d0 |= v;
-            else if ((o >> 2) == 1) d1 |= v;
-            else d2 |= v;
-        }
-    }
-};
+    for (int i = 0; i < N; ++i) asm volatile("" : "+v"(a[i]));
+    asm volatile("" ::: "memory");
+}
 
-template <int KV, int A, int FC>
-__global__ void __launch_bounds__(256) render_stripe_kernel(StripeLaunch L) {
+__device__ __forceinline__ void wave_sync() {  // cross-lane LDS ordering within the wave
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+template <int KV, int A, int FC, int NPF, int WV>
+__global__ void __launch_bounds__(64 * WV) render_stripe_kernel(StripeLaunch L) {
+    constexpr int kRows = 64 * WV;  // output rows per block (lane = row)
     extern __shared__ __attribute__((aligned(16))) float sm[];
-    constexpr int TS = FC + 4;  // tile row stride (floats): 16-byte rows for the b128 reads
+    constexpr int TS = FC + 4;   // tile row stride (floats): 16-byte rows for the b128 reads
     constexpr int SPC = FC / 8;  // steps per chunk
     const RenderDesc r = L.desc[blockIdx.z];
     const uint32_t nw = r.nw;
@@ -62,70 +90,102 @@ __global__ void __launch_bounds__(256) render_stripe_kernel(StripeLaunch L) {
     const uint32_t R0 = blockIdx.y * kRows;
     const uint32_t nh = L.nh;
     if (R0 >= nh) return;
-    const int tid = threadIdx.x;
+    const int tid = threadIdx.x, lane = tid & 63;
     const int wave = rfl(tid >> 6);
     const uint32_t row = R0 + (uint32_t)tid;
     const bool live = row < nh;
     const uint32_t oz = r.oz;
-    uint8_t* orow = L.rgb + r.rgb_off + (uint64_t)row * nw * 3;
 
-    uint8_t* cm = reinterpret_cast<uint8_t*>(sm);  // 32 B
-    if (tid < 30) cm[tid] = L.cmap[tid];
-
-    // finished column c of this lane: colormap, pack, store every 4 columns (or at c1 - 1)
-    Pack pk;
-    auto emit = [&](uint32_t c, float t) {
-        uint8_t px[3];
-        colormap_px(t, cm, px);
-        const int p = (int)(c & 3);
-        pk.put(p, px);
-        if (p == 3 || c + 1 == c1) {
-            if (live) {
-                uint8_t* o = orow + (uint64_t)(c & ~3u) * 3;
-                if (L.dword_rgb) {  // 12 bytes at a 4-byte aligned address
-                    uint32_t* o4 = reinterpret_cast<uint32_t*>(o);
-                    o4[0] = pk.d0;
-                    o4[1] = pk.d1;
-                    o4[2] = pk.d2;
-                } else {
-                    const uint32_t w[3] = {pk.d0, pk.d1, pk.d2};
-                    for (int b = 0; b < 3 * (p + 1); ++b) o[b] = (uint8_t)(w[b >> 2] >> (8 * (b & 3)));
-                }
-            }
-            pk = Pack{};
-        }
-    };
-
-    // rows with vertical work: [rlo, rhi) (rows below oz take only the zero fill: +0 sums)
-    const uint32_t rlo = R0 > oz ? R0 : oz;
-    const uint32_t rhi = R0 + kRows < nh ? R0 + kRows : nh;
-    __syncthreads();  // colormap bytes
-    if (rlo >= rhi) {  // the whole block is above the track's band: colormap(+0) everywhere
-        for (uint32_t c = c0; c < c1; ++c) emit(c, 0.0f);
-        return;
-    }
-    // this wave has no row with vertical work (every row above the band, or past the image)
-    const uint32_t wr0 = R0 + 64u * (uint32_t)wave;
-    const bool wskip = wr0 + 63 < oz || wr0 >= nh;
-
-    // LDS: colormap (32 B = 8 floats) | tile[2][tile_cap][TS] | hdr[hdr_cap] | wts[wts_cap]
-    float* tile = sm + 8;
-    int4* hdr = reinterpret_cast<int4*>(tile + 2 * L.tile_cap * TS);
-    float* wts = reinterpret_cast<float*>(hdr + L.hdr_cap);
+    // LDS: colormap pairs (128 B) | the strip's steps' first columns hdr[hdr_cap] (padded to 16 B)
+    // | their weights wts[wts_cap] ([step][frame][slot]) | per wave: tile[tile_cap][TS],
+    // finished sums [64 rows][kSumStride] (also the RGB staging [64 rows][kRgbStride dwords])
+    uint2* lut = reinterpret_cast<uint2*>(sm);
+    int* hdr = reinterpret_cast<int*>(sm + kLutFloats);
+    float* wts = reinterpret_cast<float*>(hdr + ((L.hdr_cap + 3) & ~3));
+    const int wave_floats = L.tile_cap * TS + 64 * kSumStride;
+    float* tile = wts + L.wts_cap + wave * wave_floats;
+    float* fsum = tile + L.tile_cap * TS;
+    // the RGB staging reuses the sums' space (every lane has read its sums before it is written)
+    uint32_t* rgbst = reinterpret_cast<uint32_t*>(fsum);
 
     // the strip's steps [s_lo, s_hi]: from the first column's first frame to the last column's last
     const int s_lo = r.hl[c0] >> 3;
     const int s_hi = (r.hl[c1 - 1] + r.hc[c1 - 1] - 1) >> 3;
     const int nst = s_hi - s_lo + 1;  // <= hdr_cap (host)
-    const int4* gh = reinterpret_cast<const int4*>(r.hst) + s_lo;
-    const int w0 = gh[0].z;
-    const int wend = gh[nst - 1].z + 8 * gh[nst - 1].y;  // wend - w0 <= wts_cap (host)
-    for (int i = tid; i < nst; i += 256) hdr[i] = gh[i];
-    for (int i = tid; i < wend - w0; i += 256) wts[i] = r.hsw[w0 + i];
+    const int* gh = r.hst + s_lo;
+    const float* gw = r.hsw + (uint64_t)s_lo * 8 * A;
+    if (tid < 10) {  // stop i and stop min(i + 1, 9)
+        const int i2 = tid < 9 ? tid + 1 : 9;
+        lut[tid] = make_uint2((uint32_t)L.cmap[3 * tid] | (uint32_t)L.cmap[3 * tid + 1] << 8 |
+                                  (uint32_t)L.cmap[3 * tid + 2] << 16,
+                              (uint32_t)L.cmap[3 * i2] | (uint32_t)L.cmap[3 * i2 + 1] << 8 |
+                                  (uint32_t)L.cmap[3 * i2 + 2] << 16);
+    }
+    for (int i = tid; i < nst; i += kRows) hdr[i] = gh[i];
+    for (int i = tid; i < nst * 2 * A; i += kRows)  // nst x 8 x A floats <= wts_cap (host)
+        reinterpret_cast<float4*>(wts)[i] = reinterpret_cast<const float4*>(gw)[i];
+    __syncthreads();  // the only block barrier: the waves run on their own from here
 
-    // the block's grey rows [ya, ya + nt): every tap of rows [rlo, rhi); the staged ones are
-    // those inside the track's band [top, H) (bins H - 1 - y, contiguous in a frame row); the
-    // others stay zero (the image's zero fill above the band, and padded taps below it)
+    // a finished column c: its sum into the lane's row of the wave's staging; every 16 columns
+    // (or at c1) the row's 16 sums are colormapped and packed (3 bytes a pixel, 12 dwords), and
+    // the wave's 64 rows leave as contiguous 48-byte row pieces
+    const uint32_t wr0 = R0 + 64u * (uint32_t)wave;
+    auto flush = [&](uint32_t c) {  // columns [c & ~15, c] of rows wr0 .. wr0 + 63
+        const uint32_t cb = c & ~15u;
+        const int n = (int)(c - cb) + 1;  // uniform
+        uint32_t d[12];
+#pragma unroll
+        for (int k = 0; k < 12; ++k) d[k] = 0;
+#pragma unroll
+        for (int k = 0; k < 16; ++k) {
+            if (k < n) {  // uniform
+                const uint32_t px = colormap_rgb(fsum[lane * kSumStride + k], lut);
+                // bytes 3k .. 3k + 2 of the row piece
+#pragma unroll
+                for (int ch = 0; ch < 3; ++ch) {
+                    const int o = 3 * k + ch;
+                    d[o >> 2] |= ((px >> (8 * ch)) & 0xFF) << (8 * (o & 3));
+                }
+            }
+        }
+        wave_sync();  // every lane's sums read
+#pragma unroll
+        for (int k = 0; k < 12; ++k) rgbst[lane * kRgbStride + k] = d[k];
+        wave_sync();
+        const int nbytes = 3 * n;  // per row
+        const uint32_t rows = nh - wr0 < 64u ? nh - wr0 : 64u;
+        uint8_t* gbase = L.rgb + r.rgb_off + ((uint64_t)wr0 * nw + cb) * 3;
+        if (L.dword_rgb) {  // row pieces start 4-byte aligned (nw, rgb_off multiples of 4)
+            const int nd = nbytes / 4;  // n is a multiple of 4 here
+            for (int e = lane; e < (int)rows * nd; e += 64) {
+                const int rr = e / nd, k = e - rr * nd;
+                reinterpret_cast<uint32_t*>(gbase + (uint64_t)rr * nw * 3)[k] = rgbst[rr * kRgbStride + k];
+            }
+        } else {
+            const uint8_t* sb = reinterpret_cast<const uint8_t*>(rgbst);
+            for (int b = lane; b < (int)rows * nbytes; b += 64) {
+                const int rr = b / nbytes, k = b - rr * nbytes;
+                gbase[(uint64_t)rr * nw * 3 + k] = sb[rr * kRgbStride * 4 + k];
+            }
+        }
+        wave_sync();
+    };
+    auto close_col = [&](uint32_t c, float t) {  // c in [c0, c1), ascending
+        fsum[lane * kSumStride + (c & 15)] = t;
+        if ((c & 15) == 15 || c + 1 == c1) flush(c);
+    };
+
+    // this wave's rows with vertical work: [rlo, rhi) (rows below oz take only the zero fill)
+    const uint32_t rlo = wr0 > oz ? wr0 : oz;
+    const uint32_t rhi = wr0 + 64 < nh ? wr0 + 64 : nh;
+    if (wr0 >= nh) return;
+    if (rlo >= rhi) {  // every row of the wave above the track's band: colormap(+0)
+        for (uint32_t c = c0; c < c1; ++c) close_col(c, 0.0f);
+        return;
+    }
+    // the wave's grey rows [ya, ya + nt): every tap of rows [rlo, rhi); the staged ones are those
+    // inside the track's band [top, H) (bins H - 1 - y, contiguous in a frame row); the others
+    // stay zero (the image's zero fill above the band, padded taps below it)
     const int H = (int)r.H, bins = (int)L.bins, top = H - bins;
     const int ya = r.vl[rlo];
     const int nt = r.vl[rhi - 1] + KV - ya;  // <= tile_cap (host)
@@ -133,49 +193,51 @@ __global__ void __launch_bounds__(256) render_stripe_kernel(StripeLaunch L) {
     const int ys1 = ya + nt < H ? ya + nt : H;
     const int nb = ys1 > ys0 ? ys1 - ys0 : 0;  // staged bins per frame
     const int b_lo = H - ys1;                  // lowest staged bin
-    const int tot = FC * nb;                   // <= 256 * kPf (host)
+    const int tot = FC * nb;                   // <= 64 * NPF (host)
     const uint32_t mrec = nb > 1 ? (uint32_t)((0x100000000ull + (uint32_t)nb - 1) / (uint32_t)nb) : 0u;
     const uint32_t T = r.T;
     const float* sp = L.spec + r.spec_off;
     const int F0 = 8 * s_lo;
-    for (int i = tid; i < 2 * nt * TS; i += 256) {  // both buffers: rows [0, nt)
-        const int b = i / (nt * TS), e = i - b * nt * TS;
-        tile[b * L.tile_cap * TS + e] = 0.0f;
-    }
+    for (int i = lane; i < L.tile_cap * TS; i += 64) tile[i] = 0.0f;
 
-    float pf[kPf];
+    // staging: element e of chunk k = (frame fi, staged bin bi), consecutive e = consecutive bins
+    // of one frame (coalesced). Out-of-range elements are clamped to the last one and frames
+    // past T to frame T - 1 (duplicate loads / identical stores; frames past T only ever meet
+    // zero horizontal weights, so any finite value will do): no per-element branches
+    float pf[NPF];
+    const uint32_t emax = (uint32_t)(tot > 0 ? tot - 1 : 0);
     auto issue = [&](int k) {  // chunk k's dB values -> registers
-        const int fb = F0 + k * FC;
+        const uint32_t fb = (uint32_t)(F0 + k * FC);
+        // opaque per call: the element indices and addresses are formed per chunk, not hoisted
+        // out of the frame loop into NPF x 3 registers held across it
+        int li = lane;
+        asm volatile("" : "+v"(li));
 #pragma unroll
-        for (int j = 0; j < kPf; ++j) {
-            if (256 * j >= tot) break;  // uniform
-            const uint32_t e = (uint32_t)(tid + 256 * j);
-            float v = 0.0f;
-            if ((int)e < tot) {
-                const uint32_t fi = nb > 1 ? __umulhi(e, mrec) : e;
-                const uint32_t bi = e - fi * (uint32_t)nb;
-                const uint32_t f = (uint32_t)fb + fi;
-                if (f < T) v = sp[(uint64_t)f * bins + (uint32_t)b_lo + bi];
-            }
-            pf[j] = v;
+        for (int j = 0; j < NPF; ++j) {
+            if (64 * j >= tot) break;  // uniform
+            uint32_t e = (uint32_t)(li + 64 * j);
+            e = e < emax ? e : emax;
+            const uint32_t fi = nb > 1 ? __umulhi(e, mrec) : e;
+            const uint32_t bi = e - fi * (uint32_t)nb;
+            uint32_t f = fb + fi;
+            f = f < T ? f : T - 1;
+            pf[j] = sp[f * (uint32_t)bins + (uint32_t)b_lo + bi];  // a track's rows < 2^32 floats (host)
         }
     };
-    auto commit = [&](int k) {  // registers -> grey values in tile buffer k & 1
-        float* t = tile + (k & 1) * L.tile_cap * TS;
-        const int fb = F0 + k * FC;
+    auto commit = [&](int) {  // registers -> grey values in the tile (its previous chunk read)
+        float* t = tile;
         // the element indices are formed again here, not kept from issue() across the steps
-        int tidc = tid;
-        asm volatile("" : "+v"(tidc));
+        int lc = lane;
+        asm volatile("" : "+v"(lc));
 #pragma unroll
-        for (int j = 0; j < kPf; ++j) {
-            if (256 * j >= tot) break;  // uniform
-            const uint32_t e = (uint32_t)(tidc + 256 * j);
-            if ((int)e < tot) {
-                const uint32_t fi = nb > 1 ? __umulhi(e, mrec) : e;
-                const uint32_t bi = e - fi * (uint32_t)nb;
-                const int q = H - 1 - (b_lo + (int)bi) - ya;
-                t[q * TS + (int)fi] = (uint32_t)fb + fi < T ? grey_of(pf[j], L.max, L.min) : 0.0f;
-            }
+        for (int j = 0; j < NPF; ++j) {
+            if (64 * j >= tot) break;  // uniform
+            uint32_t e = (uint32_t)(lc + 64 * j);
+            e = e < emax ? e : emax;
+            const uint32_t fi = nb > 1 ? __umulhi(e, mrec) : e;
+            const uint32_t bi = e - fi * (uint32_t)nb;
+            const int q = H - 1 - (b_lo + (int)bi) - ya;
+            t[q * TS + (int)fi] = grey_of(pf[j], L.max, L.min);
         }
     };
 
@@ -193,114 +255,144 @@ __global__ void __launch_bounds__(256) render_stripe_kernel(StripeLaunch L) {
         }
 #pragma unroll
         for (int i = 0; i < KV; ++i) wv[i] = i < n ? w[i] : 0.0f;
+        // landed before the frame loop: a first use inside it would wait (vmcnt 0) for the
+        // chunk prefetch issued behind these loads, every step
+#pragma unroll
+        for (int i = 0; i < KV; ++i) asm volatile("" : "+v"(wv[i]));
+        asm volatile("" : "+v"(q));
     }
 
     const int nchunks = (nst + SPC - 1) / SPC;
-    issue(0);
-    __syncthreads();  // tile zeroed
-    commit(0);
+    if (nb) {
+        issue(0);
+        wave_sync();  // tile zeroed
+        commit(0);
+    }
+    wave_sync();
     float acc[A];
 #pragma unroll
     for (int k = 0; k < A; ++k) acc[k] = 0.0f;
-    int cs = (int)c0;  // accumulator k <-> column cs + k
+    // slot a <-> column ca(s) + a of the step's table (columns before c0, finished by the strip
+    // on the left, and from c1 on are summed too and never stored)
     for (int k = 0; k < nchunks; ++k) {
-        __syncthreads();  // chunk k in its buffer; chunk k - 1's readers done with the other one
-        if (k + 1 < nchunks) issue(k + 1);
-        if (!wskip) {
-            const float* t = tile + (k & 1) * L.tile_cap * TS + q * TS;
-            for (int u8 = 0; u8 < SPC; ++u8) {
-                const int si = k * SPC + u8;
-                if (si >= nst) break;  // uniform
-                // vertical sums of the step's 8 frames (resize_v_px order)
-                float v[8];
+        if (k + 1 < nchunks && nb) issue(k + 1);
+        const float* t = tile + q * TS;
+        for (int u8 = 0; u8 < SPC; ++u8) {
+            const int si = k * SPC + u8;
+            if (si >= nst) break;  // uniform
+            const int ca = rfl(hdr[si]);
+            // vertical sums of the step's 8 frames (resize_v_px order), 4 frames at a time: one
+            // ds_read_b128 per tap, a batch of taps' reads in flight
+            float v[8];
+            constexpr int KB = KV % 8 == 0 ? 8 : 4;  // taps per batch of reads (divides KV)
+            static_assert(KV % KB == 0, "tap batches");
 #pragma unroll
-                for (int u = 0; u < 8; ++u) v[u] = 0.0f;
-                const float* tq = t + 8 * u8;
+            for (int hf = 0; hf < 2; ++hf) {
+                const float* tq = t + 8 * u8 + 4 * hf;
+                float a0 = 0.0f, a1 = 0.0f, a2 = 0.0f, a3 = 0.0f;
 #pragma unroll
-                for (int i = 0; i < KV; ++i) {
-                    const float4 g0 = *reinterpret_cast<const float4*>(tq + i * TS);
-                    const float4 g1 = *reinterpret_cast<const float4*>(tq + i * TS + 4);
-                    v[0] = v[0] + g0.x * wv[i];
-                    v[1] = v[1] + g0.y * wv[i];
-                    v[2] = v[2] + g0.z * wv[i];
-                    v[3] = v[3] + g0.w * wv[i];
-                    v[4] = v[4] + g1.x * wv[i];
-                    v[5] = v[5] + g1.y * wv[i];
-                    v[6] = v[6] + g1.z * wv[i];
-                    v[7] = v[7] + g1.w * wv[i];
-                }
-                // horizontal: the step's columns [cs, ce), frames ascending (resize_h order)
-                const int4 h = hdr[si];
-                const int ca = rfl(h.x), na = rfl(h.y), wo = rfl(h.z) - w0;
-                const int ce = ca + na < (int)c1 ? ca + na : (int)c1;
-                const float* wb = wts + wo + 8 * (cs - ca);
+                for (int i0 = 0; i0 < KV; i0 += KB) {
+                    float4 g[KB];
 #pragma unroll
-                for (int a = 0; a < A; ++a) {
-                    if (cs + a < ce) {  // uniform
-                        const float4 x0 = *reinterpret_cast<const float4*>(wb + 8 * a);
-                        const float4 x1 = *reinterpret_cast<const float4*>(wb + 8 * a + 4);
-                        float s = acc[a];
-                        s = s + v[0] * x0.x;
-                        s = s + v[1] * x0.y;
-                        s = s + v[2] * x0.z;
-                        s = s + v[3] * x0.w;
-                        s = s + v[4] * x1.x;
-                        s = s + v[5] * x1.y;
-                        s = s + v[6] * x1.z;
-                        s = s + v[7] * x1.w;
-                        acc[a] = s;
+                    for (int i = 0; i < KB; ++i) g[i] = *reinterpret_cast<const float4*>(tq + (i0 + i) * TS);
+#pragma unroll
+                    for (int i = 0; i < KB; ++i) {
+                        const float w = wv[i0 + i];
+                        a0 = a0 + g[i].x * w;
+                        a1 = a1 + g[i].y * w;
+                        a2 = a2 + g[i].z * w;
+                        a3 = a3 + g[i].w * w;
                     }
+                    float ap[4] = {a0, a1, a2, a3};
+                    pin_mem(ap);  // bound the reads in flight (registers)
+                    a0 = ap[0]; a1 = ap[1]; a2 = ap[2]; a3 = ap[3];
                 }
-                // the columns whose supports end in this step: finished, slots shift down
-                int cn = (int)c1;
-                if (si + 1 < nst) {
-                    const int nx = rfl(hdr[si + 1].x);
-                    cn = nx > (int)c0 ? nx : (int)c0;
-                }
-                while (cs < cn) {  // uniform
-                    emit((uint32_t)cs, acc[0]);
+                v[4 * hf] = a0;
+                v[4 * hf + 1] = a1;
+                v[4 * hf + 2] = a2;
+                v[4 * hf + 3] = a3;
+            }
+            // horizontal: every slot's chain takes the step's frames in ascending order (the
+            // resize_h order; slots outside a column's support add (+0 weight) x v = +-0); the
+            // weights of frame u + 1 are read while frame u is summed
+            const float4* wu = reinterpret_cast<const float4*>(wts + si * 8 * A);
+            float4 xc[A / 4];
 #pragma unroll
-                    for (int a = 0; a + 1 < A; ++a) acc[a] = acc[a + 1];
-                    acc[A - 1] = 0.0f;
-                    ++cs;
+            for (int a4 = 0; a4 < A / 4; ++a4) xc[a4] = wu[a4];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) {
+                float4 xn[A / 4];
+                if (u + 1 < 8) {
+#pragma unroll
+                    for (int a4 = 0; a4 < A / 4; ++a4) xn[a4] = wu[(u + 1) * (A / 4) + a4];
+                }
+#pragma unroll
+                for (int a4 = 0; a4 < A / 4; ++a4) {
+                    acc[4 * a4] = acc[4 * a4] + v[u] * xc[a4].x;
+                    acc[4 * a4 + 1] = acc[4 * a4 + 1] + v[u] * xc[a4].y;
+                    acc[4 * a4 + 2] = acc[4 * a4 + 2] + v[u] * xc[a4].z;
+                    acc[4 * a4 + 3] = acc[4 * a4 + 3] + v[u] * xc[a4].w;
+                }
+                pin_mem(acc);
+                if (u + 1 < 8) {
+#pragma unroll
+                    for (int a4 = 0; a4 < A / 4; ++a4) xc[a4] = xn[a4];
                 }
             }
+            // the columns whose supports end in this step (all of the strip's at its last):
+            // finished, the slots shift down
+            const int cn = si + 1 < nst ? rfl(hdr[si + 1]) : (int)c1;
+            for (int c = ca; c < cn; ++c) {  // uniform
+                if (c >= (int)c0 && c < (int)c1) close_col((uint32_t)c, acc[0]);
+#pragma unroll
+                for (int a = 0; a + 1 < A; ++a) acc[a] = acc[a + 1];
+                acc[A - 1] = 0.0f;
+            }
         }
-        if (k + 1 < nchunks) commit(k + 1);
+        if (k + 1 < nchunks && nb) {
+            wave_sync();  // every lane's reads of the buffer chunk k + 1 overwrites are done
+            commit(k + 1);
+            wave_sync();
+        }
     }
-    if (wskip && live && row < oz)  // rows above the band: colormap(+0)
-        for (uint32_t c = c0; c < c1; ++c) emit(c, 0.0f);
 }
 
-template <int KV, int A, int FC>
-const void* stripe_kernel() {
-    return reinterpret_cast<const void*>(render_stripe_kernel<KV, A, FC>);
+template <int KV, int A, int FC, int NPF>
+const void* stripe_kernel(int waves) {
+    return waves == 8 ? reinterpret_cast<const void*>(render_stripe_kernel<KV, A, FC, NPF, 8>)
+                      : reinterpret_cast<const void*>(render_stripe_kernel<KV, A, FC, NPF, 4>);
 }
 
 }  // namespace
 
-int render_stripe_lds_bytes(int fc, int tile_cap, int hdr_cap, int wts_cap) {
-    return 32 + 2 * tile_cap * (fc + 4) * 4 + hdr_cap * 16 + wts_cap * 4;
+int render_stripe_lds_bytes(int fc, int tile_cap, int hdr_cap, int wts_cap, int waves) {
+    return (kLutFloats + ((hdr_cap + 3) & ~3) + wts_cap +
+            waves * (tile_cap * (fc + 4) + 64 * kSumStride)) * 4;
 }
 
 int launch_render_stripe(const StripeLaunch& L, hipStream_t s) {
     if (L.n == 0 || L.nh == 0) return 0;
-    if (L.n > 65535 || L.strip == 0 || (L.strip & 3)) return -2;
+    if (L.n > 65535 || L.strip == 0 || (L.strip & 15) || (L.waves != 4 && L.waves != 8)) return -2;
     const void* kern = nullptr;
-#define THESIA_STRIPE(KV_, A_, FC_) \
-    if (L.kv == KV_ && L.slots == A_ && L.fc == FC_) kern = stripe_kernel<KV_, A_, FC_>();
-    THESIA_STRIPE(8, 8, 16) THESIA_STRIPE(8, 16, 16) THESIA_STRIPE(8, 16, 8)
-    THESIA_STRIPE(12, 16, 16) THESIA_STRIPE(12, 16, 8)
-    THESIA_STRIPE(16, 16, 16) THESIA_STRIPE(16, 16, 8)
+    // the instances (host plan_stripe picks among them): KV 8 (the groups that upsample
+    // vertically) with 8 / 12 / 16 slots; KV 12 / 16 (downsampling) with 16
+#define THESIA_STRIPE(KV_, A_, FC_, NPF_) \
+    if (L.kv == KV_ && L.slots == A_ && L.fc == FC_ && L.npf == NPF_) kern = stripe_kernel<KV_, A_, FC_, NPF_>(L.waves);
+    THESIA_STRIPE(8, 8, 16, 8) THESIA_STRIPE(8, 8, 16, 16) THESIA_STRIPE(8, 8, 8, 16)
+    THESIA_STRIPE(8, 12, 16, 8) THESIA_STRIPE(8, 12, 16, 16) THESIA_STRIPE(8, 12, 8, 16)
+    THESIA_STRIPE(8, 16, 16, 8) THESIA_STRIPE(8, 16, 16, 16) THESIA_STRIPE(8, 16, 8, 16)
+    THESIA_STRIPE(12, 16, 16, 16) THESIA_STRIPE(12, 16, 8, 16)
+    THESIA_STRIPE(16, 16, 16, 16) THESIA_STRIPE(16, 16, 8, 16)
 #undef THESIA_STRIPE
     if (!kern) return -2;
-    const int lds = render_stripe_lds_bytes(L.fc, L.tile_cap, L.hdr_cap, L.wts_cap);
+    const int lds = render_stripe_lds_bytes(L.fc, L.tile_cap, L.hdr_cap, L.wts_cap, L.waves);
     if (lds > 163840) return -2;
     if (hipFuncSetAttribute(kern, hipFuncAttributeMaxDynamicSharedMemorySize, lds) != hipSuccess) return -1;
-    const dim3 grid((L.nw_max + L.strip - 1) / L.strip, (L.nh + kRows - 1) / kRows, L.n);
+    const uint32_t rows = 64u * (uint32_t)L.waves;
+    const dim3 grid((L.nw_max + L.strip - 1) / L.strip, (L.nh + rows - 1) / rows, L.n);
     StripeLaunch a = L;
     void* args[] = {&a};
-    if (hipLaunchKernel(kern, grid, dim3(256), args, lds, s) != hipSuccess) return -1;
+    if (hipLaunchKernel(kern, grid, dim3(rows), args, lds, s) != hipSuccess) return -1;
     return 0;
 }
 

@@ -238,8 +238,8 @@ def run_batches(batches, stream=None) -> None:
 
 
 def set_batches_policy(policy: int) -> None:
-    """thesia_set_batches_policy: 1 (default) = concurrent batches share one occupancy wave by
-    work; 0 = each batch sized for the whole device."""
+    """thesia_set_batches_policy: 0 (default) = each batch sized for the whole device; 1 =
+    concurrent batches share one occupancy wave by work (measured slower)."""
     check(lib.thesia_set_batches_policy(policy))
 
 
