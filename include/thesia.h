@@ -290,15 +290,16 @@ int thesia_grey_to_rgb_device(const float* d_grey, uint32_t width, uint32_t heig
 int thesia_minmax_segments_device(const float* d_spec, const uint64_t* row0, size_t bins,
                                   size_t n, float* max, float* min, int* has_nan);
 /* Process-wide choice of the batched display path's launch structure (all byte-identical):
- * 0 = the fused path (default): per geometry group, where its geometry allows (at most 16
- * vertical taps and 16 output columns meeting one 8-frame step: the groups whose images
- * downsample along time), ONE kernel for grey + vertical Lanczos3 + horizontal Lanczos3 +
- * colormap whose f32 intermediate never leaves registers (render_stripe_kernel); for the other
- * groups one kernel for grey + vertical Lanczos3 in one pass over the spectrogram, then one for
- * horizontal Lanczos3 + colormap (row spans staged by LDS-DMA); every track of a call in each
- * launch; 1 = per-track launches (the reference's one image at a time structure); 2 = every
- * track in one launch per stage: grey, vertical, horizontal + colormap; 3 = path 0 with the
- * two-kernel structure for every group (round 3's default). */
+ * 0 = the fused path (default): per geometry group, where the group downsamples along time at
+ * least 3:1 (frames >= 3 x image columns) and its geometry allows (at most 16 vertical taps and
+ * 16 output columns meeting one 8-frame step), ONE kernel for grey + vertical Lanczos3 +
+ * horizontal Lanczos3 + colormap whose f32 intermediate never leaves registers
+ * (render_stripe_kernel); for the other groups one kernel for grey + vertical Lanczos3 in one
+ * pass over the spectrogram, then one for horizontal Lanczos3 + colormap (row spans staged by
+ * LDS-DMA); every track of a call in each launch; 1 = per-track launches (the reference's one
+ * image at a time structure); 2 = every track in one launch per stage: grey, vertical,
+ * horizontal + colormap; 3 = path 0 with the two-kernel structure for every group (round 3's
+ * default); 4 = path 0 with the single-pass kernel wherever its geometry allows. */
 int thesia_set_render_path(int path);
 int thesia_render_rgb_batch_device(const float* d_spec, const uint64_t* row0, size_t bins,
                                    size_t n, const float* up_ratio, const uint32_t* nwidth,

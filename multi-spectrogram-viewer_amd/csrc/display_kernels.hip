@@ -1054,12 +1054,12 @@ __global__ void __launch_bounds__(256) resize_h_dma_kernel(uint32_t nh, const Re
                                                            const uint8_t* cmap, uint8_t* rgb) {
     extern __shared__ __attribute__((aligned(16))) float hsm[];
     constexpr int BUF = K * 1024;  // floats per row buffer: K chunks of 64 lanes x 16 B per wave
-    uint8_t* cm = reinterpret_cast<uint8_t*>(hsm + NB * BUF);
+    uint2* lut = reinterpret_cast<uint2*>(hsm + NB * BUF);  // colormap_rgb's stop pairs
     const RenderDesc r = d[blockIdx.z];
     const uint32_t ox0 = blockIdx.x * 256;
     if (ox0 >= r.nw) return;  // block-uniform
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    if (tid < 30) cm[tid] = cmap[tid];
+    if (tid < 10) lut[tid] = colormap_pair(cmap, tid);
     const uint32_t ox = ox0 + tid;
     const bool act = ox < r.nw;
     int32_t l = 0, n = 0;
@@ -1078,19 +1078,23 @@ __global__ void __launch_bounds__(256) resize_h_dma_kernel(uint32_t nh, const Re
     const int32_t span4 = (r.hl[last] + r.hc[last] - lb4 + 3) & ~3;  // <= BUF - KT (host)
     const int nchunk = span4 > 0 ? span4 >> 2 : 1;
     const int base = l - lb4;
-    uint8_t* orgb = rgb + r.rgb_off + (uint64_t)ox * 3;
-    __syncthreads();  // colormap bytes
+    __syncthreads();  // colormap pairs
+    const uint32_t lut_lds = (uint32_t)reinterpret_cast<uintptr_t>((__attribute__((address_space(3))) uint2*)lut);
+    // a pixel's 3 bytes (colormap_rgb packs them r | g << 8 | b << 16)
+    auto put = [](uint8_t* o, uint32_t px) {
+        o[0] = (uint8_t)px;
+        o[1] = (uint8_t)(px >> 8);
+        o[2] = (uint8_t)(px >> 16);
+    };
     // rows below oz: their intermediate rows are +0 (never formed) -> colormap(+0)
     const uint32_t G = gridDim.y;
+    const uint64_t ostep = (uint64_t)G * r.nw * 3;  // bytes between the block's rows
+    uint8_t* o = rgb + r.rgb_off + (uint64_t)ox * 3 + (uint64_t)blockIdx.y * r.nw * 3;
     uint32_t y0 = blockIdx.y;
     if (r.oz > y0) {
-        uint8_t px[3];
-        colormap_px(0.0f, cm, px);
-        for (; y0 < r.oz && y0 < nh; y0 += G)
-            if (act) {
-                uint8_t* o = orgb + (uint64_t)y0 * r.nw * 3;
-                o[0] = px[0]; o[1] = px[1]; o[2] = px[2];
-            }
+        const uint32_t px = colormap_rgb(0.0f, lut);
+        for (; y0 < r.oz && y0 < nh; y0 += G, o += ostep)
+            if (act) put(o, px);
     }
     const int nrows = y0 < nh ? (int)((nh - 1 - y0) / G) + 1 : 0;
     const float* rows0 = tmp + r.tmp_off + lb4;
@@ -1107,7 +1111,7 @@ __global__ void __launch_bounds__(256) resize_h_dma_kernel(uint32_t nh, const Re
         }
     };
     for (int k = 0; k < NB - 1 && k < nrows; ++k) dma(k);
-    for (int k = 0; k < nrows; ++k) {
+    for (int k = 0; k < nrows; ++k, o += ostep) {
         if (k + NB - 2 < nrows) wait_vm<(NB - 2) * K>();
         else wait_vm<0>();
         __builtin_amdgcn_s_barrier();
@@ -1118,10 +1122,12 @@ __global__ void __launch_bounds__(256) resize_h_dma_kernel(uint32_t nh, const Re
             float t = 0.0f;
 #pragma unroll
             for (int i = 0; i < KT; ++i) t += rin[i] * w[i];
-            uint8_t px[3];
-            colormap_px(t, cm, px);
-            uint8_t* o = orgb + (uint64_t)(y0 + G * (uint32_t)k) * r.nw * 3;
-            o[0] = px[0]; o[1] = px[1]; o[2] = px[2];
+            // the pair read in asm: the compiler cannot tell it from the DMA's LDS targets and
+            // would wait for every DMA in flight (vmcnt(0)) before a plain read
+            const CmapPos cp = colormap_pos(t);
+            uint2 e;
+            asm volatile("ds_read_b64 %0, %1\n\ts_waitcnt lgkmcnt(0)" : "=v"(e) : "v"(lut_lds + 8u * (uint32_t)cp.index));
+            put(o, colormap_lerp(e, cp.ratio));
         }
     }
 }
@@ -1130,16 +1136,18 @@ __global__ void __launch_bounds__(256) resize_h_dma_kernel(uint32_t nh, const Re
 static int launch_resize_h_dma(uint32_t nh, const RenderDesc* d_desc, uint32_t n, uint32_t nw_max, int h_taps,
                                int h_span, const float* tmp, const uint8_t* cmap, uint8_t* rgb, dim3 g3,
                                hipStream_t s) {
-    const int kt = h_taps <= 16 ? 16 : h_taps <= 32 ? 32 : h_taps <= 48 ? 48 : 0;
+    // 8 taps: the groups that upsample along time (Lanczos3's 6-7 taps per column)
+    const int kt = h_taps <= 8 ? 8 : h_taps <= 16 ? 16 : h_taps <= 32 ? 32 : h_taps <= 48 ? 48 : 0;
     if (!kt) return -2;
     const int need = h_span + 4 + kt;
     const int K = need <= 1024 ? 1 : need <= 2048 ? 2 : need <= 4096 ? 4 : 0;
     if (!K) return -2;
     constexpr int NB = 4;  // row buffers (3 and 6 measured slower: 3.40 / 3.42 vs 3.36 ms per C5 step)
-    const int lds = NB * K * 1024 * 4 + 32;
+    const int lds = NB * K * 1024 * 4 + 80;  // + the colormap pairs
     const void* kern = nullptr;
 #define THESIA_HDMA(KT_, K_) \
     if (kt == KT_ && K == K_) kern = reinterpret_cast<const void*>(resize_h_dma_kernel<KT_, K_, NB>);
+    THESIA_HDMA(8, 1) THESIA_HDMA(8, 2) THESIA_HDMA(8, 4)
     THESIA_HDMA(16, 1) THESIA_HDMA(16, 2) THESIA_HDMA(16, 4)
     THESIA_HDMA(32, 1) THESIA_HDMA(32, 2) THESIA_HDMA(32, 4)
     THESIA_HDMA(48, 1) THESIA_HDMA(48, 2) THESIA_HDMA(48, 4)

@@ -1040,7 +1040,7 @@ static int g_render_path = 0;  // thesia_set_render_path
 
 int render_path() { return __atomic_load_n(&g_render_path, __ATOMIC_RELAXED); }
 int set_render_path(int path) {
-    if (path < 0 || path > 3) return set_error(THESIA_ERR_INVALID_ARG, "render path must be 0 .. 3");
+    if (path < 0 || path > 4) return set_error(THESIA_ERR_INVALID_ARG, "render path must be 0 .. 4");
     __atomic_store_n(&g_render_path, path, __ATOMIC_RELAXED);
     return THESIA_OK;
 }
@@ -1349,6 +1349,7 @@ struct FusedGroup {
 };
 
 // Host planning of one group: a RenderDesc per non-empty track (appended to `desc`), the
+// single-pass display where `stripe` asks for it (1 the automatic choice, 2 wherever covered), the
 // vertical band (the widest whose grey rows <= THESIA_VROWS and weights <= 4096 fit the LDS
 // tile for every track of the group) and the horizontal pass's tap / span bounds.
 // The single-pass display for a group (render_stripe_kernel): the instance (KV vertical taps,
@@ -1360,9 +1361,26 @@ struct StripeTrack {
     uint32_t T, H, nw, oz;
     uint64_t rgb_off;
 };
-void plan_stripe(const std::vector<StripeTrack>& trk, uint32_t bins, uint32_t nheight, FusedGroup& g) {
+// Automatic choice (render path 0): only groups whose frames outnumber their image columns at
+// least 3 to 1. There the two-kernel path's intermediate ([nheight][T] f32, written and read
+// back) dominates its traffic, and the stripe kernel's fixed 8-frame steps waste few slots
+// (about 8 + 6 T/nw columns meet a step, 6 of them with work per frame). Measured per C5 group
+// alone (profiles/r04_display): 44.1 kHz / 256 (T/nw 6.9) 846 -> 575 us, 48 kHz / 512 (3.8)
+// 604 -> 504, 22.05 kHz / 256 (3.4) 478 -> 419; slower at T/nw 1.25 .. 1.9 (8 kHz / 256 265 ->
+// 291, 16 kHz / 512 293 -> 317, 24 kHz / 512 341 -> 349, 44.1 kHz / 1024 359 -> 394) and even
+// below 1. Path 4 takes it wherever an instance covers the geometry.
+void plan_stripe(const std::vector<StripeTrack>& trk, uint32_t bins, uint32_t nheight, FusedGroup& g,
+                 bool force) {
     g.stripe = false;
     if (trk.empty()) return;
+    if (!force) {
+        uint64_t frames = 0, cols = 0;
+        for (const StripeTrack& t : trk) {
+            frames += t.T;
+            cols += t.nw;
+        }
+        if (frames < 3 * cols) return;
+    }
     int kvmax = 0, amax = 0;
     bool dword = true;
     for (const StripeTrack& t : trk) {
@@ -1422,7 +1440,7 @@ void plan_stripe(const std::vector<StripeTrack>& trk, uint32_t bins, uint32_t nh
 int plan_fused_group(const float* d_spec, const uint64_t* row0, size_t bins, size_t n,
                      const float* up_ratio, const uint32_t* nwidth, uint32_t nheight,
                      const uint64_t* rgb_off, std::vector<RenderDesc>& desc, FusedGroup& g, bool wide,
-                     bool stripe) {
+                     int stripe) {
     g.spec = d_spec;
     g.bins = (uint32_t)bins;
     g.desc0 = desc.size();
@@ -1468,7 +1486,7 @@ int plan_fused_group(const float* d_spec, const uint64_t* row0, size_t bins, siz
     }
     g.ndesc = desc.size() - g.desc0;
     if (stripe) {
-        plan_stripe(strk, (uint32_t)bins, nheight, g);
+        plan_stripe(strk, (uint32_t)bins, nheight, g, stripe == 2);
         if (g.stripe) {  // no intermediate: the group's workspace share and its cost change
             uint64_t cost = 0;
             for (size_t i = g.desc0; i < g.desc0 + g.ndesc; ++i) {
@@ -1590,7 +1608,8 @@ int render_rgb_fused(size_t n_groups, const float* const* d_specs, const uint64_
         size_t t0 = 0;
         for (size_t k = 0; k < n_groups; ++k) {
             rc = plan_fused_group(d_specs[k], row0s[k], bins[k], ns[k], up_ratio + t0, nwidth + t0, nheight,
-                                  rgb_off + t0, desc, groups[k], true, rpath == 0);
+                                  rgb_off + t0, desc, groups[k], true,
+                                  rpath == 0 ? 1 : rpath == 4 ? 2 : 0);
             if (rc) return rc;
             t0 += ns[k];
         }
@@ -1742,7 +1761,7 @@ int render_rgb_batch_device(const float* d_spec, const uint64_t* row0, size_t bi
     int crc = 0;
     const uint8_t* cmap_ptr = colormap_device(&crc);
     if (crc) return crc;
-    if (render_path() == 0 || render_path() == 3) {
+    if (render_path() == 0 || render_path() >= 3) {
         const size_t ns[1] = {n};
         const size_t bs[1] = {bins};
         return render_rgb_fused(1, &d_spec, &row0, bs, ns, up_ratio, nwidth, nheight, max, min, d_rgb,

@@ -140,9 +140,11 @@ int set_batches_policy(int policy);
 int batch_set_option(Batch* b, int option, int64_t value);  // thesia_batch_set_option
 int ranges_read(const int* d_range, size_t n, float* mx, float* mn, int* nan, hipStream_t s);
 
-// display path selection (thesia_set_render_path): 0 fused batched launches (grey + vertical
-// in one pass, then horizontal + colormap), 1 per-track launches, 2 three-stage batched
-// launches (grey, vertical, horizontal + colormap)
+// display path selection (thesia_set_render_path): 0 fused batched launches (the single-pass
+// stripe kernel for the groups that downsample along time at least 3:1, else grey + vertical in
+// one pass, then horizontal + colormap), 1 per-track launches, 2 three-stage batched launches
+// (grey, vertical, horizontal + colormap), 3 path 0 without the stripe kernel, 4 path 0 with the
+// stripe kernel wherever its instances cover the geometry
 int render_path();
 int set_render_path(int path);
 

@@ -36,28 +36,6 @@ constexpr int kRgbStride = 13;  // dwords per row of a wave's RGB staging (16 co
 constexpr int kSumStride = 17;  // floats per row of a wave's finished sums (16 columns)
 constexpr int kLutFloats = 32;  // the colormap as 10 x {stop i, stop i + 1} (8 bytes each)
 
-// colormap_px (display.rs:24-42) from the paired-stop table: one ds_read_b64 per pixel instead of
-// six byte reads, no branch. Same operations for every value: x < 0 / NaN -> 0; position
-// 10 x; below stop 9 the lerp of stops floor(position) and + 1 with ratio position - index;
-// from stop 9 on, the pair (stop 9, stop 9) with ratio 0, i.e. 0 * b + 1 * a = a exactly.
-__device__ __forceinline__ uint32_t colormap_rgb(float t, const uint2* lut) {
-    float x = t;
-    if (!(x >= 0.0f)) x = 0.0f;
-    const float position = 10.0f * x;
-    const float fl = floorf(position);
-    const bool top = fl >= 9.0f;
-    const int index = top ? 9 : (int)fl;
-    const float ratio = top ? 0.0f : position - (float)index;
-    const uint2 e = lut[index];
-    const float ar = (float)(e.x & 0xFF), ag = (float)((e.x >> 8) & 0xFF), ab = (float)((e.x >> 16) & 0xFF);
-    const float br = (float)(e.y & 0xFF), bg = (float)((e.y >> 8) & 0xFF), bb = (float)((e.y >> 16) & 0xFF);
-    const float om = 1.0f - ratio;
-    const uint32_t r = sat_u8(roundf(ratio * br + om * ar));
-    const uint32_t g = sat_u8(roundf(ratio * bg + om * ag));
-    const uint32_t b = sat_u8(roundf(ratio * bb + om * ab));
-    return r | (g << 8) | (b << 16);
-}
-
 __device__ __forceinline__ int rfl(int x) { return __builtin_amdgcn_readfirstlane(x); }
 
 // the values are formed here (not sunk past this point), and no memory access is moved across
@@ -114,13 +92,7 @@ __global__ void __launch_bounds__(64 * WV) render_stripe_kernel(StripeLaunch L) 
     const int nst = s_hi - s_lo + 1;  // <= hdr_cap (host)
     const int* gh = r.hst + s_lo;
     const float* gw = r.hsw + (uint64_t)s_lo * 8 * A;
-    if (tid < 10) {  // stop i and stop min(i + 1, 9)
-        const int i2 = tid < 9 ? tid + 1 : 9;
-        lut[tid] = make_uint2((uint32_t)L.cmap[3 * tid] | (uint32_t)L.cmap[3 * tid + 1] << 8 |
-                                  (uint32_t)L.cmap[3 * tid + 2] << 16,
-                              (uint32_t)L.cmap[3 * i2] | (uint32_t)L.cmap[3 * i2 + 1] << 8 |
-                                  (uint32_t)L.cmap[3 * i2 + 2] << 16);
-    }
+    if (tid < 10) lut[tid] = colormap_pair(L.cmap, tid);
     for (int i = tid; i < nst; i += kRows) hdr[i] = gh[i];
     for (int i = tid; i < nst * 2 * A; i += kRows)  // nst x 8 x A floats <= wts_cap (host)
         reinterpret_cast<float4*>(wts)[i] = reinterpret_cast<const float4*>(gw)[i];

@@ -145,9 +145,10 @@ def test_c5_mixed_rate_render_pipeline():
         assert r.rgb.tobytes() == img.tobytes(), (t.sr, t.n_fft)  # display path bit-exact
 
 
-# 0: single-pass stripes where the geometry allows, else two kernels; 1: per-track; 2: three-stage;
-# 3: two kernels for every group (LDS-DMA horizontal; wide vertical pass for upsampling groups)
-@pytest.mark.parametrize("path", [0, 1, 2, 3])
+# 0: single-pass stripes for groups downsampling >= 3:1 along time, else two kernels; 1: per-track;
+# 2: three-stage; 3: two kernels for every group (LDS-DMA horizontal; wide vertical pass for
+# upsampling groups); 4: single-pass stripes wherever an instance covers the geometry
+@pytest.mark.parametrize("path", [0, 1, 2, 3, 4])
 @pytest.mark.parametrize("px_per_sec", [73.0, 30.0, 9.0, 2.0])  # 30: 17-64 taps; 9, 2: wider spans
 @pytest.mark.parametrize("nheight", [90, 400, 600])  # 400, 600: H -> nheight downsampling ~2.5, taller
 def test_render_batch_ragged_groups(path, px_per_sec, nheight):
@@ -182,12 +183,13 @@ def _ragged(px_per_sec, nheight):
         assert r.rgb.tobytes() == img.tobytes(), (t.sr, t.n_fft, t.pcm.shape)
 
 
-@pytest.mark.parametrize("path", [0, 3])
+@pytest.mark.parametrize("path", [0, 3, 4])
 def test_c5_geometry_500_rows(path):
     """The C5 display geometry (100 px/s x 500 rows, every (rate, n_fft) pair) at 3 s per track:
-    the single-pass stripe kernel runs the 7 groups whose images downsample along time (two row
-    blocks of 256, strips of 64 columns, dword RGB stores: nwidth 300), the others the two-kernel
-    path; bytes equal the oracle display of the device's own dB."""
+    the single-pass stripe kernel runs the 3 groups that downsample >= 3:1 along time (path 0) or
+    the 7 whose geometry its instances cover (path 4; 8-wave blocks of 512 rows, strips of 64
+    columns, dword RGB stores: nwidth 300), the others the two-kernel path; bytes equal the
+    oracle display of the device's own dB."""
     engine.set_render_path(path)
     try:
         tracks = pipeline.c5_tracks(12, seconds=3.0)
