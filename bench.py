@@ -515,6 +515,19 @@ def main_c5(args, ws, rank, pg, device):
                 res[q].append(tm.ms / 3)
         engine.set_batches_policy(0)
         pol_ms = {str(q): {"median": float(np.median(t)), "min": float(min(t))} for q, t in res.items()}
+    mb_ms = None
+    if args.max_blocks:  # per batch, each alone: its launch's block count (0 = occupancy default)
+        import numpy as np
+        ms = [int(v) for v in args.max_blocks.split(",")]
+        res = {(pl.n_fft, m): [] for pl, _, _, _ in p.groups for m in ms}
+        for _ in range(5):  # interleaved rounds
+            for pl, _, _, b in p.groups:
+                for m in ms:
+                    b.set_option(engine.OPT_MAX_BLOCKS, m)
+                    res[(pl.n_fft, m)].append(b.run_timed(3) / 3)
+        for _, _, _, b in p.groups:
+            b.set_option(engine.OPT_MAX_BLOCKS, 0)
+        mb_ms = {str(nf): {str(m): float(np.median(res[(nf, m)])) for m in ms} for nf in sorted({k[0] for k in res})}
     if args.render_paths:
         import numpy as np
         rp = [int(v) for v in args.render_paths.split(",")]
@@ -555,6 +568,7 @@ def main_c5(args, ws, rank, pg, device):
                          "kernel_ms_note": "sum of the batches' launches, each timed alone",
                          "overlapped_ms": kms_overlap,
                          "batches_policy_ms": pol_ms,
+                         "per_batch_max_blocks_ms": mb_ms,
                          "per_batch": [{"n_fft": nf, "frames": fr, "kernel_ms": t} for nf, fr, t in kms_batches],
                          "overlapped_note": "the step's spectrogram phase: the batches on the library "
                                             "streams (thesia_batches_run), HIP events on the library stream"},

@@ -737,6 +737,7 @@ int launch_render_batch(const float* spec, uint32_t bins, float max, float min,
 // tmp[oy][x] = sum_i grey[l + i][x] * w[i] in resize_v_px's order (t = 0; t += in * w), stored
 // along frames (coalesced). The grey image itself is never written (7.7 GB of the C5 step's
 // display traffic in the three-stage path).
+template <int SV>
 __global__ void __launch_bounds__(256) grey_vert_kernel(const float* spec, uint32_t bins, float max,
                                                         float min, uint32_t nh, const RenderDesc* d,
                                                         float* tmp, int tile_cap, int kv, uint32_t band) {
@@ -765,7 +766,53 @@ __global__ void __launch_bounds__(256) grey_vert_kernel(const float* spec, uint3
     const uint32_t x = x0 + lane;
     const int32_t H = (int32_t)r.H, top = (int32_t)r.H - (int32_t)bins;
     const float* sp = spec + r.spec_off;
-    if (staged) {
+    if (staged && SV == 1) {
+        // (frame, row) pairs flattened over the block's 256 threads (f = e / rows by a
+        // multiply-high, exact for e < 2^14): consecutive threads read consecutive bins of one
+        // frame (coalesced), a thread's THESIA_VDEPTH loads in flight together. Branch-free:
+        // indices past the tile repeat its last element (same value to the same slot), frames
+        // past T read frame T - 1 (their lanes store nothing), rows outside the track's band
+        // read a clamped bin and store +0 (the image's zero fill; padded taps below the image)
+        constexpr int D = THESIA_VDEPTH;
+        const int total = 64 * rows;
+        const uint32_t mrec = rows > 1 ? (uint32_t)((0x100000000ull + rows - 1) / (uint32_t)rows) : 0u;
+        const uint32_t emax = (uint32_t)total - 1;
+        const uint32_t flast = r.T - 1 - x0;  // x0 < T (block-uniform exit above)
+        const float* sb = sp + (uint64_t)x0 * bins;
+        auto split = [&](int i, int e0, uint32_t& f, int32_t& k) {
+            uint32_t e = (uint32_t)(e0 + 256 * i + tid);
+            e = e < emax ? e : emax;
+            f = rows > 1 ? __umulhi(e, mrec) : e;
+            k = (int32_t)(e - f * (uint32_t)rows);
+        };
+        for (int e0 = 0; e0 < total; e0 += 256 * D) {
+            float v[D];
+#pragma unroll
+            for (int i = 0; i < D; ++i) {
+                uint32_t f;
+                int32_t k;
+                split(i, e0, f, k);
+                const uint32_t fl = f < flast ? f : flast;
+                int32_t b = H - 1 - (ya + k);
+                b = b < 0 ? 0 : b < (int32_t)bins ? b : (int32_t)bins - 1;
+                v[i] = sb[(uint64_t)fl * bins + (uint32_t)b];
+            }
+#pragma unroll
+            for (int i = 0; i < D; ++i) {
+                uint32_t f;
+                int32_t k;
+                split(i, e0, f, k);
+                const int32_t y = ya + k;
+                tile[k * TS + f] = (y >= top && y < H) ? grey_of(v[i], max, min) : 0.0f;
+            }
+        }
+        for (uint32_t e = tid; e < nb * (uint32_t)kv; e += 256) {
+            const uint32_t j = e / (uint32_t)kv, i = e - j * (uint32_t)kv;
+            const int32_t n = r.vc[oy0 + j];
+            wl[e] = (int32_t)i < n ? r.vw[r.vo[oy0 + j] + i] : 0.0f;
+        }
+        for (uint32_t j = tid; j < nb; j += 256) meta[j] = r.vl[oy0 + j] - ya;
+    } else if (staged) {
         // (frame, row) pairs flattened over the block's 256 threads (f = e / rows by a
         // multiply-high, exact for e < 2^14): consecutive threads read consecutive bins of one
         // frame (coalesced) and a thread's THESIA_VDEPTH loads are in flight together; the zero
@@ -1186,12 +1233,18 @@ int launch_render_batch2(const float* spec, uint32_t bins, float max, float min,
         const int tile_cap = v_rows < 256 ? v_rows : 256;
         const int lds1 = ((((int)v_band + 3) & ~3) + ((tile_cap * 65 + 3) & ~3) + (int)v_band * kv) * 4;
         if (lds1 > 163840) return -2;
-        if (hipFuncSetAttribute(reinterpret_cast<const void*>(grey_vert_kernel),
-                                hipFuncAttributeMaxDynamicSharedMemorySize, lds1) != hipSuccess)
-            return -1;
+        // the branch-free staging (1; 0: the round-3 staging, THESIA_VSTAGE=0 in the experiment build)
+        int sv = 1;
+#ifdef THESIA_EXPERIMENTS
+        if (const char* e = getenv("THESIA_VSTAGE")) sv = atoi(e) == 0 ? 0 : 1;
+#endif
+        const void* vk = sv ? reinterpret_cast<const void*>(grey_vert_kernel<1>)
+                            : reinterpret_cast<const void*>(grey_vert_kernel<0>);
+        if (hipFuncSetAttribute(vk, hipFuncAttributeMaxDynamicSharedMemorySize, lds1) != hipSuccess) return -1;
         dim3 g1((T_max + 63) / 64, (nh + v_band - 1) / v_band, n);
-        hipLaunchKernelGGL(grey_vert_kernel, g1, dim3(256), lds1, s, spec, bins, max, min, nh, d_desc, tmp,
-                           tile_cap, kv, v_band);
+        void* vargs[] = {&spec, &bins, &max, &min, &nh, &d_desc, &tmp, const_cast<int*>(&tile_cap),
+                         const_cast<int*>(&kv), &v_band};
+        if (hipLaunchKernel(vk, g1, dim3(256), vargs, lds1, s) != hipSuccess) return -1;
     }
     // K5h + K6: the three-stage path's horizontal pass (same intermediate layout [nh][T])
     // row blocks per image: THESIA_RYH, more when few images would leave CUs idle

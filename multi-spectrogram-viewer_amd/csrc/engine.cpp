@@ -1519,8 +1519,12 @@ int plan_fused_group(const float* d_spec, const uint64_t* row0, size_t bins, siz
         *rows_out = rows;
         return rows <= cap && (int)band * kv <= 4096;
     };
+    int vrows_cap = THESIA_VROWS;
+#ifdef THESIA_EXPERIMENTS
+    if (const char* e = std::getenv("THESIA_VROWS_CAP")) vrows_cap = std::max(16, std::min(256, std::atoi(e)));
+#endif
     g.v_band = THESIA_VBAND;
-    while (!band_need(g.v_band, &g.v_rows, THESIA_VROWS) && g.v_band > 1) g.v_band /= 2;
+    while (!band_need(g.v_band, &g.v_rows, vrows_cap) && g.v_band > 1) g.v_band /= 2;
     g.v_fpl = 1;
     if (wide && g.H_max <= nheight) {
         // the wide vertical pass (4 frames per lane; its tile rows are 260 floats, so it holds

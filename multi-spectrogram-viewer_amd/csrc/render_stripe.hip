@@ -105,20 +105,23 @@ __global__ void __launch_bounds__(64 * WV) render_stripe_kernel(StripeLaunch L) 
     auto flush = [&](uint32_t c) {  // columns [c & ~15, c] of rows wr0 .. wr0 + 63
         const uint32_t cb = c & ~15u;
         const int n = (int)(c - cb) + 1;  // uniform
+        // all 16 slots straight-line (their sum reads, then their LUT reads, each batch in flight
+        // together): a partial piece's slots past n hold stale or unwritten sums, whose bytes
+        // land past 3n in the row piece and are never stored
+        float sv[16];
+#pragma unroll
+        for (int k = 0; k < 16; ++k) sv[k] = fsum[lane * kSumStride + k];
+        uint32_t px[16];
+#pragma unroll
+        for (int k = 0; k < 16; ++k) px[k] = colormap_rgb(sv[k], lut);
+        // 16 pixels x 3 bytes -> 12 dwords (bytes 3k .. 3k + 2 of the row piece)
         uint32_t d[12];
 #pragma unroll
-        for (int k = 0; k < 12; ++k) d[k] = 0;
-#pragma unroll
-        for (int k = 0; k < 16; ++k) {
-            if (k < n) {  // uniform
-                const uint32_t px = colormap_rgb(fsum[lane * kSumStride + k], lut);
-                // bytes 3k .. 3k + 2 of the row piece
-#pragma unroll
-                for (int ch = 0; ch < 3; ++ch) {
-                    const int o = 3 * k + ch;
-                    d[o >> 2] |= ((px >> (8 * ch)) & 0xFF) << (8 * (o & 3));
-                }
-            }
+        for (int q = 0; q < 4; ++q) {
+            const uint32_t a = px[4 * q], b = px[4 * q + 1], e = px[4 * q + 2], f = px[4 * q + 3];
+            d[3 * q] = a | (b << 24);
+            d[3 * q + 1] = (b >> 8) | (e << 16);
+            d[3 * q + 2] = (e >> 16) | (f << 8);
         }
         wave_sync();  // every lane's sums read
 #pragma unroll

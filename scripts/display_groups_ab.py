@@ -21,6 +21,7 @@ for g in range(12):
     for i in range(g, total, 12):
         tracks += pipeline.c5_tracks(1, seconds=10.0, first=i)
     p = pipeline.RenderPipeline(tracks, px_per_sec=100.0, nheight=500)
+    p._max_sr = 48000  # the C5 step's geometry: every group's up_ratio against the 48 kHz tracks
     p.run_spectrograms()
     times = {q: [] for q in paths}
     for _ in range(4):

@@ -14,6 +14,7 @@ tracks = []
 for i in range(g, 1000, 12):
     tracks += pipeline.c5_tracks(1, seconds=10.0, first=i)
 p = pipeline.RenderPipeline(tracks, px_per_sec=100.0, nheight=500)
+p._max_sr = 48000  # the C5 step's geometry: up_ratio against the 48 kHz tracks
 p.run_spectrograms()
 engine.set_render_path(path)
 t = p.display_timed(reps)
