@@ -1096,12 +1096,14 @@ template <int N>
 __device__ __forceinline__ void wait_vm() {
     asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
 }
-template <int KT, int K, int NB>
+// RP rows per barrier (RP = 2: NB groups of two rows, the two rows' sums and colormaps
+// interleaved; half the barriers and waits per row).
+template <int KT, int K, int NB, int RP>
 __global__ void __launch_bounds__(256) resize_h_dma_kernel(uint32_t nh, const RenderDesc* d, const float* tmp,
                                                            const uint8_t* cmap, uint8_t* rgb) {
     extern __shared__ __attribute__((aligned(16))) float hsm[];
     constexpr int BUF = K * 1024;  // floats per row buffer: K chunks of 64 lanes x 16 B per wave
-    uint2* lut = reinterpret_cast<uint2*>(hsm + NB * BUF);  // colormap_rgb's stop pairs
+    uint2* lut = reinterpret_cast<uint2*>(hsm + NB * RP * BUF);  // colormap_rgb's stop pairs
     const RenderDesc r = d[blockIdx.z];
     const uint32_t ox0 = blockIdx.x * 256;
     if (ox0 >= r.nw) return;  // block-uniform
@@ -1145,36 +1147,53 @@ __global__ void __launch_bounds__(256) resize_h_dma_kernel(uint32_t nh, const Re
     }
     const int nrows = y0 < nh ? (int)((nh - 1 - y0) / G) + 1 : 0;
     const float* rows0 = tmp + r.tmp_off + lb4;
-    auto dma = [&](int k) {
-        const float* row = rows0 + (uint64_t)(y0 + G * (uint32_t)k) * r.ts;
-        float* buf = hsm + (k % NB) * BUF;
+    // group g = rows g RP .. g RP + RP - 1 in buffers (g % NB) RP + i; rows past the last repeat
+    // it (same DMA count per group, so the counted waits hold; never summed)
+    auto dma = [&](int g) {
 #pragma unroll
-        for (int m = 0; m < K; ++m) {
-            const int c = (m * 4 + wave) * 64 + lane;
-            const int cc = c < nchunk ? c : nchunk - 1;
-            __builtin_amdgcn_global_load_lds((__attribute__((address_space(1))) void*)(row + 4 * cc),
-                                             (__attribute__((address_space(3))) void*)(buf + (m * 4 + wave) * 256),
-                                             16, 0, 0);
+        for (int i = 0; i < RP; ++i) {
+            int k = g * RP + i;
+            k = k < nrows ? k : nrows - 1;
+            const float* row = rows0 + (uint64_t)(y0 + G * (uint32_t)k) * r.ts;
+            float* buf = hsm + ((g % NB) * RP + i) * BUF;
+#pragma unroll
+            for (int m = 0; m < K; ++m) {
+                const int c = (m * 4 + wave) * 64 + lane;
+                const int cc = c < nchunk ? c : nchunk - 1;
+                __builtin_amdgcn_global_load_lds((__attribute__((address_space(1))) void*)(row + 4 * cc),
+                                                 (__attribute__((address_space(3))) void*)(buf + (m * 4 + wave) * 256),
+                                                 16, 0, 0);
+            }
         }
     };
-    for (int k = 0; k < NB - 1 && k < nrows; ++k) dma(k);
-    for (int k = 0; k < nrows; ++k, o += ostep) {
-        if (k + NB - 2 < nrows) wait_vm<(NB - 2) * K>();
+    const int ng = (nrows + RP - 1) / RP;
+    for (int g = 0; g < NB - 1 && g < ng; ++g) dma(g);
+    for (int g = 0; g < ng; ++g, o += RP * ostep) {
+        if (g + NB - 2 < ng) wait_vm<(NB - 2) * K * RP>();
         else wait_vm<0>();
         __builtin_amdgcn_s_barrier();
         asm volatile("" ::: "memory");
-        if (k + NB - 1 < nrows) dma(k + NB - 1);
+        if (g + NB - 1 < ng) dma(g + NB - 1);
         if (act) {
-            const float* rin = hsm + (k % NB) * BUF + base;
-            float t = 0.0f;
+            float t[RP];
 #pragma unroll
-            for (int i = 0; i < KT; ++i) t += rin[i] * w[i];
-            // the pair read in asm: the compiler cannot tell it from the DMA's LDS targets and
-            // would wait for every DMA in flight (vmcnt(0)) before a plain read
-            const CmapPos cp = colormap_pos(t);
-            uint2 e;
-            asm volatile("ds_read_b64 %0, %1\n\ts_waitcnt lgkmcnt(0)" : "=v"(e) : "v"(lut_lds + 8u * (uint32_t)cp.index));
-            put(o, colormap_lerp(e, cp.ratio));
+            for (int q = 0; q < RP; ++q) {
+                const float* rin = hsm + ((g % NB) * RP + q) * BUF + base;
+                t[q] = 0.0f;
+#pragma unroll
+                for (int i = 0; i < KT; ++i) t[q] += rin[i] * w[i];
+            }
+#pragma unroll
+            for (int q = 0; q < RP; ++q) {
+                if (g * RP + q < nrows) {  // uniform
+                    // the pair read in asm: the compiler cannot tell it from the DMA's LDS targets
+                    // and would wait for every DMA in flight (vmcnt(0)) before a plain read
+                    const CmapPos cp = colormap_pos(t[q]);
+                    uint2 e;
+                    asm volatile("ds_read_b64 %0, %1\n\ts_waitcnt lgkmcnt(0)" : "=v"(e) : "v"(lut_lds + 8u * (uint32_t)cp.index));
+                    put(o + q * ostep, colormap_lerp(e, cp.ratio));
+                }
+            }
         }
     }
 }
@@ -1189,11 +1208,18 @@ static int launch_resize_h_dma(uint32_t nh, const RenderDesc* d_desc, uint32_t n
     const int need = h_span + 4 + kt;
     const int K = need <= 1024 ? 1 : need <= 2048 ? 2 : need <= 4096 ? 4 : 0;
     if (!K) return -2;
-    constexpr int NB = 4;  // row buffers (3 and 6 measured slower: 3.40 / 3.42 vs 3.36 ms per C5 step)
-    const int lds = NB * K * 1024 * 4 + 80;  // + the colormap pairs
+    constexpr int NB = 4;  // row groups in flight (3 and 6 measured slower: 3.40 / 3.42 vs 3.36 ms per C5 step)
+    // rows per barrier: 2 where the two rows' buffers stay small (K = 1)
+    int rp = 1;
+#ifdef THESIA_EXPERIMENTS
+    if (const char* e = getenv("THESIA_HRP")) rp = atoi(e) == 2 && K == 1 ? 2 : 1;
+#endif
+    const int lds = NB * rp * K * 1024 * 4 + 80;  // + the colormap pairs
     const void* kern = nullptr;
-#define THESIA_HDMA(KT_, K_) \
-    if (kt == KT_ && K == K_) kern = reinterpret_cast<const void*>(resize_h_dma_kernel<KT_, K_, NB>);
+#define THESIA_HDMA(KT_, K_)                                                                          \
+    if (kt == KT_ && K == K_)                                                                         \
+        kern = rp == 2 && K_ == 1 ? reinterpret_cast<const void*>(resize_h_dma_kernel<KT_, K_, NB, 2>) \
+                                  : reinterpret_cast<const void*>(resize_h_dma_kernel<KT_, K_, NB, 1>);
     THESIA_HDMA(8, 1) THESIA_HDMA(8, 2) THESIA_HDMA(8, 4)
     THESIA_HDMA(16, 1) THESIA_HDMA(16, 2) THESIA_HDMA(16, 4)
     THESIA_HDMA(32, 1) THESIA_HDMA(32, 2) THESIA_HDMA(32, 4)
@@ -1216,11 +1242,12 @@ int launch_render_batch2(const float* spec, uint32_t bins, float max, float min,
     if (n > 65535) return -2;
     (void)H_max;
     const int kv = (v_kv + 3) & ~3;
-    if (v_fpl == 4) {
+    if (v_fpl == 4 || v_fpl == 2) {
         // K4+K5v wide: every band's grey rows fit the tile (host: v_rows <= the FPL's cap)
         const int lds1 = grey_vert_wide_lds_bytes(v_fpl, v_band, v_rows, kv);
         if (lds1 > 163840) return -2;
-        const void* kern = reinterpret_cast<const void*>(grey_vert_wide_kernel<4>);
+        const void* kern = v_fpl == 4 ? reinterpret_cast<const void*>(grey_vert_wide_kernel<4>)
+                                      : reinterpret_cast<const void*>(grey_vert_wide_kernel<2>);
         if (hipFuncSetAttribute(kern, hipFuncAttributeMaxDynamicSharedMemorySize, lds1) != hipSuccess) return -1;
         const uint32_t fw = 64u * (uint32_t)v_fpl;
         dim3 g1((T_max + fw - 1) / fw, (nh + v_band - 1) / v_band, n);

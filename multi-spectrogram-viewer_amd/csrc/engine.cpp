@@ -1542,6 +1542,20 @@ int plan_fused_group(const float* d_spec, const uint64_t* row0, size_t bins, siz
             g.v_rows = rows;
         }
     }
+#ifdef THESIA_EXPERIMENTS
+    // two frames per lane (132-float tile rows, at most 80 of them) for the other groups where a
+    // band of at least 16 output rows fits (THESIA_VFPL2=1)
+    if (wide && g.v_fpl == 1 && std::getenv("THESIA_VFPL2") && std::atoi(std::getenv("THESIA_VFPL2")) == 1) {
+        uint32_t band = THESIA_VBAND;
+        int rows = 1;
+        while (!band_need(band, &rows, 80) && band > 1) band /= 2;
+        if (band >= 16 && band_need(band, &rows, 80)) {
+            g.v_fpl = 2;
+            g.v_band = band;
+            g.v_rows = rows;
+        }
+    }
+#endif
     return THESIA_OK;
 }
 
