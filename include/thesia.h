@@ -190,8 +190,9 @@ int thesia_batches_run(thesia_batch* const* batches, size_t n, void* stream);
 /* Process-wide block-count policy of thesia_batches_run for batches whose block count is
  * automatic (THESIA_BATCH_OPT_MAX_BLOCKS 0): 0 (default) = each batch sized for the whole
  * device, as thesia_batch_run; 1 = the batches share one occupancy wave of the device in
- * proportion to their work (frames x n_fft log2 n_fft), so each frame stream walks more frames.
- * Same results either way; 1 measured 1.6x slower on the C5 batches. */
+ * proportion to their work (frames x n_fft log2 n_fft), so each frame stream walks more frames;
+ * 2 = one after another on `stream`, each sized for the whole device (no fork). Same results
+ * every way; 1 measured 1.6x slower on the C5 batches. */
 int thesia_set_batches_policy(int policy);
 /* Runs `iters` passes bracketed by HIP events on the launch stream; returns the elapsed
  * milliseconds of all passes (synchronous). */

@@ -737,7 +737,6 @@ int launch_render_batch(const float* spec, uint32_t bins, float max, float min,
 // tmp[oy][x] = sum_i grey[l + i][x] * w[i] in resize_v_px's order (t = 0; t += in * w), stored
 // along frames (coalesced). The grey image itself is never written (7.7 GB of the C5 step's
 // display traffic in the three-stage path).
-template <int SV>
 __global__ void __launch_bounds__(256) grey_vert_kernel(const float* spec, uint32_t bins, float max,
                                                         float min, uint32_t nh, const RenderDesc* d,
                                                         float* tmp, int tile_cap, int kv, uint32_t band) {
@@ -766,7 +765,7 @@ __global__ void __launch_bounds__(256) grey_vert_kernel(const float* spec, uint3
     const uint32_t x = x0 + lane;
     const int32_t H = (int32_t)r.H, top = (int32_t)r.H - (int32_t)bins;
     const float* sp = spec + r.spec_off;
-    if (staged && SV == 1) {
+    if (staged) {
         // (frame, row) pairs flattened over the block's 256 threads (f = e / rows by a
         // multiply-high, exact for e < 2^14): consecutive threads read consecutive bins of one
         // frame (coalesced), a thread's THESIA_VDEPTH loads in flight together. Branch-free:
@@ -804,40 +803,6 @@ __global__ void __launch_bounds__(256) grey_vert_kernel(const float* spec, uint3
                 split(i, e0, f, k);
                 const int32_t y = ya + k;
                 tile[k * TS + f] = (y >= top && y < H) ? grey_of(v[i], max, min) : 0.0f;
-            }
-        }
-        for (uint32_t e = tid; e < nb * (uint32_t)kv; e += 256) {
-            const uint32_t j = e / (uint32_t)kv, i = e - j * (uint32_t)kv;
-            const int32_t n = r.vc[oy0 + j];
-            wl[e] = (int32_t)i < n ? r.vw[r.vo[oy0 + j] + i] : 0.0f;
-        }
-        for (uint32_t j = tid; j < nb; j += 256) meta[j] = r.vl[oy0 + j] - ya;
-    } else if (staged) {
-        // (frame, row) pairs flattened over the block's 256 threads (f = e / rows by a
-        // multiply-high, exact for e < 2^14): consecutive threads read consecutive bins of one
-        // frame (coalesced) and a thread's THESIA_VDEPTH loads are in flight together; the zero
-        // fill above the track's band (y < top), rows past the image and frames past T are
-        // never loaded
-        constexpr int D = THESIA_VDEPTH;
-        const int total = 64 * rows;
-        const uint32_t mrec = rows > 1 ? (uint32_t)((0x100000000ull + rows - 1) / (uint32_t)rows) : 0u;
-        for (int e0 = 0; e0 < total; e0 += 256 * D) {
-            float v[D];
-#pragma unroll
-            for (int i = 0; i < D; ++i) {
-                const uint32_t e = (uint32_t)(e0 + 256 * i + tid);
-                const uint32_t f = rows > 1 ? __umulhi(e, mrec) : e;
-                const int32_t k = (int32_t)(e - f * (uint32_t)rows), y = ya + k;
-                v[i] = 0.0f;
-                if ((int)e < total && y >= top && y < H && x0 + f < r.T)
-                    v[i] = sp[(uint64_t)(x0 + f) * bins + (uint32_t)(H - 1 - y)];
-            }
-#pragma unroll
-            for (int i = 0; i < D; ++i) {
-                const uint32_t e = (uint32_t)(e0 + 256 * i + tid);
-                const uint32_t f = rows > 1 ? __umulhi(e, mrec) : e;
-                const int32_t k = (int32_t)(e - f * (uint32_t)rows), y = ya + k;
-                if ((int)e < total) tile[k * TS + f] = (y >= top && y < H) ? grey_of(v[i], max, min) : 0.0f;
             }
         }
         for (uint32_t e = tid; e < nb * (uint32_t)kv; e += 256) {
@@ -1096,9 +1061,10 @@ template <int N>
 __device__ __forceinline__ void wait_vm() {
     asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
 }
-// RP rows per barrier (RP = 2: NB groups of two rows, the two rows' sums and colormaps
-// interleaved; half the barriers and waits per row).
-template <int KT, int K, int NB, int RP>
+// RP rows per barrier (groups of RP rows in NB x RP buffers). The launcher uses 1: two rows per
+// barrier, both rows' sums and colormaps interleaved, measured no faster (C5 step 3.86 vs 3.81 ms,
+// profiles/r04_display/ab_experiments.txt).
+template <int KT, int K, int NB, int RP = 1>
 __global__ void __launch_bounds__(256) resize_h_dma_kernel(uint32_t nh, const RenderDesc* d, const float* tmp,
                                                            const uint8_t* cmap, uint8_t* rgb) {
     extern __shared__ __attribute__((aligned(16))) float hsm[];
@@ -1208,18 +1174,11 @@ static int launch_resize_h_dma(uint32_t nh, const RenderDesc* d_desc, uint32_t n
     const int need = h_span + 4 + kt;
     const int K = need <= 1024 ? 1 : need <= 2048 ? 2 : need <= 4096 ? 4 : 0;
     if (!K) return -2;
-    constexpr int NB = 4;  // row groups in flight (3 and 6 measured slower: 3.40 / 3.42 vs 3.36 ms per C5 step)
-    // rows per barrier: 2 where the two rows' buffers stay small (K = 1)
-    int rp = 1;
-#ifdef THESIA_EXPERIMENTS
-    if (const char* e = getenv("THESIA_HRP")) rp = atoi(e) == 2 && K == 1 ? 2 : 1;
-#endif
-    const int lds = NB * rp * K * 1024 * 4 + 80;  // + the colormap pairs
+    constexpr int NB = 4;  // row buffers (3 and 6 measured slower: 3.40 / 3.42 vs 3.36 ms per C5 step)
+    const int lds = NB * K * 1024 * 4 + 80;  // + the colormap pairs
     const void* kern = nullptr;
-#define THESIA_HDMA(KT_, K_)                                                                          \
-    if (kt == KT_ && K == K_)                                                                         \
-        kern = rp == 2 && K_ == 1 ? reinterpret_cast<const void*>(resize_h_dma_kernel<KT_, K_, NB, 2>) \
-                                  : reinterpret_cast<const void*>(resize_h_dma_kernel<KT_, K_, NB, 1>);
+#define THESIA_HDMA(KT_, K_) \
+    if (kt == KT_ && K == K_) kern = reinterpret_cast<const void*>(resize_h_dma_kernel<KT_, K_, NB>);
     THESIA_HDMA(8, 1) THESIA_HDMA(8, 2) THESIA_HDMA(8, 4)
     THESIA_HDMA(16, 1) THESIA_HDMA(16, 2) THESIA_HDMA(16, 4)
     THESIA_HDMA(32, 1) THESIA_HDMA(32, 2) THESIA_HDMA(32, 4)
@@ -1260,13 +1219,7 @@ int launch_render_batch2(const float* spec, uint32_t bins, float max, float min,
         const int tile_cap = v_rows < 256 ? v_rows : 256;
         const int lds1 = ((((int)v_band + 3) & ~3) + ((tile_cap * 65 + 3) & ~3) + (int)v_band * kv) * 4;
         if (lds1 > 163840) return -2;
-        // the branch-free staging (1; 0: the round-3 staging, THESIA_VSTAGE=0 in the experiment build)
-        int sv = 1;
-#ifdef THESIA_EXPERIMENTS
-        if (const char* e = getenv("THESIA_VSTAGE")) sv = atoi(e) == 0 ? 0 : 1;
-#endif
-        const void* vk = sv ? reinterpret_cast<const void*>(grey_vert_kernel<1>)
-                            : reinterpret_cast<const void*>(grey_vert_kernel<0>);
+        const void* vk = reinterpret_cast<const void*>(grey_vert_kernel);
         if (hipFuncSetAttribute(vk, hipFuncAttributeMaxDynamicSharedMemorySize, lds1) != hipSuccess) return -1;
         dim3 g1((T_max + 63) / 64, (nh + v_band - 1) / v_band, n);
         void* vargs[] = {&spec, &bins, &max, &min, &nh, &d_desc, &tmp, const_cast<int*>(&tile_cap),

@@ -949,6 +949,13 @@ int batches_run(Batch* const* b, size_t n, hipStream_t s) {
         if (std::adjacent_find(seen.begin(), seen.end()) != seen.end() || seen.front() == nullptr)
             return set_error(THESIA_ERR_INVALID_ARG, "batches_run: a batch handle appears twice (or is null)");
     }
+    if (batches_policy() == 2) {  // one after another on the caller's stream
+        for (size_t i = 0; i < n; ++i) {
+            const int rc = batch_run(b[i], s);
+            if (rc) return rc;
+        }
+        return THESIA_OK;
+    }
     std::lock_guard<std::mutex> lk(run_pool_mutex());
     RunPool* p = nullptr;
     int rc = run_pool(&p);
@@ -983,7 +990,7 @@ int batches_run(Batch* const* b, size_t n, hipStream_t s) {
 static int g_batches_policy = 0;  // thesia_set_batches_policy
 int batches_policy() { return __atomic_load_n(&g_batches_policy, __ATOMIC_RELAXED); }
 int set_batches_policy(int policy) {
-    if (policy < 0 || policy > 1) return set_error(THESIA_ERR_INVALID_ARG, "batches policy must be 0 or 1");
+    if (policy < 0 || policy > 2) return set_error(THESIA_ERR_INVALID_ARG, "batches policy must be 0, 1 or 2");
     __atomic_store_n(&g_batches_policy, policy, __ATOMIC_RELAXED);
     return THESIA_OK;
 }
@@ -1344,7 +1351,8 @@ struct FusedGroup {
     // geometry (plan_stripe); then no intermediate is formed
     bool stripe = false;
     uint32_t st_strip = 64;
-    int st_kv = 0, st_slots = 0, st_fc = 0, st_npf = 0, st_waves = 4, st_tile = 0, st_hdr = 0, st_wts = 0;
+    int st_kv = 0, st_slots = 0, st_acc = 0, st_fc = 0, st_npf = 0, st_waves = 4, st_tile = 0, st_hdr = 0,
+        st_wts = 0;
     bool st_dword = false;
 };
 
@@ -1424,10 +1432,13 @@ void plan_stripe(const std::vector<StripeTrack>& trk, uint32_t bins, uint32_t nh
     // the instances compiled (render_stripe.hip launch_render_stripe)
     if (kv > 8) npf = 16;
     const int slots_run = kv > 8 ? 16 : slots;
+    // accumulators: the exact count where an instance has it (9, 10 on the 12-wide table)
+    const int acc_run = kv > 8 ? 16 : (slots == 12 && amax <= 10) ? std::max(9, amax) : slots;
     if (fc == 8) npf = 16;
     g.stripe = true;
     g.st_kv = kv;
     g.st_slots = slots_run;
+    g.st_acc = acc_run;
     g.st_fc = fc;
     g.st_npf = npf;
     g.st_waves = waves;
@@ -1519,12 +1530,8 @@ int plan_fused_group(const float* d_spec, const uint64_t* row0, size_t bins, siz
         *rows_out = rows;
         return rows <= cap && (int)band * kv <= 4096;
     };
-    int vrows_cap = THESIA_VROWS;
-#ifdef THESIA_EXPERIMENTS
-    if (const char* e = std::getenv("THESIA_VROWS_CAP")) vrows_cap = std::max(16, std::min(256, std::atoi(e)));
-#endif
     g.v_band = THESIA_VBAND;
-    while (!band_need(g.v_band, &g.v_rows, vrows_cap) && g.v_band > 1) g.v_band /= 2;
+    while (!band_need(g.v_band, &g.v_rows, THESIA_VROWS) && g.v_band > 1) g.v_band /= 2;
     g.v_fpl = 1;
     if (wide && g.H_max <= nheight) {
         // the wide vertical pass (4 frames per lane; its tile rows are 260 floats, so it holds
@@ -1542,20 +1549,6 @@ int plan_fused_group(const float* d_spec, const uint64_t* row0, size_t bins, siz
             g.v_rows = rows;
         }
     }
-#ifdef THESIA_EXPERIMENTS
-    // two frames per lane (132-float tile rows, at most 80 of them) for the other groups where a
-    // band of at least 16 output rows fits (THESIA_VFPL2=1)
-    if (wide && g.v_fpl == 1 && std::getenv("THESIA_VFPL2") && std::atoi(std::getenv("THESIA_VFPL2")) == 1) {
-        uint32_t band = THESIA_VBAND;
-        int rows = 1;
-        while (!band_need(band, &rows, 80) && band > 1) band /= 2;
-        if (band >= 16 && band_need(band, &rows, 80)) {
-            g.v_fpl = 2;
-            g.v_band = band;
-            g.v_rows = rows;
-        }
-    }
-#endif
     return THESIA_OK;
 }
 
@@ -1688,6 +1681,7 @@ int render_rgb_fused(size_t n_groups, const float* const* d_specs, const uint64_
                 L.strip = g.st_strip;
                 L.kv = g.st_kv;
                 L.slots = g.st_slots;
+                L.acc = g.st_acc;
                 L.fc = g.st_fc;
                 L.npf = g.st_npf;
                 L.waves = g.st_waves;

@@ -208,9 +208,10 @@ int launch_render_batch2(const float* spec, uint32_t bins, float max, float min,
 // horizontal Lanczos3 + colormap in one kernel, the f32 intermediate never leaving registers.
 // A block owns `strip` output columns (a multiple of 16) x 64 `waves` output rows of one track,
 // each wave 64 of the rows; its geometry bounds (host, plan_stripe): kv vertical taps (8, 12 or 16,
-// zero-padded), at most `slots` columns meeting one 8-frame step (8, 12 or 16), fc frames per staged
-// chunk (8 or 16), npf staged values per lane and chunk (8 or 16), at most tile_cap grey rows
-// per wave, hdr_cap steps and wts_cap step weights per strip. -2 when no instance fits.
+// zero-padded), at most `acc` columns meeting one 8-frame step (the accumulators: 8 .. 12 or 16),
+// the step table's row stride `slots` (8, 12 or 16 >= acc), fc frames per staged chunk (8 or 16),
+// npf staged values per lane and chunk (8 or 16), at most tile_cap grey rows per wave, hdr_cap
+// steps and wts_cap step weights per strip. -2 when no instance fits.
 struct StripeLaunch {
     const float* spec;
     uint32_t bins;
@@ -220,7 +221,7 @@ struct StripeLaunch {
     uint32_t n;          // tracks (grid.z)
     uint32_t nw_max;
     uint32_t strip;      // output columns per block (multiple of 16)
-    int kv, slots, fc, npf;
+    int kv, slots, acc, fc, npf;
     int waves;           // per block (4 or 8: 256 or 512 output rows)
     int tile_cap, hdr_cap, wts_cap;
     bool dword_rgb;      // every track's nw and rgb_off are multiples of 4 (dword RGB stores)

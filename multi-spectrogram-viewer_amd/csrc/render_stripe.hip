@@ -54,7 +54,9 @@ __device__ __forceinline__ void wave_sync() {  // cross-lane LDS ordering within
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
-template <int KV, int A, int FC, int NPF, int WV>
+// A accumulators (columns meeting a step), AW the step table's row stride (A rounded up to 4; its
+// entries past A are zero and never read into a sum)
+template <int KV, int A, int AW, int FC, int NPF, int WV>
 __global__ void __launch_bounds__(64 * WV) render_stripe_kernel(StripeLaunch L) {
     constexpr int kRows = 64 * WV;  // output rows per block (lane = row)
     extern __shared__ __attribute__((aligned(16))) float sm[];
@@ -91,10 +93,10 @@ __global__ void __launch_bounds__(64 * WV) render_stripe_kernel(StripeLaunch L) 
     const int s_hi = (r.hl[c1 - 1] + r.hc[c1 - 1] - 1) >> 3;
     const int nst = s_hi - s_lo + 1;  // <= hdr_cap (host)
     const int* gh = r.hst + s_lo;
-    const float* gw = r.hsw + (uint64_t)s_lo * 8 * A;
+    const float* gw = r.hsw + (uint64_t)s_lo * 8 * AW;
     if (tid < 10) lut[tid] = colormap_pair(L.cmap, tid);
     for (int i = tid; i < nst; i += kRows) hdr[i] = gh[i];
-    for (int i = tid; i < nst * 2 * A; i += kRows)  // nst x 8 x A floats <= wts_cap (host)
+    for (int i = tid; i < nst * 2 * AW; i += kRows)  // nst x 8 x AW floats <= wts_cap (host)
         reinterpret_cast<float4*>(wts)[i] = reinterpret_cast<const float4*>(gw)[i];
     __syncthreads();  // the only block barrier: the waves run on their own from here
 
@@ -290,28 +292,28 @@ __global__ void __launch_bounds__(64 * WV) render_stripe_kernel(StripeLaunch L) 
             // horizontal: every slot's chain takes the step's frames in ascending order (the
             // resize_h order; slots outside a column's support add (+0 weight) x v = +-0); the
             // weights of frame u + 1 are read while frame u is summed
-            const float4* wu = reinterpret_cast<const float4*>(wts + si * 8 * A);
-            float4 xc[A / 4];
+            constexpr int A4 = (A + 3) / 4;  // float4 weight reads per frame
+            const float4* wu = reinterpret_cast<const float4*>(wts + si * 8 * AW);
+            float4 xc[A4];
 #pragma unroll
-            for (int a4 = 0; a4 < A / 4; ++a4) xc[a4] = wu[a4];
+            for (int a4 = 0; a4 < A4; ++a4) xc[a4] = wu[a4];
 #pragma unroll
             for (int u = 0; u < 8; ++u) {
-                float4 xn[A / 4];
+                float4 xn[A4];
                 if (u + 1 < 8) {
 #pragma unroll
-                    for (int a4 = 0; a4 < A / 4; ++a4) xn[a4] = wu[(u + 1) * (A / 4) + a4];
+                    for (int a4 = 0; a4 < A4; ++a4) xn[a4] = wu[(u + 1) * (AW / 4) + a4];
                 }
 #pragma unroll
-                for (int a4 = 0; a4 < A / 4; ++a4) {
-                    acc[4 * a4] = acc[4 * a4] + v[u] * xc[a4].x;
-                    acc[4 * a4 + 1] = acc[4 * a4 + 1] + v[u] * xc[a4].y;
-                    acc[4 * a4 + 2] = acc[4 * a4 + 2] + v[u] * xc[a4].z;
-                    acc[4 * a4 + 3] = acc[4 * a4 + 3] + v[u] * xc[a4].w;
+                for (int a = 0; a < A; ++a) {
+                    const float4 x = xc[a / 4];
+                    const float wgt = (a & 3) == 0 ? x.x : (a & 3) == 1 ? x.y : (a & 3) == 2 ? x.z : x.w;
+                    acc[a] = acc[a] + v[u] * wgt;
                 }
                 pin_mem(acc);
                 if (u + 1 < 8) {
 #pragma unroll
-                    for (int a4 = 0; a4 < A / 4; ++a4) xc[a4] = xn[a4];
+                    for (int a4 = 0; a4 < A4; ++a4) xc[a4] = xn[a4];
                 }
             }
             // the columns whose supports end in this step (all of the strip's at its last):
@@ -332,10 +334,10 @@ __global__ void __launch_bounds__(64 * WV) render_stripe_kernel(StripeLaunch L) 
     }
 }
 
-template <int KV, int A, int FC, int NPF>
+template <int KV, int A, int AW, int FC, int NPF>
 const void* stripe_kernel(int waves) {
-    return waves == 8 ? reinterpret_cast<const void*>(render_stripe_kernel<KV, A, FC, NPF, 8>)
-                      : reinterpret_cast<const void*>(render_stripe_kernel<KV, A, FC, NPF, 4>);
+    return waves == 8 ? reinterpret_cast<const void*>(render_stripe_kernel<KV, A, AW, FC, NPF, 8>)
+                      : reinterpret_cast<const void*>(render_stripe_kernel<KV, A, AW, FC, NPF, 4>);
 }
 
 }  // namespace
@@ -350,14 +352,19 @@ int launch_render_stripe(const StripeLaunch& L, hipStream_t s) {
     if (L.n > 65535 || L.strip == 0 || (L.strip & 15) || (L.waves != 4 && L.waves != 8)) return -2;
     const void* kern = nullptr;
     // the instances (host plan_stripe picks among them): KV 8 (the groups that upsample
-    // vertically) with 8 / 12 / 16 slots; KV 12 / 16 (downsampling) with 16
-#define THESIA_STRIPE(KV_, A_, FC_, NPF_) \
-    if (L.kv == KV_ && L.slots == A_ && L.fc == FC_ && L.npf == NPF_) kern = stripe_kernel<KV_, A_, FC_, NPF_>(L.waves);
-    THESIA_STRIPE(8, 8, 16, 8) THESIA_STRIPE(8, 8, 16, 16) THESIA_STRIPE(8, 8, 8, 16)
-    THESIA_STRIPE(8, 12, 16, 8) THESIA_STRIPE(8, 12, 16, 16) THESIA_STRIPE(8, 12, 8, 16)
-    THESIA_STRIPE(8, 16, 16, 8) THESIA_STRIPE(8, 16, 16, 16) THESIA_STRIPE(8, 16, 8, 16)
-    THESIA_STRIPE(12, 16, 16, 16) THESIA_STRIPE(12, 16, 8, 16)
-    THESIA_STRIPE(16, 16, 16, 16) THESIA_STRIPE(16, 16, 8, 16)
+    // vertically) with 8 / 9 / 10 / 12 / 16 accumulators (9 and 10 on the 12-wide step table: the
+    // 48 kHz / 512 and 22.05 kHz / 256 C5 groups meet at most 9 columns per step); KV 12 / 16
+    // (downsampling) with 16
+#define THESIA_STRIPE(KV_, A_, AW_, FC_, NPF_)                                                     \
+    if (L.kv == KV_ && L.acc == A_ && L.slots == AW_ && L.fc == FC_ && L.npf == NPF_)             \
+        kern = stripe_kernel<KV_, A_, AW_, FC_, NPF_>(L.waves);
+    THESIA_STRIPE(8, 8, 8, 16, 8) THESIA_STRIPE(8, 8, 8, 16, 16) THESIA_STRIPE(8, 8, 8, 8, 16)
+    THESIA_STRIPE(8, 9, 12, 16, 8) THESIA_STRIPE(8, 9, 12, 16, 16) THESIA_STRIPE(8, 9, 12, 8, 16)
+    THESIA_STRIPE(8, 10, 12, 16, 8) THESIA_STRIPE(8, 10, 12, 16, 16) THESIA_STRIPE(8, 10, 12, 8, 16)
+    THESIA_STRIPE(8, 12, 12, 16, 8) THESIA_STRIPE(8, 12, 12, 16, 16) THESIA_STRIPE(8, 12, 12, 8, 16)
+    THESIA_STRIPE(8, 16, 16, 16, 8) THESIA_STRIPE(8, 16, 16, 16, 16) THESIA_STRIPE(8, 16, 16, 8, 16)
+    THESIA_STRIPE(12, 16, 16, 16, 16) THESIA_STRIPE(12, 16, 16, 8, 16)
+    THESIA_STRIPE(16, 16, 16, 16, 16) THESIA_STRIPE(16, 16, 16, 8, 16)
 #undef THESIA_STRIPE
     if (!kern) return -2;
     const int lds = render_stripe_lds_bytes(L.fc, L.tile_cap, L.hdr_cap, L.wts_cap, L.waves);

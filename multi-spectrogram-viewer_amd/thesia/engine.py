@@ -238,8 +238,9 @@ def run_batches(batches, stream=None) -> None:
 
 
 def set_batches_policy(policy: int) -> None:
-    """thesia_set_batches_policy: 0 (default) = each batch sized for the whole device; 1 =
-    concurrent batches share one occupancy wave by work (measured slower)."""
+    """thesia_set_batches_policy: 0 (default) = each batch sized for the whole device, the
+    batches concurrent on the library streams; 1 = concurrent batches share one occupancy wave by
+    work (measured slower); 2 = the batches one after another on the caller's stream."""
     check(lib.thesia_set_batches_policy(policy))
 
 
