@@ -773,36 +773,39 @@ __global__ void __launch_bounds__(256) grey_vert_kernel(const float* spec, uint3
         // past T read frame T - 1 (their lanes store nothing), rows outside the track's band
         // read a clamped bin and store +0 (the image's zero fill; padded taps below the image)
         constexpr int D = THESIA_VDEPTH;
-        const int total = 64 * rows;
-        const uint32_t mrec = rows > 1 ? (uint32_t)((0x100000000ull + rows - 1) / (uint32_t)rows) : 0u;
+        const int total = 64 * rows;  // rows >= kv >= 4 (host): the reciprocal below is exact
+        const uint32_t mrec = (uint32_t)((0x100000000ull + rows - 1) / (uint32_t)rows);
         const uint32_t emax = (uint32_t)total - 1;
         const uint32_t flast = r.T - 1 - x0;  // x0 < T (block-uniform exit above)
-        const float* sb = sp + (uint64_t)x0 * bins;
-        auto split = [&](int i, int e0, uint32_t& f, int32_t& k) {
-            uint32_t e = (uint32_t)(e0 + 256 * i + tid);
-            e = e < emax ? e : emax;
-            f = rows > 1 ? __umulhi(e, mrec) : e;
-            k = (int32_t)(e - f * (uint32_t)rows);
-        };
+        // the block's frames as a buffer resource: 32-bit byte offsets from frame x0 (at most
+        // 64 frames x bins floats), one buffer_load per element
+        const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+            const_cast<float*>(sp + (uint64_t)x0 * bins), (short)0, -1, 0x00020000);
+        const int32_t hy = H - 1 - ya;  // bin of tile row k: hy - k
         for (int e0 = 0; e0 < total; e0 += 256 * D) {
             float v[D];
+            uint32_t fk[D];  // (frame, tile row) of each element: f | k << 8 (f < 64, k < 256)
 #pragma unroll
             for (int i = 0; i < D; ++i) {
-                uint32_t f;
-                int32_t k;
-                split(i, e0, f, k);
+                uint32_t e = (uint32_t)(e0 + 256 * i + tid);
+                e = e < emax ? e : emax;
+                const uint32_t f = __umulhi(e, mrec);
+                const int32_t k = (int32_t)(e - f * (uint32_t)rows);
+                fk[i] = f | ((uint32_t)k << 8);
                 const uint32_t fl = f < flast ? f : flast;
-                int32_t b = H - 1 - (ya + k);
+                int32_t b = hy - k;
                 b = b < 0 ? 0 : b < (int32_t)bins ? b : (int32_t)bins - 1;
-                v[i] = sb[(uint64_t)fl * bins + (uint32_t)b];
+                v[i] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rs, (fl * bins + (uint32_t)b) * 4u, 0, 0));
             }
 #pragma unroll
             for (int i = 0; i < D; ++i) {
-                uint32_t f;
-                int32_t k;
-                split(i, e0, f, k);
+                const uint32_t f = fk[i] & 255u;
+                const int32_t k = (int32_t)(fk[i] >> 8);
                 const int32_t y = ya + k;
-                tile[k * TS + f] = (y >= top && y < H) ? grey_of(v[i], max, min) : 0.0f;
+                // formed for every element (pinned: a select, not a branch around the division)
+                float g = grey_of(v[i], max, min);
+                asm volatile("" : "+v"(g));
+                tile[k * TS + (int32_t)f] = (y >= top && y < H) ? g : 0.0f;
             }
         }
         for (uint32_t e = tid; e < nb * (uint32_t)kv; e += 256) {
@@ -1174,7 +1177,9 @@ static int launch_resize_h_dma(uint32_t nh, const RenderDesc* d_desc, uint32_t n
     const int need = h_span + 4 + kt;
     const int K = need <= 1024 ? 1 : need <= 2048 ? 2 : need <= 4096 ? 4 : 0;
     if (!K) return -2;
-    constexpr int NB = 4;  // row buffers (3 and 6 measured slower: 3.40 / 3.42 vs 3.36 ms per C5 step)
+    // row buffers (3 and 6 measured slower: 3.40 / 3.42 vs 3.36 ms per C5 step; round 4, 8 for the
+    // one-chunk spans: 3.88 vs 3.84 ms, profiles/r04_display/ab_experiments.txt)
+    constexpr int NB = 4;
     const int lds = NB * K * 1024 * 4 + 80;  // + the colormap pairs
     const void* kern = nullptr;
 #define THESIA_HDMA(KT_, K_) \
