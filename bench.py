@@ -500,6 +500,17 @@ def main_c5(args, ws, rank, pg, device):
             p.run_spectrograms()
     kms_overlap = tm.ms / 3
     disp = p.display_timed(3)
+    # the display's stored PMC record (this geometry, one GPU, render path 0): HBM traffic beside
+    # the algorithmic bytes, and its VALU issue roofline (the passes are issue- and
+    # latency-bound; the f32 intermediate of the two-kernel groups and the halo re-reads are the
+    # traffic above algorithmic)
+    drec = profile_record({"workload": "c5_display", "tracks": total, "seconds": args.seconds,
+                           "px_per_sec": 100.0, "nheight": 500, "render_path": max(args.render_path, 0)}) \
+        if ws == 1 else None
+    disp.pop("traffic_note", None)
+    disp["traffic"] = drec["hbm_bytes_per_launch"] if drec else None
+    disp["traffic_source"] = provenance(drec) if drec else "no stored PMC record of this exact workload"
+    disp_ic = issue_ceiling(drec, disp["display_ms"]) if drec else None
     pol_ms = None
     if args.spec_policies:
         import numpy as np
@@ -573,6 +584,7 @@ def main_c5(args, ws, rank, pg, device):
                          "overlapped_note": "the step's spectrogram phase: the batches on the library "
                                             "streams (thesia_batches_run), HIP events on the library stream"},
             "roofline_display": disp,
+            "roofline_display_valu_issue": disp_ic,
         }), flush=True)
     p.close()
 

@@ -215,7 +215,7 @@ class RenderPipeline:
         b = self.display_bytes()
         ach = b["total"] / (ms * 1e-3) / 1e9
         return {"bound": "hbm", "achieved": ach, "peak": 8000.0, "unit": "GB/s", "frac": ach / 8000.0,
-                "traffic": None, "traffic_note": "PMC per step in profiles/r02_c5 (FETCH/WRITE_SIZE: intermediate written 2.79 GB + read 2.97 GB, RGB 1.55 GB)",
+                "traffic": None,
                 "display_ms": ms, "algorithmic_bytes": b,
                 "kernel": "per-track range + grey/vertical Lanczos3 + horizontal Lanczos3 + colormap"}
 
