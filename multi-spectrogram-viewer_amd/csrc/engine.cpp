@@ -769,8 +769,11 @@ int batch_create(Plan* plan, const thesia_batch_desc& d, Batch** out) {
     b->k3_ok = plan->use_v2 && stft3_supports((int)plan->n_fft, (int)plan->win, (int)plan->hop,
                                               d.input_format, (int)d.channels) &&
                stft3_lds_bytes(L) <= 163840;  // the mel weights must fit LDS (else stft2)
+    // (the viewer geometry runs stft5 for the mel and linear kinds only: complex rows stay on stft3)
+    const bool view5 = !(plan->win == plan->n_fft && plan->hop * 4 == plan->n_fft);
     const bool k5_geo = b->k3_ok && stft5_supports((int)plan->n_fft, (int)plan->win, (int)plan->hop,
-                                                   d.input_format, (int)d.channels);
+                                                   d.input_format, (int)d.channels) &&
+                        !(view5 && L.out_kind == OUT_COMPLEX);
     if (k5_geo && L.melp_chunks && stft5_lds_bytes(L) > 163840) {  // packed stream too big: rounds
         b->mel_path = 1;
         b->apply_mel_path();

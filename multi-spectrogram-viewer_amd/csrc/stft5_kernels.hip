@@ -226,10 +226,19 @@ __device__ __forceinline__ void melp5(const StftLaunch& a, float* region, const 
 // (points 8 t .. 8 t + 7 of the lane's 32) lives in physical group (t + ph) & 3, the hop's new
 // samples overwrite the oldest group and ph advances (no 48 v_mov per frame pair); the first
 // radix-4 level, the only reader, is compiled once per phase behind a uniform branch.
-template <int OK, int C, int INF, int VAR = 0>
+// HQ > 0: a viewer geometry with an even hop (lib.rs:43-46: 48 kHz, win 1920 / hop 480 /
+// n_fft 2048: hop / 2 = 240 points = HQ 7 rows of 32 + rem 16), stft3's column rule
+// (stft3_kernel.hpp): lane j keeps the points of one residue mod L of the track's point grid, so
+// frame t finds them in its column jc = (j - t rem) mod L; a new frame shifts the ring by HQ rows
+// where the previous column was >= rem and by HQ + 1 where it was < rem (a select per row) and
+// takes HQ + 1 prefetched rows; the window row, the stage-1 twiddles and the transpose's write
+// column are jc's, and from the transpose's reads on (rows A = j, B = 32 - j) the lane is j.
+template <int OK, int C, int INF, int VAR = 0, int HQ = 0>
 __global__ void __launch_bounds__(Geo5::BLOCK, Geo5::WV / 4)
 stft5_kernel(StftLaunch a, uint64_t fps, int rs) {
     constexpr bool kRot = (VAR & 1) != 0;
+    constexpr bool VIEW = HQ > 0;
+    static_assert(!(VIEW && kRot), "the phase ring is for the canonical hop");
     using G = Geo5;
     using CK = Chunk<C, INF>;
     using CT = typename CK::T;
@@ -237,6 +246,9 @@ stft5_kernel(StftLaunch a, uint64_t fps, int rs) {
     constexpr int NC = G::NC, P = G::P, L = G::L, FPW = G::FPW, F = G::F, SH = G::SH, S = G::S;
     constexpr int kBlock = G::BLOCK;
     constexpr bool kStage = OK == 1;  // linear kinds: LDS-staged 16-byte row stores
+    constexpr int NPRE = VIEW ? HQ + 1 : SH;  // rows prefetched per frame
+    constexpr int KEEP = P - NPRE;            // ring rows carried into the next frame
+    static_assert(KEEP > 0, "hop shorter than the frame");
 
     extern __shared__ __attribute__((aligned(16))) float lds[];
     constexpr int kTab = G::TAB_FLOATS + (kRot ? 3 * G::TW_FLOATS : 0);
@@ -304,7 +316,8 @@ stft5_kernel(StftLaunch a, uint64_t fps, int rs) {
     const ET* in = static_cast<const ET*>(a.in);
 
     float2 raw[P];
-    CT pre[SH];
+    CT pre[NPRE];
+    const int rem = VIEW ? (hop >> 1) & (L - 1) : 0;
     bool pre_ok = false;
     int ph = 0;  // kRot: physical group of logical group 0 (wave-uniform)
     int hint = -1;
@@ -327,7 +340,6 @@ stft5_kernel(StftLaunch a, uint64_t fps, int rs) {
         // bins) inside the loop instead of hoisted as loop invariants into dozens of VGPRs
         int wj = j, wjb = jb, wkb = kb_lo;
         asm volatile("" : "+v"(wj), "+v"(wjb), "+v"(wkb));
-        const float4* wrow = reinterpret_cast<const float4*>(wtl + wj * G::WL_STRIDE);
         SI start = 0;
         if (valid) {
             if (g >= g_end || g < g_beg) {
@@ -338,6 +350,14 @@ stft5_kernel(StftLaunch a, uint64_t fps, int rs) {
                 base = a.trk_in_off[hint];
             }
             start = (SI)(g - g_beg) * hop - NC;  // half_win = NC, pad_left = 0
+        }
+        // the frame's column (HQ > 0): (j - frame start in points) mod L; window, twiddles and
+        // the transpose's write column follow it
+        int jc = j, wc = wj;  // (canonical geometry: the opaque wj, no further register)
+        if constexpr (VIEW) {
+            if (valid) jc = (j - (int)((start >> 1) & (L - 1))) & (L - 1);
+            wc = jc;
+            asm volatile("" : "+v"(wc));
         }
         // ---- the frame's raw samples: shift by SH points + the prefetched hop ----
         if (pre_ok && kRot) {
@@ -355,12 +375,21 @@ stft5_kernel(StftLaunch a, uint64_t fps, int rs) {
             else ins(std::integral_constant<int, 3>{});
             ph = (p0 + 1) & 3;
         } else if (pre_ok) {
+            if constexpr (VIEW) {
+                const bool up = ((jc + rem) & (L - 1)) < rem;  // the previous column < rem
 #pragma unroll
-            for (int n1 = 0; n1 < P - SH; ++n1) raw[n1] = raw[n1 + SH];
+                for (int n1 = 0; n1 < KEEP; ++n1) {
+                    raw[n1].x = up ? raw[n1 + HQ + 1].x : raw[n1 + HQ].x;
+                    raw[n1].y = up ? raw[n1 + HQ + 1].y : raw[n1 + HQ].y;
+                }
+            } else {
 #pragma unroll
-            for (int q = 0; q < SH; ++q) raw[P - SH + q] = CK::mix(pre[q]);
+                for (int n1 = 0; n1 < KEEP; ++n1) raw[n1] = raw[n1 + SH];
+            }
+#pragma unroll
+            for (int q = 0; q < NPRE; ++q) raw[KEEP + q] = CK::mix(pre[q]);
         } else if (valid && start >= 0 && start + 2 * NC <= n && ((base + (uint64_t)start * C) % (2 * C)) == 0) {
-            const CT* src = reinterpret_cast<const CT*>(in + base + (uint64_t)start * C) + j;
+            const CT* src = reinterpret_cast<const CT*>(in + base + (uint64_t)start * C) + jc;
             static_for<0, P / 8>([&](auto gc) {
                 constexpr int g8 = decltype(gc)::value;
                 static_for<0, 8>([&](auto ic) {
@@ -370,24 +399,26 @@ stft5_kernel(StftLaunch a, uint64_t fps, int rs) {
                 pin_range<8 * g8, 8 * g8 + 8>(raw);
             });
         } else if (valid) {
-            load_raw_generic_ool<NC, INF>(a, region, j, start, n, base, C, a.fold != 0, raw);
+            load_raw_generic_ool<NC, INF>(a, region, jc, start, n, base, C, a.fold != 0, raw);
         } else {
 #pragma unroll
             for (int n1 = 0; n1 < P; ++n1) raw[n1] = make_float2(0.f, 0.f);
         }
         if (!(pre_ok && kRot)) ph = 0;  // a reloaded ring is in logical order
         MARK5(loaded, 0);
+        const float4* wrow = reinterpret_cast<const float4*>(wtl + wc * G::WL_STRIDE);
         // ---- prefetch the next frame's hop of new samples (its points P-SH .. P-1) right
         // away: a whole frame to land, as stft3 ----
         auto prefetch = [&]() {
             const SI nstart = start + hop;
             const bool nxt = valid && g + 1 < g1 && g + 1 < g_end && nstart + 2 * NC <= n &&
-                             nstart + 2 * L * (P - SH) >= 0 &&
-                             ((base + (uint64_t)(nstart + 2 * L * (P - SH)) * C) % (2 * C)) == 0;
+                             nstart + 2 * L * KEEP >= 0 &&
+                             ((base + (uint64_t)(nstart + 2 * L * KEEP) * C) % (2 * C)) == 0;
             if (nxt) {
-                const CT* src = reinterpret_cast<const CT*>(in + base + (uint64_t)(nstart + 2 * L * (P - SH)) * C) + j;
+                const int jn = (jc - rem) & (L - 1);  // the next frame's column (= j unless HQ > 0)
+                const CT* src = reinterpret_cast<const CT*>(in + base + (uint64_t)(nstart + 2 * L * KEEP) * C) + jn;
 #pragma unroll
-                for (int q = 0; q < SH; ++q) pre[q] = src[L * q];
+                for (int q = 0; q < NPRE; ++q) pre[q] = src[L * q];
             }
             pre_ok = nxt;
         };
@@ -437,7 +468,7 @@ stft5_kernel(StftLaunch a, uint64_t fps, int rs) {
         pin(v);
         MARK5(stage1, 1);
         {
-            const float4* tp = reinterpret_cast<const float4*>(twtab) + wj + phs * (P / 2 * L);
+            const float4* tp = reinterpret_cast<const float4*>(twtab) + wc + phs * (P / 2 * L);
             static_for<0, P / 2 / G::TWC>([&](auto cc) {
                 constexpr int c0 = decltype(cc)::value * G::TWC;
                 __builtin_amdgcn_sched_barrier(0);
@@ -463,7 +494,7 @@ stft5_kernel(StftLaunch a, uint64_t fps, int rs) {
             static_for<0, P>([&](auto kc) {
                 constexpr int k1 = decltype(kc)::value;
                 constexpr int pk = ce_pos(P, k1);
-                region[k1 * S + j] = e == 0 ? v[pk].x : v[pk].y;
+                region[k1 * S + wc] = e == 0 ? v[pk].x : v[pk].y;
             });
             wave_lds_sync();
             // row A lands in the component just written out: A[n] into v[n].e (e = re / im;
@@ -629,7 +660,7 @@ static int region_stride5(const StftLaunch& a) {
     return lds5_bytes<OK, VAR>(a, Geo5::RS) <= 163840 ? Geo5::RS : Geo5::RS_MIN;
 }
 
-template <int OK, int C, int INF, int VAR = 0>
+template <int OK, int C, int INF, int VAR = 0, int HQ = 0>
 static int launch5_k(const StftLaunch& a, hipStream_t stream) {
 #ifdef THESIA_EXPERIMENTS
     if constexpr (VAR == 0 && C == 2 && INF == IN_F32) {
@@ -640,7 +671,7 @@ static int launch5_k(const StftLaunch& a, hipStream_t stream) {
     const int rs = region_stride5<OK, VAR>(a);
     const int lds = lds5_bytes<OK, VAR>(a, rs);
     if (lds > 163840) return -2;
-    auto kern = stft5_kernel<OK, C, INF, VAR>;
+    auto kern = stft5_kernel<OK, C, INF, VAR, HQ>;
     if (hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
                             hipFuncAttributeMaxDynamicSharedMemorySize, lds) != hipSuccess)
         return -1;
@@ -655,10 +686,18 @@ static int launch5_k(const StftLaunch& a, hipStream_t stream) {
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
+// the viewer geometry (HQ 7: hop 480, win <= 2048) for the mel and linear kinds (complex rows
+// stay on stft3, which is faster for them)
+static bool view5(const StftLaunch& a) { return !(a.win == 2048 && a.hop * 4 == 2048); }
 template <int C, int INF>
 static int launch5_c(const StftLaunch& a, hipStream_t s) {
+    const bool mel = a.out_kind == OUT_MEL || a.out_kind == OUT_MEL_AMP_DB;
+    if (view5(a)) {
+        if (a.out_kind == OUT_COMPLEX) return -2;
+        return mel ? launch5_k<2, C, INF, 0, 7>(a, s) : launch5_k<1, C, INF, 0, 7>(a, s);
+    }
     if (a.out_kind == OUT_COMPLEX) return launch5_k<0, C, INF>(a, s);
-    if (a.out_kind == OUT_MEL || a.out_kind == OUT_MEL_AMP_DB) return launch5_k<2, C, INF>(a, s);
+    if (mel) return launch5_k<2, C, INF>(a, s);
     return launch5_k<1, C, INF>(a, s);
 }
 
@@ -669,8 +708,12 @@ int stft5_lds_bytes(const StftLaunch& a) {
 }
 
 bool stft5_supports(int n_fft, int win, int hop, int in_format, int channels) {
-    return n_fft == 2048 && win == n_fft && hop * 4 == n_fft &&
-           (in_format == IN_F32 || in_format == IN_S16) && (channels == 1 || channels == 2);
+    // the canonical geometry, or the 48 kHz viewer one (hop / 2 = 7 rows of 32 + 16; an even win
+    // <= n_fft, as the streaming start rule needs, stft3v_kernels.hip)
+    const bool canon = win == n_fft && hop * 4 == n_fft;
+    const bool view = hop % 2 == 0 && (hop / 2) / 32 == 7 && win <= n_fft && win % 2 == 0 && win >= 2;
+    return n_fft == 2048 && (canon || view) && (in_format == IN_F32 || in_format == IN_S16) &&
+           (channels == 1 || channels == 2);
 }
 
 int launch_stft5(const StftLaunch& a, hipStream_t s) {

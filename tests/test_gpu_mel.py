@@ -161,10 +161,15 @@ def test_kernel_choice_and_unsupported_force():
     din = engine.DeviceBuffer.from_host(x[:, 0].copy())
     dout = engine.DeviceBuffer(engine.Batch.frames_for(plan, [4096]) * plan.row_bins * 4)
     b = engine.Batch(plan, din, [0], [4096], dout)
-    assert b.kernel == 3
+    assert b.kernel == 5  # stft5's viewer column rule (HQ 7) for the mel and linear kinds
+    b.set_option(engine.OPT_KERNEL, 3)
     import thesia
+    plan = engine.Plan(2048, 1920, 480, engine.OUT_COMPLEX)  # complex rows: stft3 only
+    dout = engine.DeviceBuffer(engine.Batch.frames_for(plan, [4096]) * plan.row_bins * 8)
+    b = engine.Batch(plan, din, [0], [4096], dout)
+    assert b.kernel == 3
     with pytest.raises(thesia.ThesiaError):
-        b.set_option(engine.OPT_KERNEL, 5)  # stft5: the canonical geometry only
+        b.set_option(engine.OPT_KERNEL, 5)
     plan = engine.Plan(2048, 1764, 441, engine.OUT_AMP_DB)  # 44.1 kHz viewer geometry: odd hop,
     x16 = np.zeros(4096, np.int16)                          # s16 mono (2-byte-aligned loads) streams
     din = engine.DeviceBuffer.from_host(x16)

@@ -93,6 +93,58 @@ def test_viewer_geometry_complex_streams(n_fft, win, hop, channels, fmt, gap):
 _KINDS = [engine.OUT_MAG, engine.OUT_POWER, engine.OUT_AMP_DB, engine.OUT_POWER_DB]
 
 
+def _auto(n_fft, hop):
+    """The automatic kernel for the mel / linear kinds: stft5 (its viewer column rule,
+    stft5_kernels.hip HQ 7) at the 48 kHz geometry, stft3 at the others."""
+    return 5 if (n_fft, hop) == (2048, 480) else 3
+
+
+def _check_kind(kind, g, ref, fb=None):
+    if kind == engine.OUT_MEL_AMP_DB:
+        want = O.amp_to_db_default(O.dot(O.norm(ref), fb))
+    elif kind == engine.OUT_MAG:
+        want = O.norm(ref)
+    elif kind == engine.OUT_POWER:
+        want = O.norm_sqr(ref)
+    elif kind == engine.OUT_AMP_DB:
+        want = O.amp_to_db_default(O.norm(ref))
+    else:
+        want = O.power_to_db_default(O.norm_sqr(ref))
+    if kind in (engine.OUT_AMP_DB, engine.OUT_POWER_DB, engine.OUT_MEL_AMP_DB):
+        mx, p = db_clamped_err(g, want)
+        assert mx <= DB_MAX and p <= DB_P9999, (mx, p)
+    else:
+        scale = np.abs(want).max(axis=1, keepdims=True)
+        rel = 4e-6 if kind == engine.OUT_MAG else 8e-6
+        assert np.all(np.abs(g - want) <= rel * np.maximum(scale, 1e-30)), float(np.abs(g - want).max())
+
+
+@pytest.mark.parametrize("kernel", [5, 3])
+@pytest.mark.parametrize("kind", _KINDS + [engine.OUT_MEL_AMP_DB])
+@pytest.mark.parametrize("channels,fmt", [(1, engine.IN_F32), (2, engine.IN_F32), (2, engine.IN_S16),
+                                          (1, engine.IN_S16)])
+@pytest.mark.parametrize("gap,max_blocks", [(0, 1), (3, 2), (0, 0)])
+def test_viewer_48k_stft5_column_rule(kernel, kind, channels, fmt, gap, max_blocks):
+    """stft5 at the 48 kHz viewer geometry (win 1920 / hop 480 / n_fft 2048: hop / 2 = 7 rows of
+    32 + 16, the ring's per-lane select shift and the column-rotated window, twiddles and
+    transpose writes) and stft3 forced at the same inputs, both against the oracle: streams
+    across track ends, tracks at odd element offsets (gap 3: per-frame reloads), the shortest
+    legal track, one block (every stream walks hundreds of frames through the rotation)."""
+    n_fft, win, hop, sr = 2048, 1920, 480, 48000
+    rng = np.random.default_rng(kind * 13 + channels * 5 + fmt + gap + 7 * max_blocks)
+    lens = [win - 1, 5 * n_fft + 3, 33 * hop + 1, 97 * hop + 2, 211 * hop + 11]
+    tracks = _tracks(rng, lens, channels, fmt)
+    mel = kind == engine.OUT_MEL_AMP_DB
+    plan = engine.Plan(n_fft, win, hop, kind, **({"sr": sr, "n_mels": 128} if mel else {}))
+    k, rows = _run(plan, tracks, channels, fmt, gap, max_blocks=max_blocks, kernel=kernel)
+    plan.close()
+    assert k == kernel
+    fb = O.calc_mel_fb(sr, n_fft, 128) if mel else None
+    for t, r in zip(tracks, rows):
+        ref = O.perform_stft(_x(t, fmt), win, hop, n_fft)
+        _check_kind(kind, r.reshape(ref.shape[0], -1), ref, fb)
+
+
 @pytest.mark.parametrize("n_fft,win,hop", VIEW + VIEW_ODD)
 @pytest.mark.parametrize("kind", _KINDS)
 @pytest.mark.parametrize("max_blocks", [0, 2])
@@ -103,7 +155,7 @@ def test_viewer_geometry_linear_kinds(n_fft, win, hop, kind, max_blocks):
     plan = engine.Plan(n_fft, win, hop, kind)
     k, rows = _run(plan, tracks, 2, engine.IN_F32, 0, max_blocks=max_blocks)
     plan.close()
-    assert k == 3
+    assert k == _auto(n_fft, hop)
     for t, r in zip(tracks, rows):
         ref = O.perform_stft(_x(t, engine.IN_F32), win, hop, n_fft)
         g = r.reshape(ref.shape[0], -1)
@@ -136,7 +188,7 @@ def test_viewer_geometry_mel_db(n_fft, win, hop, sr, n_mels):
     plan = engine.Plan(n_fft, win, hop, engine.OUT_MEL_AMP_DB, sr=sr, n_mels=n_mels)
     k, rows = _run(plan, tracks, 1, fmt, 0, max_blocks=2)
     plan.close()
-    assert k == 3
+    assert k == _auto(n_fft, hop)
     fb = O.calc_mel_fb(sr, n_fft, n_mels)
     for t, r in zip(tracks, rows):
         ref = O.perform_stft(_x(t, fmt), win, hop, n_fft)
