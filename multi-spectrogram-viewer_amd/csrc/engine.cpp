@@ -1514,7 +1514,16 @@ int plan_fused_group(const float* d_spec, const uint64_t* row0, size_t bins, siz
                 cost += (uint64_t)desc[i].T * bins + (3ull * desc[i].nw * nheight) / 4;
             }
             g.tmp_tot = 0;
-            g.cost = cost;
+            // the stream scheduling's cost is in HBM floats moved; the single-pass kernel is
+            // compute-bound (VALU and latency: per track ~1.8x the time of a two-kernel group of the
+            // same floats on C5), so its floats count 3 times (C5 display 2.52 / 2.51 -> 2.50 /
+            // 2.48 ms vs 1x; 5x 2.50 / 2.50, profiles/r04_display/ab_experiments.txt;
+            // THESIA_STRIPE_COST in the experiment build)
+            uint64_t factor = 3;
+#ifdef THESIA_EXPERIMENTS
+            if (const char* e = std::getenv("THESIA_STRIPE_COST")) factor = (uint64_t)std::max(1, std::atoi(e));
+#endif
+            g.cost = cost * factor;
         }
     }
     // taps per row padded to kv (a multiple of 4, zero weights): the tile holds the band's
