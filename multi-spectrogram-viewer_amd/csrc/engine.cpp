@@ -1395,7 +1395,7 @@ void plan_stripe(const std::vector<StripeTrack>& trk, uint32_t bins, uint32_t nh
     int kvmax = 0, amax = 0;
     bool dword = true;
     for (const StripeTrack& t : trk) {
-        if ((uint64_t)t.T * bins >= (1ull << 32)) return;  // the kernel's 32-bit row offsets
+        if ((uint64_t)t.T * bins >= (1ull << 30)) return;  // the kernel's 32-bit byte offsets
         kvmax = std::max(kvmax, t.vt->max_taps);
         amax = std::max(amax, t.ht->st_maxna);
         dword = dword && t.nw % 4 == 0 && t.rgb_off % 4 == 0;
@@ -1694,6 +1694,10 @@ int render_rgb_fused(size_t n_groups, const float* const* d_specs, const uint64_
                 L.kv = g.st_kv;
                 L.slots = g.st_slots;
                 L.acc = g.st_acc;
+                L.abl = 0;
+#ifdef THESIA_EXPERIMENTS
+                if (const char* e = std::getenv("THESIA_STRIPE_ABL")) L.abl = std::atoi(e);
+#endif
                 L.fc = g.st_fc;
                 L.npf = g.st_npf;
                 L.waves = g.st_waves;

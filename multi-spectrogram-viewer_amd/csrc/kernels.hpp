@@ -227,6 +227,7 @@ struct StripeLaunch {
     bool dword_rgb;      // every track's nw and rgb_off are multiples of 4 (dword RGB stores)
     const uint8_t* cmap;
     uint8_t* rgb;
+    int abl;             // experiment build only (THESIA_STRIPE_ABL, timing ablations): 0
 };
 int launch_render_stripe(const StripeLaunch& L, hipStream_t s);
 int render_stripe_lds_bytes(int fc, int tile_cap, int hdr_cap, int wts_cap, int waves);

@@ -147,7 +147,16 @@ __global__ void __launch_bounds__(64 * WV) render_stripe_kernel(StripeLaunch L) 
         }
         wave_sync();
     };
+#ifdef THESIA_EXPERIMENTS
+    const int abl = L.abl;  // timing ablations: 1 no staging past chunk 0, 2 no emission, 4 no horizontal sums
+#else
+    constexpr int abl = 0;
+#endif
     auto close_col = [&](uint32_t c, float t) {  // c in [c0, c1), ascending
+        if (abl & 2) {
+            if (t == 1.2345e-30f) fsum[lane] = t;  // keep the sums live
+            return;
+        }
         fsum[lane * kSumStride + (c & 15)] = t;
         if ((c & 15) == 15 || c + 1 == c1) flush(c);
     };
@@ -182,11 +191,18 @@ __global__ void __launch_bounds__(64 * WV) render_stripe_kernel(StripeLaunch L) 
     // past T to frame T - 1 (duplicate loads / identical stores; frames past T only ever meet
     // zero horizontal weights, so any finite value will do): no per-element branches
     float pf[NPF];
+    // each staged element's (frame, bin) kept from issue() to commit() as fi | bi << 8 where the
+    // registers fit under 128 VGPRs (4 waves / SIMD), else formed again in commit()
+    constexpr bool kKeep = NPF == 8 || (KV == 8 && A <= 12);
+    uint32_t pk[kKeep ? NPF : 1];
     const uint32_t emax = (uint32_t)(tot > 0 ? tot - 1 : 0);
+    // the track's dB rows as a buffer resource: 32-bit byte offsets (a track's rows < 2^30
+    // floats, host), one buffer_load per element
+    const __amdgpu_buffer_rsrc_t rsc = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(sp), (short)0, -1, 0x00020000);
     auto issue = [&](int k) {  // chunk k's dB values -> registers
         const uint32_t fb = (uint32_t)(F0 + k * FC);
-        // opaque per call: the element indices and addresses are formed per chunk, not hoisted
-        // out of the frame loop into NPF x 3 registers held across it
+        // opaque per call: the element indices are formed per chunk, not hoisted out of the
+        // frame loop into NPF x 3 registers held across it
         int li = lane;
         asm volatile("" : "+v"(li));
 #pragma unroll
@@ -196,25 +212,33 @@ __global__ void __launch_bounds__(64 * WV) render_stripe_kernel(StripeLaunch L) 
             e = e < emax ? e : emax;
             const uint32_t fi = nb > 1 ? __umulhi(e, mrec) : e;
             const uint32_t bi = e - fi * (uint32_t)nb;
+            if constexpr (kKeep) pk[j] = fi | (bi << 8);  // fi < FC <= 16, bi < nb <= tile rows
             uint32_t f = fb + fi;
             f = f < T ? f : T - 1;
-            pf[j] = sp[f * (uint32_t)bins + (uint32_t)b_lo + bi];  // a track's rows < 2^32 floats (host)
+            pf[j] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(
+                rsc, (f * (uint32_t)bins + (uint32_t)b_lo + bi) * 4u, 0, 0));
         }
     };
+    const int q0 = H - 1 - b_lo - ya;  // tile row of staged bin bi: q0 - bi
     auto commit = [&](int) {  // registers -> grey values in the tile (its previous chunk read)
         float* t = tile;
-        // the element indices are formed again here, not kept from issue() across the steps
-        int lc = lane;
+        int lc = lane;  // (recomputing: opaque, as in issue())
         asm volatile("" : "+v"(lc));
 #pragma unroll
         for (int j = 0; j < NPF; ++j) {
             if (64 * j >= tot) break;  // uniform
-            uint32_t e = (uint32_t)(lc + 64 * j);
-            e = e < emax ? e : emax;
-            const uint32_t fi = nb > 1 ? __umulhi(e, mrec) : e;
-            const uint32_t bi = e - fi * (uint32_t)nb;
-            const int q = H - 1 - (b_lo + (int)bi) - ya;
-            t[q * TS + (int)fi] = grey_of(pf[j], L.max, L.min);
+            int fi, bi;
+            if constexpr (kKeep) {
+                fi = (int)(pk[j] & 255u);
+                bi = (int)(pk[j] >> 8);
+            } else {
+                uint32_t e = (uint32_t)(lc + 64 * j);
+                e = e < emax ? e : emax;
+                const uint32_t f = nb > 1 ? __umulhi(e, mrec) : e;
+                fi = (int)f;
+                bi = (int)(e - f * (uint32_t)nb);
+            }
+            t[(q0 - bi) * TS + fi] = grey_of(pf[j], L.max, L.min);
         }
     };
 
@@ -252,7 +276,7 @@ __global__ void __launch_bounds__(64 * WV) render_stripe_kernel(StripeLaunch L) 
     // slot a <-> column ca(s) + a of the step's table (columns before c0, finished by the strip
     // on the left, and from c1 on are summed too and never stored)
     for (int k = 0; k < nchunks; ++k) {
-        if (k + 1 < nchunks && nb) issue(k + 1);
+        if (k + 1 < nchunks && nb && !(abl & 1)) issue(k + 1);
         const float* t = tile + q * TS;
         for (int u8 = 0; u8 < SPC; ++u8) {
             const int si = k * SPC + u8;
@@ -304,11 +328,15 @@ __global__ void __launch_bounds__(64 * WV) render_stripe_kernel(StripeLaunch L) 
 #pragma unroll
                     for (int a4 = 0; a4 < A4; ++a4) xn[a4] = wu[(u + 1) * (AW / 4) + a4];
                 }
+                if (!(abl & 4)) {
 #pragma unroll
-                for (int a = 0; a < A; ++a) {
-                    const float4 x = xc[a / 4];
-                    const float wgt = (a & 3) == 0 ? x.x : (a & 3) == 1 ? x.y : (a & 3) == 2 ? x.z : x.w;
-                    acc[a] = acc[a] + v[u] * wgt;
+                    for (int a = 0; a < A; ++a) {
+                        const float4 x = xc[a / 4];
+                        const float wgt = (a & 3) == 0 ? x.x : (a & 3) == 1 ? x.y : (a & 3) == 2 ? x.z : x.w;
+                        acc[a] = acc[a] + v[u] * wgt;
+                    }
+                } else {
+                    acc[u & (A - 1) & 7] += v[u];  // keep the vertical sums live
                 }
                 pin_mem(acc);
                 if (u + 1 < 8) {
@@ -326,7 +354,7 @@ __global__ void __launch_bounds__(64 * WV) render_stripe_kernel(StripeLaunch L) 
                 acc[A - 1] = 0.0f;
             }
         }
-        if (k + 1 < nchunks && nb) {
+        if (k + 1 < nchunks && nb && !(abl & 1)) {
             wave_sync();  // every lane's reads of the buffer chunk k + 1 overwrites are done
             commit(k + 1);
             wave_sync();
