@@ -156,9 +156,11 @@ class RenderPipeline:
         return out
 
     def render(self, group=None, keep_db: bool = False, want_rgb: bool = True) -> List[Rendered]:
-        engine.synchronize()
+        # (the range readback is ordered on the library stream after the spectrogram batches,
+        # which thesia_batches_run joins back into it, and waits for it: no device-wide sync)
         mx, mn = self._range_arrays()
-        lmx, lmn = shard.local_range(mx.tolist(), mn.tolist())
+        lmx = float(mx.max()) if mx.size else -np.inf  # shard.local_range over numpy arrays
+        lmn = float(mn.min()) if mn.size else np.inf
         gmax, gmin, max_sr = shard.global_db_range(lmx, lmn, self._max_sr, db_range=self.db_range, group=group)
         up = self._up.get(max_sr)
         if up is None:

@@ -126,7 +126,7 @@ def global_db_range(local_max: float, local_min: float, local_max_sr: int, db_ra
         active = dist.is_available() and dist.is_initialized()
     except ImportError:  # pragma: no cover - torch is in the image
         active = False
-    if active:
+    if active and dist.get_world_size(group) > 1:
         g = _host_group(dist, group)
         t = torch.tensor([mx, -mn, float(sr)], dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX, group=g)
