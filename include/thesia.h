@@ -326,6 +326,21 @@ int thesia_render_rgb_multi(size_t n_groups, const float* const* d_specs, const 
                             const size_t* bins, const size_t* ns, const float* up_ratio,
                             const uint32_t* nwidth, uint32_t nheight, float max, float min,
                             uint8_t* d_rgb, const uint64_t* rgb_off);
+/* The display's global range without a host round trip (single-device callers): the global
+ * (max, min) dB over n tracks' THESIA_BATCH_OPT_RANGE slots d_trk_range (3 ints per track, as
+ * the batches leave them), as lib.rs:194-209 computes it -- NaN-holding tracks skipped, max =
+ * min(max, 0), min = max(min, max - db_range) -- written to d_out[0], d_out[1] (device floats)
+ * by one kernel on the library stream. Asynchronous. Multi-device callers exchange the per-rank
+ * ranges on the host instead (thesia.shard.global_db_range). */
+int thesia_ranges_global(const int* d_trk_range, size_t n, float db_range, float* d_out);
+/* thesia_render_rgb_multi with the (max, min) read from the device (d_range[0], d_range[1], e.g.
+ * thesia_ranges_global's output) when the kernels run: the whole step -- batches, range, display
+ * -- enqueues without a host synchronisation. Render paths 0, 3, 4 (THESIA_ERR_UNSUPPORTED
+ * otherwise). Same bytes as thesia_render_rgb_multi with those values. */
+int thesia_render_rgb_multi_dev(size_t n_groups, const float* const* d_specs, const uint64_t* const* row0s,
+                                const size_t* bins, const size_t* ns, const float* up_ratio,
+                                const uint32_t* nwidth, uint32_t nheight, const float* d_range,
+                                uint8_t* d_rgb, const uint64_t* rgb_off);
 
 /* ---------------------------------------------------------------------------------- */
 /* MultiTrack -- lib.rs:72-365 (the viewer's stateful surface)                          */

@@ -554,6 +554,36 @@ int thesia_render_rgb_multi(size_t n_groups, const float* const* d_specs, const 
     GUARD_END
 }
 
+int thesia_ranges_global(const int* d_trk_range, size_t n, float db_range, float* d_out) {
+    GUARD_BEGIN
+    if (!d_out || (n && !d_trk_range)) return set_error(THESIA_ERR_INVALID_ARG, "null device pointer");
+    if (n > 0xFFFFFFFFull) return set_error(THESIA_ERR_INVALID_ARG, "too many tracks");
+    if (launch_range_global(d_trk_range, (uint32_t)n, (double)db_range, d_out, default_stream()))
+        return set_error(THESIA_ERR_DEVICE, "range_global launch failed");
+    return THESIA_OK;
+    GUARD_END
+}
+
+int thesia_render_rgb_multi_dev(size_t n_groups, const float* const* d_specs, const uint64_t* const* row0s,
+                                const size_t* bins, const size_t* ns, const float* up_ratio,
+                                const uint32_t* nwidth, uint32_t nheight, const float* d_range,
+                                uint8_t* d_rgb, const uint64_t* rgb_off) {
+    GUARD_BEGIN
+    size_t tot = 0;
+    if (!d_range) return set_error(THESIA_ERR_INVALID_ARG, "null device range");
+    if (n_groups && (!d_specs || !row0s || !bins || !ns)) return set_error(THESIA_ERR_INVALID_ARG, "null pointer");
+    for (size_t k = 0; k < n_groups; ++k) {
+        if (ns[k] && (!d_specs[k] || !row0s[k])) return set_error(THESIA_ERR_INVALID_ARG, "null pointer");
+        tot += ns[k];
+    }
+    if (tot && (!up_ratio || !nwidth || !d_rgb || !rgb_off)) return set_error(THESIA_ERR_INVALID_ARG, "null pointer");
+    if (!(render_path() == 0 || render_path() >= 3))
+        return set_error(THESIA_ERR_UNSUPPORTED, "render_rgb_multi_dev: the fused render paths (0, 3, 4) only");
+    return render_rgb_fused(n_groups, d_specs, row0s, bins, ns, up_ratio, nwidth, nheight, 0.0f, 0.0f,
+                            d_rgb, rgb_off, default_stream(), d_range);
+    GUARD_END
+}
+
 int thesia_inv_real_fft_device(const float* d_in, size_t n_frames, size_t length, float* d_out) {
     GUARD_BEGIN
     if (n_frames && (!d_in || !d_out)) return set_error(THESIA_ERR_INVALID_ARG, "null device pointer");

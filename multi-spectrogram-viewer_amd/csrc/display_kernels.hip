@@ -692,6 +692,44 @@ __global__ void __launch_bounds__(256) resize_h_rgb_batch_kernel(uint32_t nh, co
     }
 }
 
+// thesia_ranges_global: one block; each thread folds a stride of the tracks' slots (NaN tracks
+// skipped: ndarray-stats' max/min error -> unwrap_or, lib.rs:198-199), a shared-memory tree
+// folds the threads, thread 0 applies lib.rs:208-209 in the order thesia.shard.global_db_range
+// does (Python's min / max argument order, the difference in double, the result rounded to f32)
+__global__ void __launch_bounds__(256) range_global_kernel(const int* trk, uint32_t n, double db_range,
+                                                           float* out) {
+    __shared__ float smx[256], smn[256];
+    float mx = -INFINITY, mn = INFINITY;
+    for (uint32_t i = threadIdx.x; i < n; i += 256) {
+        if (trk[3 * i + 2]) continue;
+        mx = fmaxf(mx, range_unord(trk[3 * i]));
+        mn = fminf(mn, range_unord(trk[3 * i + 1]));
+    }
+    smx[threadIdx.x] = mx;
+    smn[threadIdx.x] = mn;
+    __syncthreads();
+    for (int w = 128; w > 0; w >>= 1) {
+        if ((int)threadIdx.x < w) {
+            smx[threadIdx.x] = fmaxf(smx[threadIdx.x], smx[threadIdx.x + w]);
+            smn[threadIdx.x] = fminf(smn[threadIdx.x], smn[threadIdx.x + w]);
+        }
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) {
+        const float gx = smx[0], gn = smn[0];
+        const float gmax = 0.0f < gx ? 0.0f : gx;               // min(mx, 0.0)
+        const double t = (double)gmax - db_range;
+        const double m = t > (double)gn ? t : (double)gn;         // max(mn, gmax - db_range)
+        out[0] = gmax;
+        out[1] = (float)m;
+    }
+}
+
+int launch_range_global(const int* trk_range, uint32_t n, double db_range, float* out, hipStream_t s) {
+    hipLaunchKernelGGL(range_global_kernel, dim3(1), dim3(256), 0, s, trk_range, n, db_range, out);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
 int launch_render_batch(const float* spec, uint32_t bins, float max, float min,
                         const RenderDesc* d_desc, uint32_t n, uint32_t T_max, uint32_t H_max,
                         uint32_t nw_max, uint32_t nh, int h_taps, int h_span, float* grey,
@@ -742,6 +780,10 @@ __global__ void __launch_bounds__(256) grey_vert_kernel(const float* spec, uint3
                                                         float* tmp, int tile_cap, int kv, uint32_t band) {
     extern __shared__ __attribute__((aligned(16))) float vsm[];
     const RenderDesc r = d[blockIdx.z];
+    if (r.grange) {  // the device-side global range (RenderDesc::grange)
+        max = r.grange[0];
+        min = r.grange[1];
+    }
     const uint32_t x0 = blockIdx.x * 64, ob = blockIdx.y * band;
     const uint32_t oy1 = ob + band < nh ? ob + band : nh;
     const uint32_t oy0 = ob > r.oz ? ob : r.oz;  // rows below oz: +0, never formed (RenderDesc)
@@ -919,6 +961,10 @@ __global__ void __launch_bounds__(256) grey_vert_wide_kernel(const float* spec, 
     constexpr int TS = FW + 4;    // tile row stride (16-byte aligned rows)
     extern __shared__ __attribute__((aligned(16))) float vsm[];
     const RenderDesc r = d[blockIdx.z];
+    if (r.grange) {  // the device-side global range (RenderDesc::grange)
+        max = r.grange[0];
+        min = r.grange[1];
+    }
     const uint32_t x0 = blockIdx.x * FW, ob = blockIdx.y * band;
     const uint32_t oy1 = ob + band < nh ? ob + band : nh;
     const uint32_t oy0 = ob > r.oz ? ob : r.oz;  // rows below oz: +0, never formed (RenderDesc)

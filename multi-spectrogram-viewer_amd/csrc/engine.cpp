@@ -1569,7 +1569,7 @@ int plan_fused_group(const float* d_spec, const uint64_t* row0, size_t bins, siz
 int render_rgb_fused(size_t n_groups, const float* const* d_specs, const uint64_t* const* row0s,
                      const size_t* bins, const size_t* ns, const float* up_ratio,
                      const uint32_t* nwidth, uint32_t nheight, float max, float min, uint8_t* d_rgb,
-                     const uint64_t* rgb_off, hipStream_t s) {
+                     const uint64_t* rgb_off, hipStream_t s, const float* d_grange) {
     if (nheight == 0) return THESIA_OK;
     int rc = 0;
     const uint8_t* cmap_ptr = colormap_device(&rc);
@@ -1594,6 +1594,7 @@ int render_rgb_fused(size_t n_groups, const float* const* d_specs, const uint64_
     put(&n_groups, sizeof n_groups);
     put(&nheight, sizeof nheight);
     put(&d_rgb, sizeof d_rgb);
+    put(&d_grange, sizeof d_grange);
     for (size_t k = 0; k < n_groups; ++k) {
         put(&d_specs[k], sizeof(void*));
         put(&bins[k], sizeof(size_t));
@@ -1669,6 +1670,7 @@ int render_rgb_fused(size_t n_groups, const float* const* d_specs, const uint64_
         // once per allocation, so every float a horizontal pass may stage is finite
         if (ws.tmp.p != tmp_before) THESIA_HIP(hipMemsetAsync(ws.tmp.p, 0, ws.tmp.bytes, s));
         if (!desc.empty())
+            for (RenderDesc& r : desc) r.grange = d_grange;  // (part of the cache key)
             THESIA_HIP(copy_ordered(ws.desc.p, desc.data(), desc.size() * sizeof(RenderDesc), hipMemcpyHostToDevice));
         ws.groups = std::move(groups);
         ws.key = std::move(key);

@@ -169,7 +169,7 @@ int minmax_segments_multi(size_t n_groups, const float* const* d_x, const uint64
 int render_rgb_fused(size_t n_groups, const float* const* d_specs, const uint64_t* const* row0s,
                      const size_t* bins, const size_t* ns, const float* up_ratio,
                      const uint32_t* nwidth, uint32_t nheight, float max, float min, uint8_t* d_rgb,
-                     const uint64_t* rgb_off, hipStream_t s);
+                     const uint64_t* rgb_off, hipStream_t s, const float* d_grange = nullptr);
 int inv_real_fft_device(const float* d_in, size_t n_frames, size_t length, float* d_out, hipStream_t s);
 int render_rgb_batch_device(const float* d_spec, const uint64_t* row0, size_t bins, size_t n,
                             const float* up_ratio, const uint32_t* nwidth, uint32_t nheight,

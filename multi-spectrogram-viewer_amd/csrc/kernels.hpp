@@ -188,7 +188,15 @@ struct RenderDesc {
     // 8s + u (+0 outside its support)
     const int32_t* hst;
     const float* hsw;
+    // the display's (max, min) dB on the device (thesia_ranges_global: the global range reduced
+    // there, no host round trip), read by the grey stages in place of their max / min
+    // arguments; null = the arguments
+    const float* grange;
 };
+// the global (max, min) dB of n tracks' THESIA_BATCH_OPT_RANGE slots (lib.rs:194-209: NaN tracks
+// skipped, max = min(max, 0), min = max(min, max - db_range), as thesia.shard.global_db_range) ->
+// out[0], out[1] on the device; one block
+int launch_range_global(const int* trk_range, uint32_t n, double db_range, float* out, hipStream_t s);
 int launch_render_batch(const float* spec, uint32_t bins, float max, float min,
                         const RenderDesc* d_desc, uint32_t n, uint32_t T_max, uint32_t H_max,
                         uint32_t nw_max, uint32_t nh, int h_taps, int h_span, float* grey,

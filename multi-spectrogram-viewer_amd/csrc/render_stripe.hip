@@ -63,6 +63,8 @@ __global__ void __launch_bounds__(64 * WV) render_stripe_kernel(StripeLaunch L) 
     constexpr int TS = FC + 4;   // tile row stride (floats): 16-byte rows for the b128 reads
     constexpr int SPC = FC / 8;  // steps per chunk
     const RenderDesc r = L.desc[blockIdx.z];
+    // the grey values' (max, min): the device-side global range where the call has one
+    const float gmax = r.grange ? r.grange[0] : L.max, gmin = r.grange ? r.grange[1] : L.min;
     const uint32_t nw = r.nw;
     const uint32_t c0 = blockIdx.x * L.strip;
     if (c0 >= nw) return;  // block-uniform
@@ -238,7 +240,7 @@ __global__ void __launch_bounds__(64 * WV) render_stripe_kernel(StripeLaunch L) 
                 fi = (int)f;
                 bi = (int)(e - f * (uint32_t)nb);
             }
-            t[(q0 - bi) * TS + fi] = grey_of(pf[j], L.max, L.min);
+            t[(q0 - bi) * TS + fi] = grey_of(pf[j], gmax, gmin);
         }
     };
 

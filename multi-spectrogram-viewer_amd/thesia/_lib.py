@@ -107,6 +107,10 @@ _SIGS = {
     "thesia_render_rgb_multi": (_i, [_sz, C.POINTER(C.c_void_p), C.POINTER(_u64p), C.POINTER(_sz),
                                      C.POINTER(_sz), _fp, C.POINTER(C.c_uint32), _u32, _f, _f, C.c_void_p,
                                      _u64p]),
+    "thesia_ranges_global": (_i, [C.c_void_p, _sz, _f, C.c_void_p]),
+    "thesia_render_rgb_multi_dev": (_i, [_sz, C.POINTER(C.c_void_p), C.POINTER(_u64p), C.POINTER(_sz),
+                                         C.POINTER(_sz), _fp, C.POINTER(C.c_uint32), _u32, C.c_void_p,
+                                         C.c_void_p, _u64p]),
     "thesia_mt_get_wav": (_i, [_vp, _u64, _fp, _sz, C.POINTER(_sz)]),
     "thesia_inv_real_fft": (_i, [_fp, _sz, _sz, _fp]),
     "thesia_inv_real_fft_device": (_i, [C.c_void_p, _sz, _sz, C.c_void_p]),

@@ -245,8 +245,20 @@ def set_batches_policy(policy: int) -> None:
 
 
 def set_render_path(path: int) -> None:
-    """0: batched display launches (default); 1: per-track launches (cross-check)."""
+    """thesia_set_render_path: 0 the fused display with the single-pass kernel where it pays
+    (default); 1 per-track launches; 2 three-stage launches; 3 two kernels for every group; 4 the
+    single-pass kernel wherever its instances cover the geometry (all byte-identical)."""
     check(lib.thesia_set_render_path(path))
+    global _RENDER_PATH
+    _RENDER_PATH = int(path)
+
+
+_RENDER_PATH = 0  # the library's default (thesia_set_render_path)
+
+
+def render_path() -> int:
+    """The render path last set through set_render_path (the library's default 0 otherwise)."""
+    return _RENDER_PATH
 
 
 def synth_pcm_device(buf: DeviceBuffer, fmt: int, channels: int, n_tracks: int, n_samples: int,

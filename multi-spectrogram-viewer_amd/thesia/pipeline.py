@@ -18,6 +18,7 @@ up_ratio = max_sr / sr (lib.rs:231-248), nwidth = (px_per_sec * n / sr) as u32 (
 from __future__ import annotations
 
 import ctypes as C
+import os
 from collections import OrderedDict
 from dataclasses import dataclass
 from typing import List, Optional, Sequence
@@ -123,6 +124,7 @@ class RenderPipeline:
         # per-track dB ranges left by the spectrogram launches themselves (Batch range option,
         # folded into the streaming kernel's row epilogue): 3 int32 per track, call order
         self._d_range = engine.DeviceBuffer(12 * max(len(self._order), 1))
+        self._d_grange = engine.DeviceBuffer(8)  # the device-side global (max, min), render()
         t0 = 0
         for _, _, _, b in self.groups:
             b.set_option(engine.OPT_RANGE, self._d_range.ptr.value + 12 * t0)
@@ -134,6 +136,14 @@ class RenderPipeline:
         """One kernel launch per geometry group, the launches overlapped on the library's
         streams (thesia_batches_run; asynchronous, ordered before later library calls)."""
         engine.run_batches([b for _, _, _, b in self.groups])
+
+    def _up_for(self, max_sr):
+        up = self._up.get(max_sr)
+        if up is None:
+            up = np.array([shard.up_ratio(self.tracks[i].sr, max_sr, freq_scale_mel=False)
+                           for i in self._order.tolist()], np.float32)
+            self._up[max_sr] = up
+        return up
 
     def _spec_ptr(self, i):
         g, row0, T, bins = self.where[i]
@@ -155,18 +165,37 @@ class RenderPipeline:
             out[i] = (float(mx[k]), float(mn[k]))
         return out
 
-    def render(self, group=None, keep_db: bool = False, want_rgb: bool = True) -> List[Rendered]:
+    def _single_rank(self, group) -> bool:
+        try:
+            import torch.distributed as dist
+            return not (dist.is_available() and dist.is_initialized() and dist.get_world_size(group) > 1)
+        except ImportError:  # pragma: no cover - torch is in the image
+            return True
+
+    def render(self, group=None, keep_db: bool = False, want_rgb: bool = True) -> Optional[List[Rendered]]:
+        """The global-range exchange and the display of every track. want_rgb=False and
+        keep_db=False on one rank: the range is reduced on the device (thesia_ranges_global)
+        and the display reads it there (thesia_render_rgb_multi_dev), so nothing waits for the
+        spectrograms on the host; the images stay in HBM and None is returned (asynchronous).
+        Otherwise the ranges come back to the host (the multi-rank exchange, the per-track
+        results) and the rendered tracks are returned."""
+        # (THESIA_HOST_RANGE=1 in the environment keeps the host exchange: A/B)
+        if (not want_rgb and not keep_db and engine.render_path() in (0, 3, 4) and self._single_rank(group)
+                and os.environ.get("THESIA_HOST_RANGE") != "1"):
+            check(lib.thesia_ranges_global(self._d_range.ptr, len(self._order), self.db_range, self._d_grange.ptr))
+            up = self._up_for(self._max_sr)
+            check(lib.thesia_render_rgb_multi_dev(
+                self._n_disp, self._c_specs, self._c_row0, self._c_bins, self._c_ns,
+                up.ctypes.data_as(_fp), self._nw.ctypes.data_as(C.POINTER(C.c_uint32)), self.nheight,
+                self._d_grange.ptr, self._rgb.ptr, self._off.ctypes.data_as(_u64p)))
+            return None
         # (the range readback is ordered on the library stream after the spectrogram batches,
         # which thesia_batches_run joins back into it, and waits for it: no device-wide sync)
         mx, mn = self._range_arrays()
         lmx = float(mx.max()) if mx.size else -np.inf  # shard.local_range over numpy arrays
         lmn = float(mn.min()) if mn.size else np.inf
         gmax, gmin, max_sr = shard.global_db_range(lmx, lmn, self._max_sr, db_range=self.db_range, group=group)
-        up = self._up.get(max_sr)
-        if up is None:
-            up = np.array([shard.up_ratio(self.tracks[i].sr, max_sr, freq_scale_mel=False)
-                           for i in self._order.tolist()], np.float32)
-            self._up[max_sr] = up
+        up = self._up_for(max_sr)
         check(lib.thesia_render_rgb_multi(
             self._n_disp, self._c_specs, self._c_row0, self._c_bins, self._c_ns,
             up.ctypes.data_as(_fp), self._nw.ctypes.data_as(C.POINTER(C.c_uint32)), self.nheight,

@@ -239,3 +239,29 @@ def test_render_rejects_overlapping_rgb_ranges():
         assert "overlap" in lib.thesia_last_error().decode()
     finally:
         p.close()
+
+
+@pytest.mark.parametrize("path", [0, 3, 4])
+def test_device_range_render_equals_host_exchange(path):
+    """render(want_rgb=False) on one rank reduces the global range on the device
+    (thesia_ranges_global) and the display reads it there (thesia_render_rgb_multi_dev): the
+    device range equals the host exchange's (shard.global_db_range, lib.rs:194-209) and the RGB
+    bytes equal the host-exchange render's, for every render path that takes it."""
+    engine.set_render_path(path)
+    try:
+        tracks = pipeline.c5_tracks(24, seconds=1.2)
+        p = pipeline.RenderPipeline(tracks, px_per_sec=100.0, nheight=300)
+        p.run_spectrograms()
+        assert p.render(want_rgb=False) is None
+        engine.synchronize()
+        dev = p._rgb.read(np.uint8, p._rgb_total).copy()
+        g2 = p._d_grange.read(np.float32, 2).copy()
+        out = p.render(want_rgb=True)
+        host = p._rgb.read(np.uint8, p._rgb_total)
+        gmax, gmin, _ = shard.global_db_range(max(r.spec_max for r in out), min(r.spec_min for r in out),
+                                              max(t.sr for t in tracks))
+        assert (float(g2[0]), float(g2[1])) == (gmax, gmin)
+        assert dev.tobytes() == host.tobytes()
+        p.close()
+    finally:
+        engine.set_render_path(0)
