@@ -1217,8 +1217,10 @@ __global__ void __launch_bounds__(256) resize_h_dma_kernel(uint32_t nh, const Re
 static int launch_resize_h_dma(uint32_t nh, const RenderDesc* d_desc, uint32_t n, uint32_t nw_max, int h_taps,
                                int h_span, const float* tmp, const uint8_t* cmap, uint8_t* rgb, dim3 g3,
                                hipStream_t s) {
-    // 8 taps: the groups that upsample along time (Lanczos3's 6-7 taps per column)
-    const int kt = h_taps <= 8 ? 8 : h_taps <= 16 ? 16 : h_taps <= 32 ? 32 : h_taps <= 48 ? 48 : 0;
+    // 8 taps: the groups that upsample along time (Lanczos3's 6-7 taps per column); 10 / 12: the
+    // groups that downsample 1.2-2x (9-12 taps)
+    const int kt = h_taps <= 8 ? 8 : h_taps <= 10 ? 10 : h_taps <= 12 ? 12 : h_taps <= 16 ? 16
+                 : h_taps <= 32 ? 32 : h_taps <= 48 ? 48 : 0;
     if (!kt) return -2;
     const int need = h_span + 4 + kt;
     const int K = need <= 1024 ? 1 : need <= 2048 ? 2 : need <= 4096 ? 4 : 0;
@@ -1231,6 +1233,8 @@ static int launch_resize_h_dma(uint32_t nh, const RenderDesc* d_desc, uint32_t n
 #define THESIA_HDMA(KT_, K_) \
     if (kt == KT_ && K == K_) kern = reinterpret_cast<const void*>(resize_h_dma_kernel<KT_, K_, NB>);
     THESIA_HDMA(8, 1) THESIA_HDMA(8, 2) THESIA_HDMA(8, 4)
+    THESIA_HDMA(10, 1) THESIA_HDMA(10, 2) THESIA_HDMA(10, 4)
+    THESIA_HDMA(12, 1) THESIA_HDMA(12, 2) THESIA_HDMA(12, 4)
     THESIA_HDMA(16, 1) THESIA_HDMA(16, 2) THESIA_HDMA(16, 4)
     THESIA_HDMA(32, 1) THESIA_HDMA(32, 2) THESIA_HDMA(32, 4)
     THESIA_HDMA(48, 1) THESIA_HDMA(48, 2) THESIA_HDMA(48, 4)

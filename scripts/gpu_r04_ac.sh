@@ -1,5 +1,5 @@
 #!/bin/bash
-# Round 4: stripe staging with kept indices + buffer loads -- render parity, per group alone, C5.
+# Round 4: render parity, per group alone (path 0), C5 line twice.
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 R=$PWD
