@@ -779,6 +779,7 @@ int batch_create(Plan* plan, const thesia_batch_desc& d, Batch** out) {
         b->apply_mel_path();
     }
     b->k5_ok = k5_geo && stft5_lds_bytes(L) <= 163840;
+    b->k5_view = view5;
     b->kernel = b->auto_kernel();
     if (hipEventCreate(&b->ev0) != hipSuccess || hipEventCreate(&b->ev1) != hipSuccess) {
         delete b;

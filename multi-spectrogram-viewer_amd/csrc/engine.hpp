@@ -118,10 +118,17 @@ struct Batch {
     // complex rows, 9.0 vs 6.98 ms, and stft3 folds the per-track range into its row epilogue;
     // DESIGN.md §6), stft3 for the other streaming geometries, then the 4-waves/SIMD kernel for
     // its sizes, else the general one
+    // at the viewer geometry (k5_view) stft5 pays only on large batches: its per-block setup
+    // (the packed mel stream, the rotation tables) against stft3's, measured at 48 kHz mel-128
+    // (profiles/r04_viewer/batch_size_ab.txt): 3.0e6 frames 4.48 vs 4.76 ms, 3.0e5 0.576 vs
+    // 0.570, 2.6e4 0.102 vs 0.077
+    static constexpr uint64_t kView5MinFrames = 400000;
+    bool k5_view = false;
     int auto_kernel() const {
         const bool mel = launch.out_kind == OUT_MEL || launch.out_kind == OUT_MEL_AMP_DB;
         const bool lin = !mel && launch.out_kind != OUT_COMPLEX && !range;
-        return k5_ok && (mel || lin) ? 5 : k3_ok ? 3 : plan->use_v2 ? 2 : 1;
+        const bool k5 = k5_ok && (mel || lin) && (!k5_view || total_frames >= kView5MinFrames);
+        return k5 ? 5 : k3_ok ? 3 : plan->use_v2 ? 2 : 1;
     }
     bool kernel_forced = false;  // THESIA_BATCH_OPT_KERNEL set a kernel (else auto_kernel follows)
     // mel projection of stft5 (THESIA_BATCH_OPT_MEL_PATH): 0 automatic, 1 the rounds' chunk

@@ -161,8 +161,8 @@ def test_kernel_choice_and_unsupported_force():
     din = engine.DeviceBuffer.from_host(x[:, 0].copy())
     dout = engine.DeviceBuffer(engine.Batch.frames_for(plan, [4096]) * plan.row_bins * 4)
     b = engine.Batch(plan, din, [0], [4096], dout)
-    assert b.kernel == 5  # stft5's viewer column rule (HQ 7) for the mel and linear kinds
-    b.set_option(engine.OPT_KERNEL, 3)
+    assert b.kernel == 3  # a small batch: stft3 (stft5's viewer rule from 400 000 frames on)
+    b.set_option(engine.OPT_KERNEL, 5)  # stft5's viewer column rule (HQ 7) runs it when forced
     import thesia
     plan = engine.Plan(2048, 1920, 480, engine.OUT_COMPLEX)  # complex rows: stft3 only
     dout = engine.DeviceBuffer(engine.Batch.frames_for(plan, [4096]) * plan.row_bins * 8)

@@ -93,10 +93,11 @@ def test_viewer_geometry_complex_streams(n_fft, win, hop, channels, fmt, gap):
 _KINDS = [engine.OUT_MAG, engine.OUT_POWER, engine.OUT_AMP_DB, engine.OUT_POWER_DB]
 
 
-def _auto(n_fft, hop):
+def _auto(n_fft, hop, frames=0):
     """The automatic kernel for the mel / linear kinds: stft5 (its viewer column rule,
-    stft5_kernels.hip HQ 7) at the 48 kHz geometry, stft3 at the others."""
-    return 5 if (n_fft, hop) == (2048, 480) else 3
+    stft5_kernels.hip HQ 7) at the 48 kHz geometry for batches of >= 400 000 frames
+    (Batch::kView5MinFrames), stft3 otherwise -- these tests' batches are small."""
+    return 5 if (n_fft, hop) == (2048, 480) and frames >= 400000 else 3
 
 
 def _check_kind(kind, g, ref, fb=None):
