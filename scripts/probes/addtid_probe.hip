@@ -1,6 +1,6 @@
 // Where does ds_write_addtid_b32 put lane L's dword for a given M0 and offset? (round-4 probe; its
 // output, profiles/r04_close/addtid_probe.txt, did not follow M0 + offset + 4 lane: not used)
-// waves; wave w writes (w << 16 | lane) with M0 = m0[w], offset = OFF; the whole LDS (160 KiB)
+// One block of two waves; wave w writes (w << 16 | lane) with M0 = m0[w], offset = OFF; the whole LDS (160 KiB)
 // is then copied out and the host prints the dword index of a few lanes.
 #include <hip/hip_runtime.h>
 #include <cstdio>
