@@ -1433,6 +1433,9 @@ void plan_stripe(const std::vector<StripeTrack>& trk, uint32_t bins, uint32_t nh
     if (fc * nbmax > 64 * npf || lds() > (waves == 8 ? 81920 : 54613)) fc = 8;
     if (waves == 8 && lds() > 81920) waves = 4;
     if (fc * nbmax > 64 * npf || lds() > 163840) return;
+    // the kept element places (render_stripe.hip pk): a chunk's row offsets and the tile's float
+    // indices below 2^16
+    if (fc * (int)bins >= 65536 || tile * (fc + 4) >= 65536) return;
     // the instances compiled (render_stripe.hip launch_render_stripe)
     if (kv > 8) npf = 16;
     const int slots_run = kv > 8 ? 16 : slots;

@@ -193,16 +193,43 @@ __global__ void __launch_bounds__(64 * WV) render_stripe_kernel(StripeLaunch L) 
     // past T to frame T - 1 (duplicate loads / identical stores; frames past T only ever meet
     // zero horizontal weights, so any finite value will do): no per-element branches
     float pf[NPF];
-    // each staged element's (frame, bin) kept from issue() to commit() as fi | bi << 8 where the
-    // registers fit under 128 VGPRs (4 waves / SIMD), else formed again in commit()
+    // where the registers fit under 128 VGPRs (4 waves / SIMD), each staged element's place is
+    // formed once per wave and kept for every chunk: pk[j] = its offset in the chunk's frame rows
+    // (fi bins + bi < 2^16) | its float index in the wave's tile (< 2^16) << 16; the chunk's loads
+    // take a uniform base, and frames past T read +0 through the buffer's range check (frames
+    // past T only ever meet zero horizontal weights, and grey_of(+0) is finite). Otherwise the
+    // (frame, bin) of each element is formed again per chunk, frames clamped to T - 1.
     constexpr bool kKeep = NPF == 8 || (KV == 8 && A <= 12);
     uint32_t pk[kKeep ? NPF : 1];
     const uint32_t emax = (uint32_t)(tot > 0 ? tot - 1 : 0);
+    const int q0 = H - 1 - b_lo - ya;  // tile row of staged bin bi: q0 - bi
     // the track's dB rows as a buffer resource: 32-bit byte offsets (a track's rows < 2^30
     // floats, host), one buffer_load per element
-    const __amdgpu_buffer_rsrc_t rsc = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(sp), (short)0, -1, 0x00020000);
+    const __amdgpu_buffer_rsrc_t rsc = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<float*>(sp), (short)0, kKeep ? (int)(T * (uint32_t)bins * 4u) : -1, 0x00020000);
+    if constexpr (kKeep) {
+#pragma unroll
+        for (int j = 0; j < NPF; ++j) {
+            if (64 * j >= tot) break;  // uniform
+            uint32_t e = (uint32_t)(lane + 64 * j);
+            e = e < emax ? e : emax;
+            const uint32_t fi = nb > 1 ? __umulhi(e, mrec) : e;
+            const uint32_t bi = e - fi * (uint32_t)nb;
+            pk[j] = (fi * (uint32_t)bins + bi) | ((uint32_t)((q0 - (int)bi) * TS + (int)fi) << 16);
+        }
+    }
     auto issue = [&](int k) {  // chunk k's dB values -> registers
         const uint32_t fb = (uint32_t)(F0 + k * FC);
+        if constexpr (kKeep) {
+            const uint32_t base = (fb * (uint32_t)bins + (uint32_t)b_lo) * 4u;  // uniform
+#pragma unroll
+            for (int j = 0; j < NPF; ++j) {
+                if (64 * j >= tot) break;  // uniform
+                pf[j] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(
+                    rsc, (pk[j] & 0xffffu) * 4u + base, 0, 0));
+            }
+            return;
+        }
         // opaque per call: the element indices are formed per chunk, not hoisted out of the
         // frame loop into NPF x 3 registers held across it
         int li = lane;
@@ -214,26 +241,29 @@ __global__ void __launch_bounds__(64 * WV) render_stripe_kernel(StripeLaunch L) 
             e = e < emax ? e : emax;
             const uint32_t fi = nb > 1 ? __umulhi(e, mrec) : e;
             const uint32_t bi = e - fi * (uint32_t)nb;
-            if constexpr (kKeep) pk[j] = fi | (bi << 8);  // fi < FC <= 16, bi < nb <= tile rows
             uint32_t f = fb + fi;
             f = f < T ? f : T - 1;
             pf[j] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(
                 rsc, (f * (uint32_t)bins + (uint32_t)b_lo + bi) * 4u, 0, 0));
         }
     };
-    const int q0 = H - 1 - b_lo - ya;  // tile row of staged bin bi: q0 - bi
     auto commit = [&](int) {  // registers -> grey values in the tile (its previous chunk read)
         float* t = tile;
+        if constexpr (kKeep) {
+#pragma unroll
+            for (int j = 0; j < NPF; ++j) {
+                if (64 * j >= tot) break;  // uniform
+                t[pk[j] >> 16] = grey_of(pf[j], gmax, gmin);
+            }
+            return;
+        }
         int lc = lane;  // (recomputing: opaque, as in issue())
         asm volatile("" : "+v"(lc));
 #pragma unroll
         for (int j = 0; j < NPF; ++j) {
             if (64 * j >= tot) break;  // uniform
             int fi, bi;
-            if constexpr (kKeep) {
-                fi = (int)(pk[j] & 255u);
-                bi = (int)(pk[j] >> 8);
-            } else {
+            {
                 uint32_t e = (uint32_t)(lc + 64 * j);
                 e = e < emax ? e : emax;
                 const uint32_t f = nb > 1 ? __umulhi(e, mrec) : e;
