@@ -91,4 +91,36 @@ __device__ __forceinline__ float grey_of(float db, float max, float min) {  // g
     return fminf(v, 1.0f);
 }
 
+// grey_of without the f32 division sequence (11 VALU with a v_rcp): the f32 difference a =
+// db - min times the f64 reciprocal of the f32 span b = max - min, rounded once to f32. The
+// product is within 2^-52 (relative) of a / b, and for a normal quotient that is closer than any
+// f32 rounding midpoint can be to a quotient of two f32 (a midpoint there has 25 significant bits,
+// so a - b m is a nonzero multiple of b m's 49-bit grid: > 2^-49 relative), so the result is
+// RN(a / b) bit for bit. Below the normal range exact ties exist (midpoints with few significant
+// bits): those quotients, zero and non-finite ones are divided in f32 (tests/test_grey_map.py).
+struct GreyMap {
+    float min, span;
+    double rspan;
+    __host__ __device__ GreyMap(float max, float mn) : min(mn), span(max - mn), rspan(1.0 / (double)(max - mn)) {}
+    __host__ __device__ __forceinline__ float operator()(float db) const {
+        const float a = db - min;
+        float v = (float)((double)a * rspan);
+#ifdef __HIP_DEVICE_COMPILE__
+        const bool normal = __builtin_amdgcn_classf(v, 0x108);  // +-normal: one v_cmp_class
+#else
+        const bool normal = fabsf(v) >= 1.17549435e-38f && fabsf(v) <= 3.40282347e+38f;
+#endif
+        if (!normal) {
+            // a real branch (rarely taken), not a division formed for every element and selected
+            float t = a;
+#ifdef __HIP_DEVICE_COMPILE__
+            asm volatile("" : "+v"(t));
+#endif
+            v = t / span;
+        }
+        v = fmaxf(v, 0.0f);
+        return fminf(v, 1.0f);
+    }
+};
+
 }  // namespace thesia

@@ -784,6 +784,7 @@ __global__ void __launch_bounds__(256) grey_vert_kernel(const float* spec, uint3
         max = r.grange[0];
         min = r.grange[1];
     }
+    const GreyMap gm(max, min);
     const uint32_t x0 = blockIdx.x * 64, ob = blockIdx.y * band;
     const uint32_t oy1 = ob + band < nh ? ob + band : nh;
     const uint32_t oy0 = ob > r.oz ? ob : r.oz;  // rows below oz: +0, never formed (RenderDesc)
@@ -844,8 +845,8 @@ __global__ void __launch_bounds__(256) grey_vert_kernel(const float* spec, uint3
                 const uint32_t f = fk[i] & 255u;
                 const int32_t k = (int32_t)(fk[i] >> 8);
                 const int32_t y = ya + k;
-                // formed for every element (pinned: a select, not a branch around the division)
-                float g = grey_of(v[i], max, min);
+                // formed for every element (pinned: a select, not a branch around the grey value)
+                float g = gm(v[i]);
                 asm volatile("" : "+v"(g));
                 tile[k * TS + (int32_t)f] = (y >= top && y < H) ? g : 0.0f;
             }
@@ -924,7 +925,7 @@ __global__ void __launch_bounds__(256) grey_vert_kernel(const float* spec, uint3
         float t = 0.0f;
         for (int32_t i = 0; i < n; ++i) {
             const int32_t y = l + i;
-            t += (y >= top ? grey_of(srow[H - 1 - y], max, min) : 0.0f) * wr[i];
+            t += (y >= top ? gm(srow[H - 1 - y]) : 0.0f) * wr[i];
         }
         out[(uint64_t)oy * r.ts] = t;
     }
@@ -965,6 +966,7 @@ __global__ void __launch_bounds__(256) grey_vert_wide_kernel(const float* spec, 
         max = r.grange[0];
         min = r.grange[1];
     }
+    const GreyMap gm(max, min);
     const uint32_t x0 = blockIdx.x * FW, ob = blockIdx.y * band;
     const uint32_t oy1 = ob + band < nh ? ob + band : nh;
     const uint32_t oy0 = ob > r.oz ? ob : r.oz;  // rows below oz: +0, never formed (RenderDesc)
@@ -1015,7 +1017,7 @@ __global__ void __launch_bounds__(256) grey_vert_wide_kernel(const float* spec, 
                 int32_t k;
                 split(e, f, k);
                 const int32_t y = ya + k;
-                if ((int)e < total) tile[k * TS + f] = (y >= top && y < H) ? grey_of(v[i], max, min) : 0.0f;
+                if ((int)e < total) tile[k * TS + f] = (y >= top && y < H) ? gm(v[i]) : 0.0f;
             }
         }
         for (uint32_t e = tid; e < nb * (uint32_t)kv; e += 256) {

@@ -65,6 +65,7 @@ __global__ void __launch_bounds__(64 * WV) render_stripe_kernel(StripeLaunch L) 
     const RenderDesc r = L.desc[blockIdx.z];
     // the grey values' (max, min): the device-side global range where the call has one
     const float gmax = r.grange ? r.grange[0] : L.max, gmin = r.grange ? r.grange[1] : L.min;
+    const GreyMap gm(gmax, gmin);
     const uint32_t nw = r.nw;
     const uint32_t c0 = blockIdx.x * L.strip;
     if (c0 >= nw) return;  // block-uniform
@@ -197,7 +198,7 @@ __global__ void __launch_bounds__(64 * WV) render_stripe_kernel(StripeLaunch L) 
     // formed once per wave and kept for every chunk: pk[j] = its offset in the chunk's frame rows
     // (fi bins + bi < 2^16) | its float index in the wave's tile (< 2^16) << 16; the chunk's loads
     // take a uniform base, and frames past T read +0 through the buffer's range check (frames
-    // past T only ever meet zero horizontal weights, and grey_of(+0) is finite). Otherwise the
+    // past T only ever meet zero horizontal weights, and the grey value of +0 is finite). Otherwise the
     // (frame, bin) of each element is formed again per chunk, frames clamped to T - 1.
     constexpr bool kKeep = NPF == 8 || (KV == 8 && A <= 12);
     uint32_t pk[kKeep ? NPF : 1];
@@ -253,7 +254,7 @@ __global__ void __launch_bounds__(64 * WV) render_stripe_kernel(StripeLaunch L) 
 #pragma unroll
             for (int j = 0; j < NPF; ++j) {
                 if (64 * j >= tot) break;  // uniform
-                t[pk[j] >> 16] = grey_of(pf[j], gmax, gmin);
+                t[pk[j] >> 16] = gm(pf[j]);
             }
             return;
         }
@@ -270,7 +271,7 @@ __global__ void __launch_bounds__(64 * WV) render_stripe_kernel(StripeLaunch L) 
                 fi = (int)f;
                 bi = (int)(e - f * (uint32_t)nb);
             }
-            t[(q0 - bi) * TS + fi] = grey_of(pf[j], gmax, gmin);
+            t[(q0 - bi) * TS + fi] = gm(pf[j]);
         }
     };
 
