@@ -808,7 +808,50 @@ __global__ void __launch_bounds__(256) grey_vert_kernel(const float* spec, uint3
     const uint32_t x = x0 + lane;
     const int32_t H = (int32_t)r.H, top = (int32_t)r.H - (int32_t)bins;
     const float* sp = spec + r.spec_off;
-    if (staged) {
+    if (staged && rows <= 128) {
+        // thread -> (tile row k = tid mod rows, frame phase p = tid / rows): P = 256 / rows
+        // phases walk the block's frames p, p + P, ...; consecutive threads read consecutive
+        // (descending) bins of one frame (coalesced). A thread's bin, its tile row and whether
+        // its row is inside the track's band [top, H) are fixed, so an element costs its load
+        // (per-thread byte offset + a uniform per-step one), its grey value and an LDS store with
+        // an immediate offset; rows outside the band read a clamped bin and store +0 (the image's
+        // zero fill; padded taps below the image). THESIA_VDEPTH loads in flight per thread.
+        constexpr int D = THESIA_VDEPTH;
+        const int P = __builtin_amdgcn_readfirstlane(256 / rows);  // >= 2 (rows <= 128), uniform
+        const int k = tid % rows, p = tid / rows;
+        const uint32_t nf = r.T - x0 < 64u ? r.T - x0 : 64u;  // the block's frames (uniform)
+        if (p < P) {
+            const int32_t y = ya + k;
+            const bool inb = y >= top && y < H;
+            int32_t b = H - 1 - y;
+            b = b < 0 ? 0 : b < (int32_t)bins ? b : (int32_t)bins - 1;
+            const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+                const_cast<float*>(sp + (uint64_t)x0 * bins), (short)0, (int)(nf * bins * 4u), 0x00020000);
+            const uint32_t vo = ((uint32_t)p * bins + (uint32_t)b) * 4u;  // this thread's first element
+            const uint32_t step = __builtin_amdgcn_readfirstlane((uint32_t)P * bins * 4u);  // per phase step
+            float* trow = tile + k * TS + p;
+            const int nit = (64 + P - 1) / P;  // phase steps covering 64 frames (uniform)
+            for (int i0 = 0; i0 < nit; i0 += D) {
+                float v[D];
+#pragma unroll
+                for (int i = 0; i < D; ++i)  // frames past the block's read +0 (range check)
+                    v[i] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rs, vo, (i0 + i) * step, 0));
+#pragma unroll
+                for (int i = 0; i < D; ++i) {
+                    const int f = p + P * (i0 + i);
+                    float g = gm(v[i]);
+                    asm volatile("" : "+v"(g));  // a select, not a branch around the grey value
+                    if (f < 64) trow[P * (i0 + i)] = inb ? g : 0.0f;
+                }
+            }
+        }
+        for (uint32_t e = tid; e < nb * (uint32_t)kv; e += 256) {
+            const uint32_t j = e / (uint32_t)kv, i = e - j * (uint32_t)kv;
+            const int32_t n = r.vc[oy0 + j];
+            wl[e] = (int32_t)i < n ? r.vw[r.vo[oy0 + j] + i] : 0.0f;
+        }
+        for (uint32_t j = tid; j < nb; j += 256) meta[j] = r.vl[oy0 + j] - ya;
+    } else if (staged) {
         // (frame, row) pairs flattened over the block's 256 threads (f = e / rows by a
         // multiply-high, exact for e < 2^14): consecutive threads read consecutive bins of one
         // frame (coalesced), a thread's THESIA_VDEPTH loads in flight together. Branch-free:
