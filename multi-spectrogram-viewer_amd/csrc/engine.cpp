@@ -1401,8 +1401,9 @@ void plan_stripe(const std::vector<StripeTrack>& trk, uint32_t bins, uint32_t nh
         amax = std::max(amax, t.ht->st_maxna);
         dword = dword && t.nw % 4 == 0 && t.rgb_off % 4 == 0;
     }
-    const int kv = kvmax <= 8 ? 8 : kvmax <= 12 ? 12 : kvmax <= 16 ? 16 : 0;
     const int slots = amax <= 8 ? 8 : amax <= 12 ? 12 : amax <= 16 ? 16 : 0;
+    // 7 taps (no padded tap for the upsampling rows' 6-7) where an instance has the step table
+    const int kv = kvmax <= 7 && slots <= 12 ? 7 : kvmax <= 8 ? 8 : kvmax <= 12 ? 12 : kvmax <= 16 ? 16 : 0;
     if (!kv || !slots) return;
     constexpr int kWaveRows = 64;  // render_stripe.hip: lane = row, a wave's rows stage their own tile
     const uint32_t strip = g.st_strip;

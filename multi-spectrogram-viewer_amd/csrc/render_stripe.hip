@@ -200,7 +200,7 @@ __global__ void __launch_bounds__(64 * WV) render_stripe_kernel(StripeLaunch L) 
     // take a uniform base, and frames past T read +0 through the buffer's range check (frames
     // past T only ever meet zero horizontal weights, and the grey value of +0 is finite). Otherwise the
     // (frame, bin) of each element is formed again per chunk, frames clamped to T - 1.
-    constexpr bool kKeep = NPF == 8 || (KV == 8 && A <= 12);
+    constexpr bool kKeep = NPF == 8 || (KV <= 8 && A <= 12);
     uint32_t pk[kKeep ? NPF : 1];
     const uint32_t emax = (uint32_t)(tot > 0 ? tot - 1 : 0);
     const int q0 = H - 1 - b_lo - ya;  // tile row of staged bin bi: q0 - bi
@@ -318,7 +318,7 @@ __global__ void __launch_bounds__(64 * WV) render_stripe_kernel(StripeLaunch L) 
             // vertical sums of the step's 8 frames (resize_v_px order), 4 frames at a time: one
             // ds_read_b128 per tap, a batch of taps' reads in flight
             float v[8];
-            constexpr int KB = KV % 8 == 0 ? 8 : 4;  // taps per batch of reads (divides KV)
+            constexpr int KB = KV % 8 == 0 ? 8 : KV % 4 == 0 ? 4 : KV;  // taps per batch of reads (divides KV)
             static_assert(KV % KB == 0, "tap batches");
 #pragma unroll
             for (int hf = 0; hf < 2; ++hf) {
@@ -412,13 +412,17 @@ int launch_render_stripe(const StripeLaunch& L, hipStream_t s) {
     if (L.n == 0 || L.nh == 0) return 0;
     if (L.n > 65535 || L.strip == 0 || (L.strip & 15) || (L.waves != 4 && L.waves != 8)) return -2;
     const void* kern = nullptr;
-    // the instances (host plan_stripe picks among them): KV 8 (the groups that upsample
-    // vertically) with 8 / 9 / 10 / 12 / 16 accumulators (9 and 10 on the 12-wide step table: the
-    // 48 kHz / 512 and 22.05 kHz / 256 C5 groups meet at most 9 columns per step); KV 12 / 16
-    // (downsampling) with 16
+    // the instances (host plan_stripe picks among them): KV 7 / 8 (the groups that upsample
+    // vertically: Lanczos3's 6-7 taps per row, 7 where no row has 8) with 8 / 9 / 10 / 12 (and for
+    // KV 8, 16) accumulators (9 and 10 on the 12-wide step table: the 48 kHz / 512 and 22.05 kHz /
+    // 256 C5 groups meet at most 9 columns per step); KV 12 / 16 (downsampling) with 16
 #define THESIA_STRIPE(KV_, A_, AW_, FC_, NPF_)                                                     \
     if (L.kv == KV_ && L.acc == A_ && L.slots == AW_ && L.fc == FC_ && L.npf == NPF_)             \
         kern = stripe_kernel<KV_, A_, AW_, FC_, NPF_>(L.waves);
+    THESIA_STRIPE(7, 8, 8, 16, 8) THESIA_STRIPE(7, 8, 8, 16, 16) THESIA_STRIPE(7, 8, 8, 8, 16)
+    THESIA_STRIPE(7, 9, 12, 16, 8) THESIA_STRIPE(7, 9, 12, 16, 16) THESIA_STRIPE(7, 9, 12, 8, 16)
+    THESIA_STRIPE(7, 10, 12, 16, 8) THESIA_STRIPE(7, 10, 12, 16, 16) THESIA_STRIPE(7, 10, 12, 8, 16)
+    THESIA_STRIPE(7, 12, 12, 16, 8) THESIA_STRIPE(7, 12, 12, 16, 16) THESIA_STRIPE(7, 12, 12, 8, 16)
     THESIA_STRIPE(8, 8, 8, 16, 8) THESIA_STRIPE(8, 8, 8, 16, 16) THESIA_STRIPE(8, 8, 8, 8, 16)
     THESIA_STRIPE(8, 9, 12, 16, 8) THESIA_STRIPE(8, 9, 12, 16, 16) THESIA_STRIPE(8, 9, 12, 8, 16)
     THESIA_STRIPE(8, 10, 12, 16, 8) THESIA_STRIPE(8, 10, 12, 16, 16) THESIA_STRIPE(8, 10, 12, 8, 16)
