@@ -173,6 +173,10 @@ def _ragged(px_per_sec, nheight):
         n = max(n, t.n_fft)
         tracks.append(pipeline.Track(t.pcm[:n].copy(), t.sr, t.n_fft))
     out = pipeline.render_tracks(tracks, px_per_sec=px_per_sec, nheight=nheight, keep_db=True)
+    _oracle_check(tracks, out, nheight)
+
+
+def _oracle_check(tracks, out, nheight):
     gmax, gmin, max_sr = shard.global_db_range(max(r.spec_max for r in out),
                                                min(r.spec_min for r in out),
                                                max(t.sr for t in tracks))
@@ -181,6 +185,28 @@ def _ragged(px_per_sec, nheight):
         grey = O.spec_to_grey(r.db, up, gmax, gmin)
         img, _ = O.grey_to_rgb(grey, r.nwidth, nheight)
         assert r.rgb.tobytes() == img.tobytes(), (t.sr, t.n_fft, t.pcm.shape)
+
+
+@pytest.mark.parametrize("path", [0, 3, 4])
+@pytest.mark.parametrize("mode", ["some_silent", "all_silent"])
+def test_render_silent_tracks(path, mode):
+    """Silent tracks in a display batch: their dB rows sit at the global minimum, so the grey
+    quotient (db - min) / (max - min) is +0 (the kernels' GreyMap takes its f32-division branch
+    there); with every track silent the span is 0 and every quotient 0 / 0 (NaN, grey +0 after
+    the clamps, as in display.rs). Bytes equal the oracle's on every render path."""
+    base = pipeline.c5_tracks(12, seconds=0.6)
+    tracks = []
+    for k, t in enumerate(base):
+        pcm = t.pcm.copy()
+        if mode == "all_silent" or k in (0, 5, 7):
+            pcm[:] = 0
+        tracks.append(pipeline.Track(pcm, t.sr, t.n_fft))
+    engine.set_render_path(path)
+    try:
+        out = pipeline.render_tracks(tracks, px_per_sec=30.0, nheight=400, keep_db=True)
+    finally:
+        engine.set_render_path(0)
+    _oracle_check(tracks, out, 400)
 
 
 @pytest.mark.parametrize("path", [0, 3, 4])
