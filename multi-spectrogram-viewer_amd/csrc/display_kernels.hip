@@ -1207,6 +1207,15 @@ __global__ void __launch_bounds__(256) resize_h_dma_kernel(uint32_t nh, const Re
     }
     const int nrows = y0 < nh ? (int)((nh - 1 - y0) / G) + 1 : 0;
     const float* rows0 = tmp + r.tmp_off + lb4;
+    // where the image's rows start 4-byte aligned (nwidth and the RGB offset multiples of 4), a
+    // wave's 64 pixels (192 bytes) are packed through LDS and leave as 48 dword stores instead of
+    // 3 x 64 byte stores (a quarter of the addresses for the texture addresser). The LDS accesses
+    // are inline asm: the compiler cannot tell plain LDS accesses from the DMA's targets and would
+    // wait for every DMA in flight before them.
+    const bool drgb = ((r.nw | (uint32_t)r.rgb_off) & 3u) == 0;  // block-uniform
+    const uint32_t wpx = r.nw - (ox0 + 64u * (uint32_t)wave) < 64u ? r.nw - (ox0 + 64u * (uint32_t)wave) : 64u;
+    const int nd = (int)(3u * wpx) >> 2, ntail = (int)(3u * wpx) & 3;  // the wave's dwords, tail bytes
+    const uint32_t stg = lut_lds + 128u + 192u * (uint32_t)wave;        // the wave's 192 staging bytes
     // group g = rows g RP .. g RP + RP - 1 in buffers (g % NB) RP + i; rows past the last repeat
     // it (same DMA count per group, so the counted waits hold; never summed)
     auto dma = [&](int g) {
@@ -1251,7 +1260,30 @@ __global__ void __launch_bounds__(256) resize_h_dma_kernel(uint32_t nh, const Re
                     const CmapPos cp = colormap_pos(t[q]);
                     uint2 e;
                     asm volatile("ds_read_b64 %0, %1\n\ts_waitcnt lgkmcnt(0)" : "=v"(e) : "v"(lut_lds + 8u * (uint32_t)cp.index));
-                    put(o + q * ostep, colormap_lerp(e, cp.ratio));
+                    const uint32_t px = colormap_lerp(e, cp.ratio);
+                    if (drgb) {
+                        uint8_t* ow = o + q * ostep - 3 * lane;  // the wave's first pixel
+                        uint32_t dw;
+                        asm volatile(
+                            "ds_write_b8 %1, %2\n\t"
+                            "ds_write_b8 %1, %3 offset:1\n\t"
+                            "ds_write_b8 %1, %4 offset:2\n\t"
+                            "ds_read_b32 %0, %5\n\t"
+                            "s_waitcnt lgkmcnt(0)"
+                            : "=&v"(dw)
+                            : "v"(stg + 3u * (uint32_t)lane), "v"(px), "v"(px >> 8), "v"(px >> 16),
+                              "v"(stg + 4u * (uint32_t)lane)
+                            : "memory");
+                        if (lane < nd) reinterpret_cast<uint32_t*>(ow)[lane] = dw;
+                        if (lane < ntail) {
+                            uint32_t b;
+                            asm volatile("ds_read_u8 %0, %1\n\ts_waitcnt lgkmcnt(0)"
+                                         : "=v"(b) : "v"(stg + 4u * (uint32_t)nd + (uint32_t)lane) : "memory");
+                            ow[4 * nd + lane] = (uint8_t)b;
+                        }
+                    } else {
+                        put(o + q * ostep, px);
+                    }
                 }
             }
         }
@@ -1273,7 +1305,7 @@ static int launch_resize_h_dma(uint32_t nh, const RenderDesc* d_desc, uint32_t n
     // row buffers (3 and 6 measured slower: 3.40 / 3.42 vs 3.36 ms per C5 step; round 4, 8 for the
     // one-chunk spans: 3.88 vs 3.84 ms, profiles/r04_display/ab_experiments.txt)
     constexpr int NB = 4;
-    const int lds = NB * K * 1024 * 4 + 80;  // + the colormap pairs
+    const int lds = NB * K * 1024 * 4 + 128 + 4 * 192;  // + the colormap pairs, the RGB staging
     const void* kern = nullptr;
 #define THESIA_HDMA(KT_, K_) \
     if (kt == KT_ && K == K_) kern = reinterpret_cast<const void*>(resize_h_dma_kernel<KT_, K_, NB>);
