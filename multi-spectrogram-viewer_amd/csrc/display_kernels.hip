@@ -809,39 +809,65 @@ __global__ void __launch_bounds__(256) grey_vert_kernel(const float* spec, uint3
     const int32_t H = (int32_t)r.H, top = (int32_t)r.H - (int32_t)bins;
     const float* sp = spec + r.spec_off;
     if (staged && rows <= 128) {
-        // thread -> (tile row k = tid mod rows, frame phase p = tid / rows): P = 256 / rows
-        // phases walk the block's frames p, p + P, ...; consecutive threads read consecutive
-        // (descending) bins of one frame (coalesced). A thread's bin, its tile row and whether
-        // its row is inside the track's band [top, H) are fixed, so an element costs its load
-        // (per-thread byte offset + a uniform per-step one), its grey value and an LDS store with
-        // an immediate offset; rows outside the band read a clamped bin and store +0 (the image's
-        // zero fill; padded taps below the image). THESIA_VDEPTH loads in flight per thread.
+        // Tile row k holds bin hy - k (hy = H - 1 - ya). The in-band bins [blo, bhi] are read as
+        // groups of four consecutive bins [4m, 4m + 3] (16-byte loads, never below bin 0: a
+        // buffer load whose offset wraps below the base returns 0 in every dword, measured; past
+        // the frame's last bin it reads the next frame's or, past the block's frames, +0 per
+        // dword -- rows never stored): thread -> (group g = tid mod ng, frame phase p = tid / ng),
+        // P = 256 / ng phases walk the block's frames p, p + P, ...; consecutive threads read
+        // consecutive 16 bytes of one frame row (coalesced). An element costs a quarter of a
+        // load, its grey value and an LDS store. Rows outside the band (the image's zero fill
+        // above it, padded taps below the image) are zero-filled on their own.
         constexpr int D = THESIA_VDEPTH;
-        const int P = __builtin_amdgcn_readfirstlane(256 / rows);  // >= 2 (rows <= 128), uniform
-        const int k = tid % rows, p = tid / rows;
-        const uint32_t nf = r.T - x0 < 64u ? r.T - x0 : 64u;  // the block's frames (uniform)
-        if (p < P) {
-            const int32_t y = ya + k;
-            const bool inb = y >= top && y < H;
-            int32_t b = H - 1 - y;
-            b = b < 0 ? 0 : b < (int32_t)bins ? b : (int32_t)bins - 1;
-            const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
-                const_cast<float*>(sp + (uint64_t)x0 * bins), (short)0, (int)(nf * bins * 4u), 0x00020000);
-            const uint32_t vo = ((uint32_t)p * bins + (uint32_t)b) * 4u;  // this thread's first element
-            const uint32_t step = __builtin_amdgcn_readfirstlane((uint32_t)P * bins * 4u);  // per phase step
-            float* trow = tile + k * TS + p;
-            const int nit = (64 + P - 1) / P;  // phase steps covering 64 frames (uniform)
-            for (int i0 = 0; i0 < nit; i0 += D) {
-                float v[D];
+        const int32_t hy = H - 1 - ya;
+        const int32_t blo = hy - rows + 1 > 0 ? hy - rows + 1 : 0;
+        const int32_t bhi = hy < (int32_t)bins - 1 ? hy : (int32_t)bins - 1;
+        // zero rows: k < hy - bhi (above the band) and k > hy - blo (below the image)
+        const int32_t kz0 = hy - bhi < rows ? (hy - bhi > 0 ? hy - bhi : 0) : rows;
+        const int32_t kz1 = blo <= bhi ? hy - blo + 1 : kz0;  // first zero row below the band
+        {
+            const int nz0 = kz0, nz1 = rows - (kz1 > kz0 ? kz1 : kz0);
+            for (int e = tid; e < (nz0 + nz1) * 64; e += 256) {
+                const int z = e >> 6, f = e & 63;
+                const int kk = z < nz0 ? z : (kz1 > kz0 ? kz1 : kz0) + (z - nz0);
+                tile[kk * TS + f] = 0.0f;
+            }
+        }
+        if (blo <= bhi) {
+            const int mlo = blo >> 2, ng = (bhi >> 2) - mlo + 1;  // <= 34
+            const int P = __builtin_amdgcn_readfirstlane(256 / ng);
+            const int g = tid % ng, p = tid / ng;
+            const uint32_t nf = r.T - x0 < 64u ? r.T - x0 : 64u;  // the block's frames (uniform)
+            if (p < P) {
+                const int32_t b0 = 4 * (mlo + g);
+                const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+                    const_cast<float*>(sp + (uint64_t)x0 * bins), (short)0, (int)(nf * bins * 4u), 0x00020000);
+                const uint32_t vo = ((uint32_t)p * bins + (uint32_t)b0) * 4u;  // this thread's first load
+                const uint32_t step = __builtin_amdgcn_readfirstlane((uint32_t)P * bins * 4u);  // per phase step
+                bool ok[4];
+                float* trow[4];
 #pragma unroll
-                for (int i = 0; i < D; ++i)  // frames past the block's read +0 (range check)
-                    v[i] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rs, vo, (i0 + i) * step, 0));
+                for (int q = 0; q < 4; ++q) {
+                    ok[q] = b0 + q >= blo && b0 + q <= bhi;
+                    trow[q] = tile + (hy - (b0 + q)) * TS + p;
+                }
+                const int nit = (64 + P - 1) / P;  // phase steps covering 64 frames (uniform)
+                typedef float v4f __attribute__((ext_vector_type(4)));
+                for (int i0 = 0; i0 < nit; i0 += D) {
+                    v4f v[D];
 #pragma unroll
-                for (int i = 0; i < D; ++i) {
-                    const int f = p + P * (i0 + i);
-                    float g = gm(v[i]);
-                    asm volatile("" : "+v"(g));  // a select, not a branch around the grey value
-                    if (f < 64) trow[P * (i0 + i)] = inb ? g : 0.0f;
+                    for (int i = 0; i < D; ++i)
+                        v[i] = __builtin_amdgcn_raw_buffer_load_b128(rs, vo, (i0 + i) * step, 0);
+#pragma unroll
+                    for (int i = 0; i < D; ++i) {
+                        const int f = p + P * (i0 + i);
+                        if (f < 64) {
+                            if (ok[0]) trow[0][P * (i0 + i)] = gm(v[i].x);
+                            if (ok[1]) trow[1][P * (i0 + i)] = gm(v[i].y);
+                            if (ok[2]) trow[2][P * (i0 + i)] = gm(v[i].z);
+                            if (ok[3]) trow[3][P * (i0 + i)] = gm(v[i].w);
+                        }
+                    }
                 }
             }
         }
