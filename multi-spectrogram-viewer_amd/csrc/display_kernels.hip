@@ -1226,22 +1226,36 @@ __global__ void __launch_bounds__(256) resize_h_dma_kernel(uint32_t nh, const Re
     const uint64_t ostep = (uint64_t)G * r.nw * 3;  // bytes between the block's rows
     uint8_t* o = rgb + r.rgb_off + (uint64_t)ox * 3 + (uint64_t)blockIdx.y * r.nw * 3;
     uint32_t y0 = blockIdx.y;
+    // where the image's rows start 4-byte aligned (nwidth and the RGB offset multiples of 4), a
+    // wave's 64 pixels (192 bytes) leave as 48 dword stores instead of 64 byte + 64 short stores (a
+    // third of the addresses for the texture addresser): the summed rows packed through LDS (inline
+    // asm: the compiler cannot tell plain LDS accesses from the DMA's targets and would wait for
+    // every DMA in flight before them), the colormap(+0) rows below oz as the repeating pattern
+    const bool drgb = ((r.nw | (uint32_t)r.rgb_off) & 3u) == 0;  // block-uniform
+    const uint32_t wb = ox0 + 64u * (uint32_t)wave;              // the wave's first column
+    const uint32_t wpx = wb < r.nw ? (r.nw - wb < 64u ? r.nw - wb : 64u) : 0u;
+    const int nd = (int)(3u * wpx) >> 2, ntail = (int)(3u * wpx) & 3;  // the wave's dwords, tail bytes
+    const uint32_t stg = lut_lds + 128u + 192u * (uint32_t)wave;        // the wave's 192 staging bytes
     if (r.oz > y0) {
         const uint32_t px = colormap_rgb(0.0f, lut);
-        for (; y0 < r.oz && y0 < nh; y0 += G, o += ostep)
-            if (act) put(o, px);
+        if (drgb) {
+            // byte i of the row piece is component i mod 3 of px; dword lane = bytes 4 lane ..
+            auto comp = [&](int i) { return (px >> (8 * (i % 3))) & 0xFFu; };
+            const int b0 = 4 * lane;
+            const uint32_t dw = comp(b0) | comp(b0 + 1) << 8 | comp(b0 + 2) << 16 | comp(b0 + 3) << 24;
+            const uint32_t tb = comp(4 * nd + lane);
+            uint8_t* ow = o - 3 * tid + 192 * wave;  // the wave's first pixel (o = base + 3 ox)
+            for (; y0 < r.oz && y0 < nh; y0 += G, ow += ostep, o += ostep) {
+                if (lane < nd) reinterpret_cast<uint32_t*>(ow)[lane] = dw;
+                if (lane < ntail) ow[4 * nd + lane] = (uint8_t)tb;
+            }
+        } else {
+            for (; y0 < r.oz && y0 < nh; y0 += G, o += ostep)
+                if (act) put(o, px);
+        }
     }
     const int nrows = y0 < nh ? (int)((nh - 1 - y0) / G) + 1 : 0;
     const float* rows0 = tmp + r.tmp_off + lb4;
-    // where the image's rows start 4-byte aligned (nwidth and the RGB offset multiples of 4), a
-    // wave's 64 pixels (192 bytes) are packed through LDS and leave as 48 dword stores instead of
-    // 3 x 64 byte stores (a quarter of the addresses for the texture addresser). The LDS accesses
-    // are inline asm: the compiler cannot tell plain LDS accesses from the DMA's targets and would
-    // wait for every DMA in flight before them.
-    const bool drgb = ((r.nw | (uint32_t)r.rgb_off) & 3u) == 0;  // block-uniform
-    const uint32_t wpx = r.nw - (ox0 + 64u * (uint32_t)wave) < 64u ? r.nw - (ox0 + 64u * (uint32_t)wave) : 64u;
-    const int nd = (int)(3u * wpx) >> 2, ntail = (int)(3u * wpx) & 3;  // the wave's dwords, tail bytes
-    const uint32_t stg = lut_lds + 128u + 192u * (uint32_t)wave;        // the wave's 192 staging bytes
     // group g = rows g RP .. g RP + RP - 1 in buffers (g % NB) RP + i; rows past the last repeat
     // it (same DMA count per group, so the counted waits hold; never summed)
     auto dma = [&](int g) {
