@@ -1318,6 +1318,9 @@ int minmax_segments_device(const float* d_x, const uint64_t* row0, size_t bins, 
 #ifndef THESIA_VBAND
 #define THESIA_VBAND 64  // widest vertical band tried (64 beat 128-512 on C5: more blocks)
 #endif
+#ifndef THESIA_STRIP
+#define THESIA_STRIP 64  // output columns per stripe block (a multiple of 16)
+#endif
 #ifndef THESIA_VROWS
 #define THESIA_VROWS 128  // grey rows per vertical tile (<= 256; A/B via scripts/build_variant.sh)
 #endif
@@ -1354,7 +1357,7 @@ struct FusedGroup {
     // the single-pass display (render_stripe_kernel) where its instances cover the group's
     // geometry (plan_stripe); then no intermediate is formed
     bool stripe = false;
-    uint32_t st_strip = 64;
+    uint32_t st_strip = THESIA_STRIP;
     int st_kv = 0, st_slots = 0, st_acc = 0, st_fc = 0, st_npf = 0, st_waves = 4, st_tile = 0, st_hdr = 0,
         st_wts = 0;
     bool st_dword = false;
