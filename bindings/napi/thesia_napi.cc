@@ -87,15 +87,27 @@ bool num(napi_env env, napi_value v, double* out) {
     return false;
 }
 
-// a whole number in [0, max] (u32 / usize arguments of the reference); RangeError otherwise
-// (a negative, NaN or huge value cast straight to an unsigned type is undefined behaviour or a
-// huge allocation)
+// wasm-bindgen hands u32 / usize (wasm32: 32-bit) parameters over with ToUint32 (`x >>> 0`):
+// NaN and infinities become 0, fractions truncate toward zero, everything wraps mod 2^32
+// (get_spec_image(id, 100, 250.7) renders 250 rows, as the reference does)
+double to_uint32(double d) {
+    if (!(d == d) || d == __builtin_inf() || d == -__builtin_inf()) return 0.0;
+    double t = __builtin_trunc(d);
+    double m = __builtin_fmod(t, 4294967296.0);
+    if (m < 0) m += 4294967296.0;
+    return m;
+}
+
+// a u32 / usize argument of the reference, coerced like wasm-bindgen (to_uint32); a value above
+// `max` after that is refused with a RangeError -- only the lengths that size an allocation have
+// a max below 2^32 - 1 (the one divergence from the wasm surface)
 bool uint_arg(napi_env env, napi_value v, double max, const char* name, double* out) {
     double d = 0;
     if (!num(env, v, &d)) return false;
-    if (!(d >= 0) || !(d <= max) || d != (double)(uint64_t)d) {
-        napi_throw_range_error(env, "ERR_ARG", (std::string(name) + ": expected a whole number in [0, " +
-                                                std::to_string((uint64_t)max) + "]").c_str());
+    d = to_uint32(d);
+    if (!(d <= max)) {
+        napi_throw_range_error(env, "ERR_ARG", (std::string(name) + ": at most " +
+                                                std::to_string((uint64_t)max) + " accepted").c_str());
         return false;
     }
     *out = d;
@@ -107,11 +119,7 @@ constexpr double kLenMax = 268435456.0;  // 2^28 elements: sizes beyond this are
 bool id_arg(napi_env env, napi_value v, uint64_t* id) {
     double d = 0;
     if (!num(env, v, &d)) return false;
-    if (!(d >= 0) || d != (double)(uint64_t)d) {  // usize in the reference
-        napi_throw_range_error(env, "ERR_ARG", "id must be a non-negative integer");
-        return false;
-    }
-    *id = (uint64_t)d;
+    *id = (uint64_t)to_uint32(d);  // usize in the reference (wasm32): ToUint32 as wasm-bindgen
     return true;
 }
 

@@ -302,6 +302,8 @@ int thesia_minmax_segments_device(const float* d_spec, const uint64_t* row0, siz
  * horizontal + colormap; 3 = path 0 with the two-kernel structure for every group (round 3's
  * default); 4 = path 0 with the single-pass kernel wherever its geometry allows. */
 int thesia_set_render_path(int path);
+/* The render path in effect (the value thesia_set_render_path last stored, 0 by default). */
+int thesia_get_render_path(void);
 int thesia_render_rgb_batch_device(const float* d_spec, const uint64_t* row0, size_t bins,
                                    size_t n, const float* up_ratio, const uint32_t* nwidth,
                                    uint32_t nheight, float max, float min, uint8_t* d_rgb,

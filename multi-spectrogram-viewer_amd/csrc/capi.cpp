@@ -381,6 +381,7 @@ int thesia_batch_set_option(thesia_batch* batch, int option, int64_t value) {
 }
 
 int thesia_set_render_path(int path) { return set_render_path(path); }
+int thesia_get_render_path(void) { return render_path(); }
 int thesia_set_batches_policy(int policy) { return set_batches_policy(policy); }
 
 

@@ -1677,9 +1677,10 @@ int render_rgb_fused(size_t n_groups, const float* const* d_specs, const uint64_
         // the intermediate rows' padding [T, ts) is never written by the vertical pass: zero it
         // once per allocation, so every float a horizontal pass may stage is finite
         if (ws.tmp.p != tmp_before) THESIA_HIP(hipMemsetAsync(ws.tmp.p, 0, ws.tmp.bytes, s));
-        if (!desc.empty())
+        if (!desc.empty()) {
             for (RenderDesc& r : desc) r.grange = d_grange;  // (part of the cache key)
             THESIA_HIP(copy_ordered(ws.desc.p, desc.data(), desc.size() * sizeof(RenderDesc), hipMemcpyHostToDevice));
+        }
         ws.groups = std::move(groups);
         ws.key = std::move(key);
     }

@@ -175,13 +175,10 @@ int MultiTrack::add_tracks(const std::vector<uint64_t>& ids, const std::vector<P
         g.batch.reset(b);
         // the viewer path computes in the reference's operation order (stftx_kernel): its
         // images are the oracle pipeline's bytes; opt-in (set_fast): the automatic streaming
-        // kernel (stft3 at the viewer geometries; stft5 for the 48 kHz mel rows of batches of
-        // >= 400 000 frames), except that linear rows stay on stft3 where stft5 would take them:
-        // stft5's amp dB from |X|^2 flipped 1.3e-4 of the pixels by 1 LSB on the sample files
-        // (stft3: within the e2e contract's 1e-4, tests/test_gpu_parity.py)
+        // kernel (stft3 at the viewer geometries; stft5 for the 48 kHz rows of batches of
+        // >= 400 000 frames), held to the e2e contract relative to the reference's own f32
+        // error (tests/test_gpu_parity.py _check_multitrack)
         rc = batch_set_option(b, THESIA_BATCH_OPT_KERNEL, fast_ ? 0 : 9);
-        if (!rc && fast_ && b->kernel == 5 && b->k3_ok && set_.freq_scale != 1)
-            rc = batch_set_option(b, THESIA_BATCH_OPT_KERNEL, 3);
         if (!rc) rc = batch_run(b, s);
         if (rc) return rc;
         g.spec = spec->as<float>();

@@ -95,6 +95,7 @@ _SIGS = {
     "thesia_batch_ranges_read": (_i, [C.c_void_p, _sz, _fp, _fp, C.POINTER(C.c_int)]),
     "thesia_set_batches_policy": (_i, [_i]),
     "thesia_set_render_path": (_i, [_i]),
+    "thesia_get_render_path": (_i, []),
     "thesia_minmax_device": (_i, [C.c_void_p, C.c_uint64, C.POINTER(C.c_float), C.POINTER(C.c_float),
                                   C.POINTER(C.c_int)]),
     "thesia_spec_to_grey_device": (_i, [C.c_void_p, _sz, _sz, _f, _f, _f, C.c_void_p]),

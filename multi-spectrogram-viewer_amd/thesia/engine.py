@@ -24,6 +24,13 @@ def set_device(d: int) -> None:
     check(lib.thesia_set_device(d))
 
 
+def current_device() -> int:
+    """The device the library's calls from this thread use (thesia_get_device)."""
+    d = C.c_int()
+    check(lib.thesia_get_device(C.byref(d)))
+    return d.value
+
+
 def synchronize() -> None:
     check(lib.thesia_device_synchronize())
 
@@ -249,16 +256,12 @@ def set_render_path(path: int) -> None:
     (default); 1 per-track launches; 2 three-stage launches; 3 two kernels for every group; 4 the
     single-pass kernel wherever its instances cover the geometry (all byte-identical)."""
     check(lib.thesia_set_render_path(path))
-    global _RENDER_PATH
-    _RENDER_PATH = int(path)
-
-
-_RENDER_PATH = 0  # the library's default (thesia_set_render_path)
 
 
 def render_path() -> int:
-    """The render path last set through set_render_path (the library's default 0 otherwise)."""
-    return _RENDER_PATH
+    """The library's render path (thesia_get_render_path: whatever set it, this binding or
+    another one)."""
+    return int(lib.thesia_get_render_path())
 
 
 def synth_pcm_device(buf: DeviceBuffer, fmt: int, channels: int, n_tracks: int, n_samples: int,

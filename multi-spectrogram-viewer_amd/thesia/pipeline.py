@@ -62,13 +62,17 @@ def _geometry(t: Track):
 class RenderPipeline:
     """The C5 pipeline with its inputs resident in HBM: `prepare` uploads the tracks and builds
     one Plan + Batch per geometry group; `run_spectrograms` is one launch per group; `render`
-    runs the global-range exchange and the device display path for every track."""
+    runs the global-range exchange and the device display path for every track. `render` with
+    want_rgb=False and keep_db=False on one rank is asynchronous and returns None (the images
+    stay in HBM); otherwise it returns one Rendered per track."""
 
     def __init__(self, tracks: Sequence[Track], px_per_sec: float = 100.0, nheight: int = 500,
-                 db_range: float = 120.0, pinned_output: bool = False):
+                 db_range: float = 120.0, pinned_output: bool = False, kernel: int = 0):
         """pinned_output: read the RGB images back into one page-locked host buffer (one
         DMA-rate copy per render); the returned images are then views that the next
-        render() overwrites. Default: fresh pageable arrays per render()."""
+        render() overwrites. Default: fresh pageable arrays per render().
+        kernel: the spectrogram kernel of every batch (0 = automatic; 9 = the reference-order
+        kernel, whose images equal the oracle pipeline's bytes; thesia_batch_set_option)."""
         self.tracks = list(tracks)
         self.pinned_output = pinned_output
         self._pinned = {}  # group -> registered host array
@@ -90,7 +94,7 @@ class RenderPipeline:
             din = engine.DeviceBuffer.from_host(flat)
             T_all = engine.Batch.frames_for(plan, lens)
             dout = engine.DeviceBuffer(T_all * plan.row_bins * 4)
-            b = engine.Batch(plan, din, offs, lens, dout, input_format=fmt, channels=ch)
+            b = engine.Batch(plan, din, offs, lens, dout, input_format=fmt, channels=ch, kernel=kernel)
             g = len(self.groups)
             self.groups.append((plan, din, dout, b))
             k0 = 0

@@ -14,4 +14,4 @@ THESIA_RENDER_STREAMS=1 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O
 python3 $R/scripts/kt_segments.py $O/ktg/kt_kernel_trace.csv > $O/groups_kt0.txt
 cat $O/groups_kt0.txt
 cd $R
-bash scripts/gpu_r04_m.sh ${1:-r04_p}/m10 10 0 "grey_vert|resize_h"
+bash scripts/runs/gpu_r04_m.sh ${1:-r04_p}/m10 10 0 "grey_vert|resize_h"

@@ -103,40 +103,158 @@ def test_e2e_rgb_c5_generator():
     assert worst <= E2E_MAX_LSB and diff_px / total_px <= E2E_MAX_FRAC, (worst, diff_px, total_px)
 
 
+def _oracle_specs(pcm, srs, scale, with_f64=False):
+    """Per track: the oracle's amp-dB rows (|X| [, mel], dB; lib.rs:112-136) and, with_f64, the
+    same rows from the float64 spectrum (tolerances.stft_f64), i.e. what both the reference's f32
+    path and the kernels approximate. A thread pool (the oracle's C calls release the GIL)."""
+    from concurrent.futures import ThreadPoolExecutor
+    from tolerances import stft_f64
+    mel = scale == thesia.FreqScale.Mel
+
+    def spec(args):
+        x, sr = args
+        win, hop, n_fft = O.track_params(sr)
+        w = (O.hann(win) / np.float32(n_fft)).astype(np.float32)
+        x = (np.float32(0.0) + x).astype(np.float32)
+        mag = O.norm(O.perform_stft(x, win, hop, n_fft, window=w))
+        fb = O.calc_mel_fb_default(sr, n_fft) if mel else None
+        if mel:
+            mag = O.dot(mag, fb)
+        db64 = None
+        if with_f64:
+            m64 = np.abs(stft_f64(x, win, hop, n_fft, w))
+            if mel:
+                m64 = m64 @ fb.astype(np.float64)
+            db64 = (20.0 * np.log10(np.maximum(m64, 1e-18))).astype(np.float32)
+        return O.amp_to_db_default(mag), db64
+
+    with ThreadPoolExecutor(min(16, len(pcm))) as ex:
+        res = list(ex.map(spec, zip(pcm, srs)))
+    return [r[0] for r in res], [r[1] for r in res]
+
+
+def _global_range(dbs, db_range=120.0):
+    """lib.rs:194-209 (in f32)."""
+    gmax = float(np.float32(min(max(float(d.max()) for d in dbs), 0.0)))
+    gmin = float(np.float32(max(min(float(d.min()) for d in dbs), gmax - db_range)))
+    return gmax, gmin
+
+
+def _oracle_images(pcm, srs, scale, nh, dbs, rng):
+    """spec_to_grey (display.rs:44-54) + Lanczos3 + colormap (display.rs:56-61) of the given dB
+    rows under the given global range, the reference's geometry (lib.rs:231-248, 294-298)."""
+    from concurrent.futures import ThreadPoolExecutor
+    mel = scale == thesia.FreqScale.Mel
+    gmax, gmin = rng
+
+    def one(args):
+        x, sr, db = args
+        up = shard.up_ratio(sr, max(srs), freq_scale_mel=mel)
+        grey = O.spec_to_grey(db, up, gmax, gmin)
+        nwidth = int(np.float32(100.0) * np.float32(len(x)) / np.float32(sr))
+        return np.asarray(O.grey_to_rgb(grey, nwidth, nh)[0], np.uint8)
+    with ThreadPoolExecutor(min(16, len(pcm))) as ex:
+        return list(ex.map(one, zip(pcm, srs, dbs)))
+
+
+def _flipped(a, b):
+    """Pixels of a that differ from b in any channel, and the largest channel difference."""
+    d = np.abs(a.reshape(-1, 3).astype(np.int16) - b.reshape(-1, 3).astype(np.int16)).max(axis=1)
+    return int((d > 0).sum()), int(d.max(initial=0))
+
+
+def _check_multitrack(mt, pcm, srs, scale, nh, exact):
+    """MultiTrack images against the oracle pipeline.
+
+    exact (the reference-order kernel): the global range equals the oracle's and every image is
+    the oracle pipeline's bytes.
+
+    Otherwise SURVEY.md §8c as the reference's own f32 arithmetic allows it (round 5's diagnosis,
+    scripts/diag_e2e_flips.py): a non-reference-order FFT differs from the oracle
+    in bins 100+ dB below their frame's peak (f32 rounding noise: the 48 kHz substitute is 24 kHz
+    content upsampled), where the oracle differs from the float64 spectrum as much (linear
+    excerpts: oracle 1.15e-4, stft3 1.22e-4, stft5 1.41e-4 of the pixels against the float64
+    image). Two consequences are held separately:
+      range: the global max within 1e-3 dB of the oracle's; the global min -- the deepest value of
+        the noise floor when the -120 dB clamp does not bind -- within max(DB_MAX, 2 x the
+        oracle's own distance from the float64 min);
+      images under the device's own range: at most 1 LSB anywhere, flipped pixels at most
+        max(1e-4, 2 x the share the oracle's image flips against the float64 spectrum's image
+        under that range)."""
+    dbs, db64 = _oracle_specs(pcm, srs, scale, with_f64=not exact)
+    ro = _global_range(dbs)
+    rd = (mt.get_max_db(), mt.get_min_db())
+    if exact:
+        assert rd == ro, (rd, ro)
+    else:
+        r64 = _global_range(db64)
+        assert abs(rd[0] - ro[0]) <= 1e-3, (rd, ro)
+        assert abs(rd[1] - ro[1]) <= max(DB_MAX, 2 * abs(ro[1] - r64[1])), (rd, ro, r64)
+    ref = _oracle_images(pcm, srs, scale, nh, dbs, rd)
+    f64 = None if exact else _oracle_images(pcm, srs, scale, nh, db64, rd)
+    flips = f64_flips = total = worst = 0
+    for i in range(len(pcm)):
+        got = np.frombuffer(mt.get_spec_image(i, 100.0, nh), np.uint8)
+        assert got.size == ref[i].size
+        if exact:
+            assert np.array_equal(got, ref[i].reshape(-1)), (i, _flipped(got, ref[i]))
+            continue
+        f, m = _flipped(got, ref[i])
+        flips += f
+        worst = max(worst, m)
+        f64_flips += _flipped(ref[i], f64[i])[0]
+        total += ref[i].size // 3
+    if not exact:
+        bound = max(E2E_MAX_FRAC, 2.0 * f64_flips / total)
+        assert worst <= E2E_MAX_LSB and flips / total <= bound, (worst, flips, f64_flips, total)
+    return flips, f64_flips, total, dbs
+
+
 @pytest.mark.parametrize("fast", [False, True])
 @pytest.mark.parametrize("scale", [thesia.FreqScale.Mel, thesia.FreqScale.Linear])
 def test_e2e_rgb_multitrack_samples(scale, fast):
     """MultiTrack (lib.rs:170-298) on the reference's sample excerpts + the 48 kHz substitute:
-    get_spec_image bytes vs the oracle pipeline from the PCM; fast = the streaming kernel at the
-    viewer's geometries (thesia_mt_set_fast) instead of the reference-order one."""
+    get_spec_image bytes vs the oracle pipeline from the PCM -- equal bytes on the default
+    (reference-order) path; fast = the streaming kernels at the viewer's geometries
+    (thesia_mt_set_fast), held to _check_multitrack's contract."""
     z = np.load(fixtures.GOLDEN + "/samples_excerpt.npz")
     tags = ["8k", "16k", "22k05", "24k", "44k1"]
     pcm = [fixtures.s16_to_f32(z[f"pcm_{t}"]) for t in tags] + [fixtures.s16_to_f32(fixtures.c1_substitute()[:72000])]
     srs = [int(z[f"sr_{t}"]) for t in tags] + [48000]
     mt = thesia.MultiTrack(freq_scale=scale, fast=fast)
     mt.add_tracks_pcm(list(range(len(pcm))), pcm, srs)
-    dbs = []
-    for x, sr in zip(pcm, srs):
-        win, hop, n_fft = O.track_params(sr)
-        w = (O.hann(win) / np.float32(n_fft)).astype(np.float32)
-        mag = O.norm(O.perform_stft((np.float32(0.0) + x).astype(np.float32), win, hop, n_fft, window=w))
-        if scale == thesia.FreqScale.Mel:
-            mag = O.dot(mag, O.calc_mel_fb_default(sr, n_fft))
-        dbs.append(O.amp_to_db_default(mag))
-    gmax = float(np.float32(min(max(float(d.max()) for d in dbs), 0.0)))
-    gmin = float(np.float32(max(min(float(d.min()) for d in dbs), gmax - 120.0)))
-    max_sr = max(srs)
-    nh = 300
-    worst, diff_px, total_px = 0, 0.0, 0
-    for i, (x, sr, db) in enumerate(zip(pcm, srs, dbs)):
-        up = shard.up_ratio(sr, max_sr, freq_scale_mel=scale == thesia.FreqScale.Mel)
-        grey = O.spec_to_grey(db, up, gmax, gmin)
-        nwidth = int(np.float32(100.0) * np.float32(len(x)) / np.float32(sr))
-        img, _ = O.grey_to_rgb(grey, nwidth, nh)
-        got = np.frombuffer(mt.get_spec_image(i, 100.0, nh), np.uint8)
-        assert got.size == img.size
-        m, f = _rgb_diff(got, img)
-        worst = max(worst, m)
-        diff_px += f * img.size / 3
-        total_px += img.size // 3
-    assert worst <= E2E_MAX_LSB and diff_px / total_px <= E2E_MAX_FRAC, (worst, diff_px, total_px)
+    _check_multitrack(mt, pcm, srs, scale, 300, exact=not fast)
+    mt.close()
+
+
+@pytest.mark.parametrize("scale", [thesia.FreqScale.Mel, thesia.FreqScale.Linear])
+def test_e2e_rgb_multitrack_fast_stft5(scale):
+    """MultiTrack's fast path where it takes stft5: one add_tracks of 16
+    48 kHz tracks x 250 s (25 000 frames each, 400 000 frames in the call's batch: the automatic
+    rule's kView5MinFrames, engine.hpp), mel and linear rows, images vs the oracle pipeline under
+    the same contract as the excerpts, plus the dB rows themselves."""
+    from thesia import engine
+    sr, n, k = 48000, 250 * 48000, 16
+    pcm = [fixtures.s16_to_f32(engine.synth_pcm_host(1, i, n, sr, seed=5)).reshape(-1) for i in range(k)]
+    win, hop, n_fft = O.track_params(sr)
+    T = O.stft_n_frames(n, win, hop)
+    assert k * T >= 400000
+    # the automatic rule MultiTrack's fast path applies to this batch (Batch::auto_kernel)
+    kind = engine.OUT_MEL_AMP_DB if scale == thesia.FreqScale.Mel else engine.OUT_AMP_DB
+    plan = engine.Plan(n_fft, win, hop, kind, sr=sr,
+                       **({"mel_fb": O.calc_mel_fb_default(sr, n_fft)} if kind == engine.OUT_MEL_AMP_DB else {}))
+    din, dout = engine.DeviceBuffer(8), engine.DeviceBuffer(8)
+    b = engine.Batch(plan, din, [0] * k, [n] * k, dout)
+    assert b.kernel == 5  # (never run: the buffers only stand in for the rule)
+    b.close()
+    plan.close()
+    din.close()
+    dout.close()
+    mt = thesia.MultiTrack(freq_scale=scale, fast=True)
+    mt.add_tracks_pcm(list(range(k)), pcm, [sr] * k)
+    flips, f64_flips, total, dbs = _check_multitrack(mt, pcm, [sr] * k, scale, 300, exact=False)
+    print(f"stft5 fast path: {flips} flipped of {total} px; the oracle vs float64: {f64_flips}")
+    for i in (0, k - 1):
+        mx, p = db_clamped_err(mt.get_spec(i), dbs[i])
+        assert mx <= DB_MAX and p <= DB_P9999, (i, mx, p)
+    mt.close()

@@ -146,6 +146,31 @@ def test_viewer_48k_stft5_column_rule(kernel, kind, channels, fmt, gap, max_bloc
         _check_kind(kind, r.reshape(ref.shape[0], -1), ref, fb)
 
 
+@pytest.mark.parametrize("win,hop", [(1792, 448), (2040, 510), (2016, 504), (1800, 450), (2048, 496)])
+@pytest.mark.parametrize("kind", [engine.OUT_MAG, engine.OUT_AMP_DB, engine.OUT_MEL_AMP_DB])
+@pytest.mark.parametrize("channels,fmt", [(1, engine.IN_F32), (2, engine.IN_S16)])
+@pytest.mark.parametrize("gap,max_blocks", [(3, 1), (0, 0)])
+def test_stft5_every_supported_view_hop(win, hop, kind, channels, fmt, gap, max_blocks):
+    """stft5_supports takes every even hop with hop / 2 = 7 rows of 32 + rem (rem 0..31) and every
+    even win <= 2048: the column rule at rem 0 (hop 448: the shift-by-HQ+1 select
+    never taken), rem 31 (hop 510), win 2016 / hop 504 (the viewer's 42 ms window at 48 kHz),
+    an odd rem (hop 450: 225 = 7 x 32 + 1) and win = n_fft with a non-canonical hop, forced, against
+    the oracle with odd-offset tracks (per-frame reloads) and one-block grids."""
+    n_fft, sr = 2048, 48000
+    rng = np.random.default_rng(win + hop + 17 * kind + channels + gap)
+    lens = [win - 1, 5 * n_fft + 3, 33 * hop + 1, 97 * hop + 2]
+    tracks = _tracks(rng, lens, channels, fmt)
+    mel = kind == engine.OUT_MEL_AMP_DB
+    plan = engine.Plan(n_fft, win, hop, kind, **({"sr": sr, "n_mels": 128} if mel else {}))
+    k, rows = _run(plan, tracks, channels, fmt, gap, max_blocks=max_blocks, kernel=5)
+    plan.close()
+    assert k == 5
+    fb = O.calc_mel_fb(sr, n_fft, 128) if mel else None
+    for t, r in zip(tracks, rows):
+        ref = O.perform_stft(_x(t, fmt), win, hop, n_fft)
+        _check_kind(kind, r.reshape(ref.shape[0], -1), ref, fb)
+
+
 @pytest.mark.parametrize("n_fft,win,hop", VIEW + VIEW_ODD)
 @pytest.mark.parametrize("kind", _KINDS)
 @pytest.mark.parametrize("max_blocks", [0, 2])
