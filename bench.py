@@ -33,6 +33,7 @@ HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s HBM3E (spec)
 METRIC = "STFT frames/sec (n_fft=2048 hop=512) at 1/2/4/8 GPUs; % HBM roofline"
 KERNEL_NAMES = {1: "thesia::stft_kernel (general)", 2: "thesia::stft2_kernel (general, 4 waves/SIMD)",
                 3: "thesia::stft3_kernel (streaming)", 5: "thesia::stft5_kernel (streaming, n_fft 2048)",
+                7: "thesia::stftr_kernel (streaming, reference order, bit-exact)",
                 9: "thesia::stftx_kernel (reference order, bit-exact)"}
 
 
@@ -66,7 +67,8 @@ def parse():
                    help="CPU baseline threads (0: OMP_NUM_THREADS if set, else the affinity mask)")
     p.add_argument("--variants", default="", help="experiment (needs THESIA_LIB=lib/libthesia_exp.so): "
                    "comma list of THESIA_STFT_VARIANT values to A/B (interleaved rounds, one process)")
-    p.add_argument("--kernel", type=int, default=0, help="force a fused kernel (1/2/3/5; 0 = automatic)")
+    p.add_argument("--kernel", type=int, default=0, help="force a fused kernel (1/2/3/5; 7 / 9 = the bit-exact "
+                   "reference-order kernels, streaming / one wave per frame; 0 = automatic)")
     p.add_argument("--max-blocks", default="", help="A/B of the launch's block count (thesia_batch_set_option "
                    "MAX_BLOCKS): comma list, 0 = the occupancy default")
     p.add_argument("--kernels", default="", help="A/B of named kernels on the product library: comma list "

@@ -363,14 +363,16 @@ static int build_mel4(Plan* p) {
 static const int kLdsG[2][16] = {{0, 1, 2, 3, 12, 13, 14, 15, 20, 21, 22, 23, 24, 25, 26, 27},
                                  {4, 5, 6, 7, 8, 9, 10, 11, 16, 17, 18, 19, 28, 29, 30, 31}};
 
-static int build_melp(Plan* p, int S, Plan::Melp& out) {
+// L: lanes per frame (32: stft5, two frames per wave; 64: stftr, one frame per wave, whose
+// b128 read groups are build_mel4's for each half); region: the floats of a frame's LDS region.
+static int build_melp(Plan* p, int S, Plan::Melp& out, int L = 32, int region = kStft5Region) {
     out.chunks = 0;
     out.steps = S;
-    constexpr int L = 32;
     const long F = (long)p->NC + 1, F4 = (F + 3) / 4 * 4;
     const int M = (int)p->n_mels;
-    if (p->NC != 1024 || F4 != kMelpOut || M <= 0 || kMelpOut + M + kMelpDummies > kStft5Region)
+    if (p->NC != 1024 || F4 != kMelpOut || M <= 0 || kMelpOut + M + kMelpDummies > region)
         return THESIA_OK;  // not stft5's geometry / the mel slots do not fit the region
+    const int NG = L / 16;  // 16-lane groups of a ds_read_b128
     struct Flt { long kmin, kmax; int ch; };
     std::vector<Flt> fl(M);
     for (int m = 0; m < M; ++m) {
@@ -400,15 +402,16 @@ static int build_melp(Plan* p, int S, Plan::Melp& out) {
     const int C = *std::max_element(load.begin(), load.end());
     if (C > 64) return THESIA_OK;
 
-    int grp[L];
-    for (int g = 0; g < 2; ++g)
-        for (int i = 0; i < 16; ++i) grp[kLdsG[g][i]] = g;
+    auto glane = [&](int g, int i) { return kLdsG[g & 1][i] + 32 * (g >> 1); };
+    std::vector<int> grp(L);
+    for (int g = 0; g < NG; ++g)
+        for (int i = 0; i < 16; ++i) grp[glane(g, i)] = g;
     std::vector<long> offs((size_t)L * C);  // |X| float offset per (lane, chunk); -1 = idle
     auto cell = [&](int c, int g) {
         long seen[16][16];
         int cnt[16] = {0}, worst = 0;
         for (int i = 0; i < 16; ++i) {
-            const long o = offs[(size_t)kLdsG[g][i] * C + c];
+            const long o = offs[(size_t)glane(g, i) * C + c];
             if (o < 0) continue;
             const int s = (int)((o / 4) & 15);
             bool dup = false;
@@ -461,7 +464,8 @@ static int build_melp(Plan* p, int S, Plan::Melp& out) {
                 for (int i = 0; i < fl[f].ch; ++i) offs[(size_t)j * C + c0_of[f] + i] = bk + 4L * S * i;
             }
         long total = 0;
-        for (int c = 0; c < C; ++c) total += cell(c, 0) + cell(c, 1);
+        for (int c = 0; c < C; ++c)
+            for (int g = 0; g < NG; ++g) total += cell(c, g);
         if (best < 0 || total < best) {
             best = total;
             best_lane = lane_of;
@@ -494,12 +498,12 @@ static int build_melp(Plan* p, int S, Plan::Melp& out) {
     // idle chunks read an address another lane of their group reads (a broadcast: no cycle)
     std::vector<int> xoff((size_t)(C + 1) * L, 0);
     for (int c = 0; c < C; ++c)
-        for (int g = 0; g < 2; ++g) {
+        for (int g = 0; g < NG; ++g) {
             long any = 0;
             for (int i = 0; i < 16; ++i)
-                if (offs[(size_t)kLdsG[g][i] * C + c] >= 0) { any = offs[(size_t)kLdsG[g][i] * C + c]; break; }
+                if (offs[(size_t)glane(g, i) * C + c] >= 0) { any = offs[(size_t)glane(g, i) * C + c]; break; }
             for (int i = 0; i < 16; ++i) {
-                const int j = kLdsG[g][i];
+                const int j = glane(g, i);
                 const long o = offs[(size_t)j * C + c];
                 xoff[(size_t)c * L + j] = (int)((o >= 0 ? o : any) * 4);
             }
@@ -639,12 +643,19 @@ int plan_create(const thesia_plan_desc& d, Plan** out) {
         if (!rc) rc = build_mel(p);
         if (!rc) rc = build_mel4(p);
         for (int i = 0; i < 2 && !rc; ++i) rc = build_melp(p, 2 + i, p->melp[i]);
+        for (int i = 0; i < 2 && !rc; ++i) rc = build_melp(p, 2 + i, p->melr[i], 64, stftr_region_floats());
         if (!rc) {  // default: the fewest estimated instructions per chunk stream (5 + 6 S each)
             long bc = -1;
             for (int i = 0; i < 2; ++i)
                 if (p->melp[i].chunks > 0) {
                     const long c = (long)p->melp[i].chunks * (5 + 6 * p->melp[i].steps);
                     if (bc < 0 || c < bc) { bc = c; p->melp_best = i; }
+                }
+            bc = -1;
+            for (int i = 0; i < 2; ++i)
+                if (p->melr[i].chunks > 0) {
+                    const long c = (long)p->melr[i].chunks * (5 + 6 * p->melr[i].steps);
+                    if (bc < 0 || c < bc) { bc = c; p->melr_best = i; }
                 }
         }
         if (!rc) {  // the reference-order kernel: each mel's nonzero band, weights flat
@@ -779,6 +790,18 @@ int batch_create(Plan* plan, const thesia_batch_desc& d, Batch** out) {
         b->apply_mel_path();
     }
     b->k5_ok = k5_geo && stft5_lds_bytes(L) <= 163840;
+    // the reference-order streaming kernel (stftr): canonical n_fft 2048 geometry; mel kinds
+    // need its packed stream (64 lanes per frame)
+    if (plan->melr_best >= 0) {
+        const Plan::Melp& m = plan->melr[plan->melr_best];
+        L.melr_chunks = m.chunks;
+        L.melr_steps = m.steps;
+        L.melr_meta = m.meta.as<int4>();
+        L.melr_wt = m.wt.as<float4>();
+    }
+    const bool mel_kind = L.out_kind == OUT_MEL || L.out_kind == OUT_MEL_AMP_DB;
+    b->kr_ok = stftr_supports((int)plan->n_fft, (int)plan->win, (int)plan->hop, d.input_format, (int)d.channels) &&
+               (!mel_kind || L.melr_chunks > 0) && stftr_lds_bytes(L) <= 163840;
     b->k5_view = view5;
     b->kernel = b->auto_kernel();
     if (hipEventCreate(&b->ev0) != hipSuccess || hipEventCreate(&b->ev1) != hipSuccess) {
@@ -813,6 +836,7 @@ int batch_set_option(Batch* b, int option, int64_t value) {
             else if (value == 2 && stft2_supports((int)b->plan->n_fft)) b->kernel = 2;
             else if (value == 3 && b->k3_ok) b->kernel = 3;
             else if (value == 5 && b->k5_ok) b->kernel = 5;
+            else if (value == 7 && b->kr_ok) b->kernel = 7;
             else if (value == 9 && stftx_lds_bytes((int)b->plan->n_fft, true) <= 163840) b->kernel = 9;
             else return set_error(THESIA_ERR_UNSUPPORTED, "kernel " + std::to_string(value) +
                                                              " does not run this batch's geometry");
@@ -874,6 +898,9 @@ int batch_run(Batch* b, hipStream_t s) {
     if (b->kernel == 9) {
         rc = launch_stftx(b->launch, s);
         if (rc) return set_error(rc == -2 ? THESIA_ERR_UNSUPPORTED : THESIA_ERR_DEVICE, "stftx launch failed");
+    } else if (b->kernel == 7) {
+        rc = launch_stftr(b->launch, s);
+        if (rc) return set_error(rc == -2 ? THESIA_ERR_UNSUPPORTED : THESIA_ERR_DEVICE, "stftr launch failed");
     } else {
         if (b->kernel == 5) rc = launch_stft5(b->launch, s);
         if (rc == -2 && b->kernel >= 3) {

@@ -94,6 +94,8 @@ struct Plan {
         int steps = 0;
     } melp[2];
     int melp_best = -1;  // index into melp of the default (fewest estimated instructions), -1 none
+    Melp melr[2];        // the same stream for 64 lanes per frame (stftr_kernel)
+    int melr_best = -1;
     bool use_v2 = false;  // stft2_kernel runs this plan (n_fft 256..2048)
     size_t row_bins() const;
     size_t out_elem_bytes() const { return out_kind == OUT_COMPLEX ? 8 : 4; }
@@ -108,11 +110,12 @@ struct Batch {
     DevBuf d_in_off, d_len, d_frame0;
     uint64_t total_frames = 0;
     StftLaunch launch{};
-    // 1 stft_kernel, 2 stft2_kernel, 3 stft3_kernel, 5 stft5_kernel (streaming), 9 stftx_kernel
-    // (reference operation order)
+    // 1 stft_kernel, 2 stft2_kernel, 3 stft3_kernel, 5 stft5_kernel (streaming), 7 stftr_kernel
+    // (streaming, reference operation order), 9 stftx_kernel (reference operation order)
     int kernel = 1;
     bool k3_ok = false;  // the streaming kernel supports this batch's geometry
     bool k5_ok = false;  // ... and so does its n_fft 2048 variant (stft5_kernel)
+    bool kr_ok = false;  // the reference-order streaming kernel (stftr_kernel) runs this batch
     // automatic choice: stft5 for the mel kinds at n_fft 2048 and for linear rows without the
     // range option (measured faster there: stereo power dB 5.64 vs 6.22 ms in round 3; slower for
     // complex rows, 9.0 vs 6.98 ms, and stft3 folds the per-track range into its row epilogue;

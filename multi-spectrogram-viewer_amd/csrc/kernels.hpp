@@ -82,6 +82,11 @@ struct StftLaunch {
     int melp_v4 = 0;  // n_mels % 4 == 0 and 16-byte aligned rows: float4 row stores
     const int4* melp_meta = nullptr;
     const float4* melp_wt = nullptr;
+    // the same packed stream built for 64 lanes per frame (stftr_kernel's one frame per wave)
+    int melr_chunks = 0;
+    int melr_steps = 0;
+    const int4* melr_meta = nullptr;
+    const float4* melr_wt = nullptr;
     // output
     void* out = nullptr;  // packed rows: frame g at out + g * row_elems
     // scheduling / named alternatives (thesia_batch_set_option)
@@ -153,6 +158,12 @@ int launch_irfftx(const float* in, uint64_t n_frames, int length, const int* xpo
 int launch_stft5(const StftLaunch& a, hipStream_t stream);
 bool stft5_supports(int n_fft, int win, int hop, int in_format, int channels);
 int stft5_lds_bytes(const StftLaunch& a);
+// stftr_kernel (streaming, reference operation order: rows equal the oracle's bit for bit;
+// n_fft 2048, win = n_fft, hop = n_fft / 4; stftr_kernels.hip)
+int launch_stftr(const StftLaunch& a, hipStream_t stream);
+bool stftr_supports(int n_fft, int win, int hop, int in_format, int channels);
+int stftr_lds_bytes(const StftLaunch& a);
+constexpr int stftr_region_floats() { return 16 * 136; }  // GeoR::REGION
 // LDS bytes / frames per block pass / lanes per frame of the kernel for n_fft.
 int stft_kernel_info(int n_fft, int* lds_bytes, int* tile_frames, int* lanes_per_frame);
 

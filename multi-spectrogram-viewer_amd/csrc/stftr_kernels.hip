@@ -1,0 +1,491 @@
+// stftr_kernels.hip -- the reference-order STREAMING STFT (batch kernel 7): every f32 operation of
+// the reference path in the reference's order, as stftx_kernel (stftx_kernels.hip), so the rows
+// equal the oracle's bit for bit, with the streaming data movement of the fast kernels
+// (stft3/stft5): a wave walks consecutive frames of a stream, the downmixed samples stay in a
+// register ring and a hop loads only its new samples.
+//
+// n_fft 2048 (NC = 1024 complex points), win = n_fft, hop = n_fft / 4: the C2-C4 geometry of
+// BASELINE.json. One frame per 64-lane wave, 16 points per lane.
+//
+// rustfft 4.0 Radix4 for NC = 1024 (oracle cfft_tab, realfft.rs:126-138): input point m sits at
+// position p = digit-reverse4(m) (prepare_radix4); level 0 is butterfly_4 over base-4 digit 0 of
+// p, levels 1..4 are butterfly_4 over digit l with the table twiddles tw[j t NC / 4^(l+1)], j = p
+// mod 4^l. Bit-exactness needs only that every butterfly sees the same operands in the same
+// operation order -- which lane holds which point does not matter. So:
+//   ring layout   lane l holds m = l + 64 n (n < 16): the hop (256 points) keeps a point in its
+//                 lane (the ring shifts by 4 registers). m's base-4 digits (i0 .. i4) are p's
+//                 digits reversed: lane l = d4 + 4 d3 + 16 d2, register n = d1 + 4 d0.
+//   levels 0, 1   in registers (digits d0, d1); level-1 twiddles are wave-uniform (tw[64 d0 t]).
+//   swap          lane bits 4, 5 (d2) <-> register bits 2, 3 (d0): v_permlane16_swap /
+//                 v_permlane32_swap, one VALU per dword (no LDS): lane = d4 + 4 d3 + 16 d0,
+//                 register = d1 + 4 d2.
+//   level 2       in registers (d2; twiddles per lane from the LDS table).
+//   transpose     LDS, one row of 64 complex per p >> 6: lane l writes its 16 points into row
+//                 d3 + 4 d4 (columns d0 + 4 n), lane reads column c = p mod 64 (row stride 136
+//                 floats: the 64 lanes' stores land 4 per bank, the row reads are contiguous).
+//   levels 3, 4   in registers (d3, d4): register r holds Z[c + 64 r] (natural order).
+//   untangle      realfft.rs:142-157 on the pairs (k, NC - k): the partner of column c is 64 - c,
+//                 and lanes are numbered so that it is lane +- 32 (c <= 32: lane c; c > 32: lane
+//                 96 - c), so one v_permlane32_swap per dword brings the partner's Z[8 .. 15];
+//                 lanes 0 (c = 0) and 32 (c = 32) pair inside their own column.
+//   |X|           hypotf as glibc (double, one rounding; exact_math.hpp), |X|^2 as num-complex
+//                 norm_sqr, mel as the k-ascending fma chain (a packed stream for 64 lanes,
+//                 engine.cpp build_melp), dB with glibc's log10f (exact_math.hpp).
+// No fused multiply-add anywhere but the mel chain (the oracle's dot is an fma chain):
+// -ffp-contract=off, products as num-complex Mul.
+#include "exact_math.hpp"
+#include "stft3_core.hpp"
+
+#include <type_traits>
+
+namespace thesia {
+
+struct GeoR {
+    static constexpr int NC = 1024, L = 64, P = 16, F = NC + 1, SH = 4, KEEP = P - SH;
+    static constexpr int RS = 136;             // transpose row stride (floats): 128 + 8
+    static constexpr int REGION = 16 * RS;     // per-wave LDS region (floats): 2176
+    static constexpr int WL_STRIDE = 2 * P + 4;  // window row of a lane (floats)
+    static constexpr int WL_FLOATS = L * WL_STRIDE;
+    static constexpr int TW_FLOATS = 2 * NC + 4;   // rustfft twiddles tw[0 .. NC)
+    static constexpr int SC_FLOATS = 2 * NC + 4;   // realfft sin_cos, entry NC = padding
+    static constexpr int TAB_FLOATS = WL_FLOATS + TW_FLOATS + SC_FLOATS;
+    static_assert(REGION >= 2 * F + 3 && REGION >= kMelpOut + 16 && REGION == stftr_region_floats(), "region");
+};
+
+namespace {
+
+// num-complex Mul (no fused multiply-add): (a.re b.re - a.im b.im, a.re b.im + a.im b.re)
+__device__ __forceinline__ float2 rmul(float2 a, float2 b) {
+    return make_float2(a.x * b.x - a.y * b.y, a.x * b.y + a.y * b.x);
+}
+
+// rustfft butterfly_4 (levels >= 1, forward; oracle cfft_tab), in place
+__device__ __forceinline__ void rbfly(float2& d0, float2& d1, float2& d2, float2& d3, float2 w1,
+                                      float2 w2, float2 w3) {
+    const float2 s0 = rmul(d1, w1), s1 = rmul(d2, w2), s2 = rmul(d3, w3);
+    const float2 s5 = csub(d0, s1);
+    const float2 a = cadd(d0, s1);
+    const float2 s3 = cadd(s0, s2), s4 = csub(s0, s2);
+    d2 = csub(a, s3);
+    d0 = cadd(a, s3);
+    d1 = make_float2(s5.x + s4.y, s5.y - s4.x);
+    d3 = make_float2(s5.x - s4.y, s5.y + s4.x);
+}
+
+// rustfft Butterfly4 (the base level, forward): bfly2(0, 2), bfly2(1, 3), rotate 3 by -i,
+// bfly2(0, 1), bfly2(2, 3), outputs (0, 2, 1, 3)
+__device__ __forceinline__ void rbfly4(float2& a0, float2& a1, float2& a2, float2& a3) {
+    float2 v0 = a0, v1 = a1, v2 = a2, v3 = a3;
+    float2 t = cadd(v0, v2);
+    v2 = csub(v0, v2);
+    v0 = t;
+    t = cadd(v1, v3);
+    v3 = csub(v1, v3);
+    v1 = t;
+    v3 = make_float2(v3.y, -v3.x);
+    t = cadd(v0, v1);
+    v1 = csub(v0, v1);
+    v0 = t;
+    t = cadd(v2, v3);
+    v3 = csub(v2, v3);
+    v2 = t;
+    a0 = v0;
+    a1 = v2;
+    a2 = v1;
+    a3 = v3;
+}
+
+__device__ __forceinline__ float2 pl16(float2& x, float2& y) {  // swap odd rows of x with even rows of y
+    auto rx = __builtin_amdgcn_permlane16_swap(__builtin_bit_cast(unsigned, x.x), __builtin_bit_cast(unsigned, y.x),
+                                               false, false);
+    auto ry = __builtin_amdgcn_permlane16_swap(__builtin_bit_cast(unsigned, x.y), __builtin_bit_cast(unsigned, y.y),
+                                               false, false);
+    x = make_float2(__builtin_bit_cast(float, rx[0]), __builtin_bit_cast(float, ry[0]));
+    y = make_float2(__builtin_bit_cast(float, rx[1]), __builtin_bit_cast(float, ry[1]));
+    return x;
+}
+__device__ __forceinline__ void pl32(float2& x, float2& y) {  // lanes 32..63 of x <-> lanes 0..31 of y
+    auto rx = __builtin_amdgcn_permlane32_swap(__builtin_bit_cast(unsigned, x.x), __builtin_bit_cast(unsigned, y.x),
+                                               false, false);
+    auto ry = __builtin_amdgcn_permlane32_swap(__builtin_bit_cast(unsigned, x.y), __builtin_bit_cast(unsigned, y.y),
+                                               false, false);
+    x = make_float2(__builtin_bit_cast(float, rx[0]), __builtin_bit_cast(float, ry[0]));
+    y = make_float2(__builtin_bit_cast(float, rx[1]), __builtin_bit_cast(float, ry[1]));
+}
+
+// decibel.rs:49-55 (ref 1: log_ref = 0) then the factor pass (:65 / :75), glibc log10f
+__device__ __forceinline__ float rdb(float x, float log_amin, float amin, float factor) {
+    const float y = x > amin ? exact::log10f_glibc(x) - 0.0f : log_amin - 0.0f;
+    return factor * y;
+}
+
+// The packed mel stream for 64 lanes per frame (engine.cpp build_melp with L = 64): lane j runs
+// its filters' chunks back to back, each a k-ascending fma chain over S float4 steps of the |X|
+// row (region), its running sum stored at woff and ANDed with keep after the chunk; chunk c + 1's
+// meta, weights and |X| are read before chunk c's chain.
+template <int S>
+__device__ __forceinline__ void melr_stream(const int4* meta, const float4* wt, float* region, int lj, int C) {
+    constexpr int L = GeoR::L;
+    char* rb = reinterpret_cast<char*>(region);
+    const int4* mp = meta + lj;
+    const float4* wp = wt + lj;
+    struct Buf {
+        float4 w[S], x[S];
+        int4 m;
+    };
+    auto issue = [&](int c, int xoff, Buf& b) {
+        b.m = mp[(c + 1) * L];
+#pragma unroll
+        for (int u = 0; u < S; ++u) b.w[u] = wp[(c * S + u) * L];
+        const float4* xp = reinterpret_cast<const float4*>(rb + xoff);
+#pragma unroll
+        for (int u = 0; u < S; ++u) b.x[u] = xp[u];
+        __builtin_amdgcn_sched_barrier(0);
+    };
+    float acc = 0.0f;
+    auto chain = [&](const Buf& b) {
+#pragma unroll
+        for (int u = 0; u < S; ++u) {
+            acc = __builtin_fmaf(b.x[u].x, b.w[u].x, acc);
+            acc = __builtin_fmaf(b.x[u].y, b.w[u].y, acc);
+            acc = __builtin_fmaf(b.x[u].z, b.w[u].z, acc);
+            acc = __builtin_fmaf(b.x[u].w, b.w[u].w, acc);
+        }
+        *reinterpret_cast<float*>(rb + b.m.x) = acc;
+        acc = __builtin_bit_cast(float, __builtin_bit_cast(int, acc) & b.m.y);
+    };
+    Buf A, B;
+    int c = 0;
+    const int x0 = mp[0].z;
+    if (C & 1) {
+        issue(0, x0, B);
+        issue(1, B.m.z, A);
+        chain(B);
+        c = 1;
+    } else {
+        issue(0, x0, A);
+    }
+    for (; c < C; c += 2) {
+        issue(c + 1, A.m.z, B);
+        chain(A);
+        issue(c + 2, B.m.z, A);
+        chain(B);
+    }
+}
+
+}  // namespace
+
+// OK: 0 complex, 1 linear kinds, 2 mel kinds. C: 1 mono, 2 stereo (interleaved); INF: f32 / s16.
+// WV waves per block (one block per CU): 12 (3 waves per SIMD) or 8.
+template <int OK, int C, int INF, int WV>
+__global__ void __launch_bounds__(64 * WV)
+stftr_kernel(StftLaunch a, uint64_t fps) {
+    using G = GeoR;
+    using CK = Chunk<C, INF>;
+    using CT = typename CK::T;
+    using ET = typename std::conditional<INF == IN_S16, int16_t, float>::type;
+    constexpr int NC = G::NC, P = G::P, L = G::L, F = G::F, SH = G::SH, KEEP = G::KEEP, RS = G::RS;
+
+    extern __shared__ __attribute__((aligned(16))) float lds[];
+    float* wtl = lds;
+    float2* twl = reinterpret_cast<float2*>(lds + G::WL_FLOATS);
+    float2* scl = reinterpret_cast<float2*>(lds + G::WL_FLOATS + G::TW_FLOATS);
+    float* work = lds + G::TAB_FLOATS;
+    const bool mel = OK == 2;
+    int4* pm_lds = reinterpret_cast<int4*>(work + WV * G::REGION);
+    float4* pw_lds = reinterpret_cast<float4*>(pm_lds + (mel ? (a.melr_chunks + 2) * L : 0));
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    constexpr int kBlock = 64 * WV;
+
+    for (int i = threadIdx.x; i < 2 * NC; i += kBlock) {  // window: lane row (w[2m], w[2m+1])
+        const int m = i >> 1, l = m % L, n = m / L;
+        wtl[l * G::WL_STRIDE + 2 * n + (i & 1)] = a.wpad[i];
+    }
+    for (int i = threadIdx.x; i < NC; i += kBlock) {
+        twl[i] = a.tw1[i];
+        scl[i] = a.sincos[i];
+    }
+    if (threadIdx.x == 0) scl[NC] = make_float2(0.f, 0.f);
+    if constexpr (OK == 2) {
+        for (int i = threadIdx.x; i < (a.melr_chunks + 2) * L; i += kBlock) pm_lds[i] = a.melr_meta[i];
+        const int nw = (a.melr_chunks + 1) * a.melr_steps * L;
+        for (int i = threadIdx.x; i < nw; i += kBlock) pw_lds[i] = a.melr_wt[i];
+    }
+    __syncthreads();
+
+    // lane roles: the column this lane holds after the transpose (partner column 64 - c is lane
+    // +- 32), the row it writes in the transpose, its digit d0 after the swap
+    const int col = lane <= 32 ? lane : 96 - lane;
+    const bool lo_half = lane < 32;
+    const bool lane0 = lane == 0, special = lane == 0 || lane == 32;
+    const int wrow = ((lane >> 2) & 3) + 4 * (lane & 3);  // d3 + 4 d4
+    const int d0s = lane >> 4;                             // d0 after the swap
+    // level-3 twiddles: tw[c t 4], t = 1..3 (fixed per lane)
+    const float2 w3a = twl[col * 4], w3b = twl[col * 8], w3c = twl[col * 12];
+
+    const uint64_t total = a.total_frames;
+    const uint64_t stream = (uint64_t)blockIdx.x * WV + wave;
+    const uint64_t g0 = stream * fps;
+    const uint64_t g1 = g0 + fps < total ? g0 + fps : total;
+    const int hop = a.hop;
+    float* region = work + wave * G::REGION;
+    const ET* in = static_cast<const ET*>(a.in);
+
+    float2 raw[P];
+    CT pre[SH];
+    bool pre_ok = false;
+    int hint = -1;
+    uint64_t g_beg = 1, g_end = 0, base = 0;
+    int64_t n = 0;
+    for (uint64_t it = 0; it < fps; ++it) {  // wave-uniform trip count
+        const uint64_t g = g0 + it;
+        const bool valid = g < g1;
+        int lj = lane;
+        asm volatile("" : "+v"(lj));
+        int64_t start = 0;
+        if (valid) {
+            if (g >= g_end || g < g_beg) {
+                hint = find_track(a.trk_frame0, a.n_tracks, g, hint);
+                g_beg = a.trk_frame0[hint];
+                g_end = a.trk_frame0[hint + 1];
+                n = (int64_t)a.trk_len[hint];
+                base = a.trk_in_off[hint];
+            }
+            start = (int64_t)(g - g_beg) * hop - NC;  // t hop - win / 2 (pad_left = 0)
+        }
+        // ---- the frame's downmixed samples: ring shift by SH rows + the prefetched hop ----
+        if (pre_ok) {
+#pragma unroll
+            for (int q = 0; q < KEEP; ++q) raw[q] = raw[q + SH];
+#pragma unroll
+            for (int q = 0; q < SH; ++q) raw[KEEP + q] = CK::mix(pre[q]);
+        } else if (valid && start >= 0 && start + 2 * NC <= n && ((base + (uint64_t)start * C) % (2 * C)) == 0) {
+            const CT* src = reinterpret_cast<const CT*>(in + base + (uint64_t)start * C) + lj;
+#pragma unroll
+            for (int q = 0; q < P; ++q) raw[q] = CK::mix(src[L * q]);
+        } else if (valid) {
+#pragma unroll
+            for (int e = 0; e < 2; ++e) {
+                wave_lds_sync();
+                fill_raw_half<L, P, INF>(a.in, region, lj, start, n, base, C, a.fold != 0, e);
+                wave_lds_sync();
+#pragma unroll
+                for (int q = 0; q < P; ++q) {
+                    const float r = region[L * q + lj];
+                    if (e == 0) raw[q].x = r; else raw[q].y = r;
+                }
+            }
+            wave_lds_sync();
+        } else {
+#pragma unroll
+            for (int q = 0; q < P; ++q) raw[q] = make_float2(0.f, 0.f);
+        }
+        // ---- prefetch the next frame's new points (rows KEEP .. P - 1) ----
+        {
+            const int64_t nstart = start + hop;
+            const bool nxt = valid && g + 1 < g1 && g + 1 < g_end && nstart + 2 * NC <= n &&
+                             nstart + 2 * L * KEEP >= 0 &&
+                             ((base + (uint64_t)(nstart + 2 * L * KEEP) * C) % (2 * C)) == 0;
+            if (nxt) {
+                const CT* src = reinterpret_cast<const CT*>(in + base + (uint64_t)(nstart + 2 * L * KEEP) * C) + lj;
+#pragma unroll
+                for (int q = 0; q < SH; ++q) pre[q] = src[L * q];
+            }
+            pre_ok = nxt;
+        }
+        // ---- window (lib.rs:379: x * w) ----
+        float2 v[P];
+        {
+            const float4* wr = reinterpret_cast<const float4*>(wtl + lj * G::WL_STRIDE);
+#pragma unroll
+            for (int q = 0; q < P / 2; ++q) {
+                const float4 w = wr[q];
+                v[2 * q] = make_float2(raw[2 * q].x * w.x, raw[2 * q].y * w.y);
+                v[2 * q + 1] = make_float2(raw[2 * q + 1].x * w.z, raw[2 * q + 1].y * w.w);
+            }
+        }
+        // ---- level 0: Butterfly4 over d0 (registers d1 + 4 d0) ----
+#pragma unroll
+        for (int d1 = 0; d1 < 4; ++d1) rbfly4(v[d1], v[d1 + 4], v[d1 + 8], v[d1 + 12]);
+        // ---- level 1: butterfly_4 over d1, j = d0, twiddles tw[64 j t] (wave-uniform) ----
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+            rbfly(v[4 * j], v[4 * j + 1], v[4 * j + 2], v[4 * j + 3], twl[64 * j], twl[128 * j], twl[192 * j]);
+        // ---- swap lane bits 4, 5 with register bits 2, 3 ----
+#pragma unroll
+        for (int q = 0; q < 16; ++q)
+            if ((q & 4) == 0) pl16(v[q], v[q + 4]);
+#pragma unroll
+        for (int q = 0; q < 8; ++q) pl32(v[q], v[q + 8]);
+        // ---- level 2: butterfly_4 over d2 (registers d1 + 4 d2), j = d0 + 4 d1 ----
+#pragma unroll
+        for (int d1 = 0; d1 < 4; ++d1) {
+            const int j = d0s + 4 * d1;
+            rbfly(v[d1], v[d1 + 4], v[d1 + 8], v[d1 + 12], twl[16 * j], twl[32 * j], twl[48 * j]);
+        }
+        // ---- LDS transpose: row d3 + 4 d4, column d0 + 4 n'; read column col ----
+        wave_lds_sync();
+        {
+            float2* wb = reinterpret_cast<float2*>(region + wrow * RS) + d0s;
+#pragma unroll
+            for (int q = 0; q < P; ++q) wb[4 * q] = v[q];
+        }
+        wave_lds_sync();
+        {
+            const float2* rb = reinterpret_cast<const float2*>(region) + col;
+#pragma unroll
+            for (int r = 0; r < P; ++r) v[r] = rb[r * (RS / 2)];
+        }
+        // ---- level 3: butterfly_4 over d3 (registers d3 + 4 d4), j = col ----
+#pragma unroll
+        for (int d4 = 0; d4 < 4; ++d4) rbfly(v[4 * d4], v[4 * d4 + 1], v[4 * d4 + 2], v[4 * d4 + 3], w3a, w3b, w3c);
+        // ---- level 4: butterfly_4 over d4, j = col + 64 d3 ----
+#pragma unroll
+        for (int d3 = 0; d3 < 4; ++d3) {
+            const int j = col + 64 * d3;
+            rbfly(v[d3], v[d3 + 4], v[d3 + 8], v[d3 + 12], twl[j], twl[2 * j], twl[3 * j]);
+        }
+        // v[r] = Z[col + 64 r]. ---- the partner column's Z[8 .. 15] (lanes +- 32) ----
+        float2 pr[8];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            float2 x = v[8 + i], y = v[8 + i];
+            pl32(x, y);
+            // lanes < 32 receive into y, lanes >= 32 into x; lanes 0 and 32 keep their own
+            float2 t = lo_half ? y : x;
+            pr[i] = special ? v[8 + i] : t;
+        }
+        // partner of own register r (r < 8): general and lane 32: pr[7 - r] (= Z_partner[15 - r]);
+        // lane 0: Z[(16 - r) & 15] = r == 0 ? v[0] : pr[8 - r]
+        wave_lds_sync();  // the transpose's reads are done: the region takes the output row
+        auto sc_at = [&](int k) { return scl[k]; };
+        // realfft.rs:142-156 for bins k (own) and NC - k (partner), the 1/2 last
+        auto pair = [&](float2 b, float2 rr, float2 sck, float2 sckp, float2& xk, float2& xkp) {
+            const float sre = b.x + rr.x, sim = b.y + rr.y;
+            const float dre = b.x - rr.x, dim = b.y - rr.y;
+            xk.x = 0.5f * ((sre + sck.y * sim) - sck.x * dre);
+            xk.y = 0.5f * ((dim - sck.x * sim) - sck.y * dre);
+            // partner: b' = rr, r' = b: (rr.re + b.re) = sre, (rr.re - b.re) = -dre, ...
+            xkp.x = 0.5f * ((sre + sckp.y * sim) - sckp.x * (-dre));
+            xkp.y = 0.5f * (((-dim) - sckp.x * sim) - sckp.y * (-dre));
+        };
+        float* row = region;
+        const int sh = OK == 2 ? 0
+                     : (int)((reinterpret_cast<uintptr_t>(static_cast<float*>(a.out) + g * (uint64_t)(OK == 0 ? 2 * F : F)) >> 2) & 3);
+        auto emit = [&](int k, float2 x) {
+            if constexpr (OK == 0) {
+                *reinterpret_cast<float2*>(row + sh + 2 * k) = x;
+            } else {
+                const int kind = a.out_kind;
+                float val;
+                if (kind == OUT_POWER || kind == OUT_POWER_DB) {
+                    val = x.x * x.x + x.y * x.y;  // num-complex norm_sqr
+                    if (kind == OUT_POWER_DB) val = rdb(val, a.log_amin, 1e-36f, 10.0f);
+                } else {
+                    val = exact::hypotf_glibc(x.x, x.y);  // num-complex norm (lib.rs:124)
+                    if (kind == OUT_AMP_DB) val = rdb(val, a.log_amin, 1e-18f, 20.0f);
+                }
+                row[sh + k] = val;
+            }
+        };
+#pragma unroll
+        for (int r = 0; r < 8; ++r) {
+            const int k = col + 64 * r;
+            float2 rr = pr[7 - r];
+            if (r == 0) rr = lane0 ? v[0] : rr;
+            else rr = lane0 ? pr[8 - r] : rr;
+            const int kp = NC - k;  // lane 0, r = 0: bin NC (set below)
+            float2 xk, xkp;
+            pair(v[r], rr, sc_at(k), sc_at(kp), xk, xkp);
+            if (r == 0 && lane0) xkp = make_float2(v[0].x - v[0].y, 0.0f);  // realfft.rs:157
+            emit(k, xk);
+            emit(kp, xkp);
+        }
+        {  // lane 0: bin NC / 2 pairs with itself (realfft.rs:142-156 with b = r = Z[NC/2])
+            float2 xk, xkp;
+            pair(v[8], v[8], sc_at(NC / 2), sc_at(NC / 2), xk, xkp);
+            if (lane0) emit(NC / 2, xk);
+        }
+        wave_lds_sync();
+        if constexpr (OK == 2) {
+            // lib.rs:131 (the packed stream) then amp dB (decibel.rs:79-88)
+            if (lane0) {
+#pragma unroll
+                for (int k = F; k < kMelpOut; ++k) row[k] = 0.0f;
+            }
+            wave_lds_sync();
+            if (a.melr_steps == 2) melr_stream<2>(pm_lds, pw_lds, region, lj, a.melr_chunks);
+            else melr_stream<3>(pm_lds, pw_lds, region, lj, a.melr_chunks);
+            wave_lds_sync();
+            const int n_mels = a.n_mels;
+            const bool db = a.out_kind == OUT_MEL_AMP_DB;
+            float* out = static_cast<float*>(a.out) + g * (uint64_t)n_mels;
+            for (int m = lj; m < n_mels; m += L) {
+                const float x = region[kMelpOut + m];
+                if (valid) out[m] = db ? rdb(x, a.log_amin, 1e-18f, 20.0f) : x;
+            }
+        } else {
+            constexpr int nfl = OK == 0 ? 2 * F : F;
+            float* frow = static_cast<float*>(a.out) + g * (uint64_t)nfl;
+            if (valid) store_row_b128<L>(frow, sh, region, nfl, lj);
+        }
+    }
+}
+
+// ------------------------------------------------------------------------------------------
+// host side
+// ------------------------------------------------------------------------------------------
+static int ldsr_bytes(const StftLaunch& a, int wv) {
+    const bool mel = a.out_kind == OUT_MEL || a.out_kind == OUT_MEL_AMP_DB;
+    const int meltab = mel ? ((a.melr_chunks + 2) + (a.melr_chunks + 1) * a.melr_steps) * GeoR::L * 16 : 0;
+    return (GeoR::TAB_FLOATS + wv * GeoR::REGION) * 4 + meltab;
+}
+
+template <int OK, int C, int INF, int WV>
+static int launchr_k(const StftLaunch& a, hipStream_t s) {
+    const int lds = ldsr_bytes(a, WV);
+    if (lds > 163840) return -2;
+    auto kern = stftr_kernel<OK, C, INF, WV>;
+    if (hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize, lds) !=
+        hipSuccess)
+        return -1;
+    if (a.total_frames == 0) return 0;
+    int grid = grid_for(reinterpret_cast<const void*>(kern), 64 * WV, lds, (a.total_frames + WV - 1) / WV, a.grid,
+                        a.grid_share);
+    const uint64_t streams = (uint64_t)grid * WV;
+    const uint64_t fps = (a.total_frames + streams - 1) / streams;
+    grid = (int)((a.total_frames + fps * WV - 1) / (fps * WV));
+    hipLaunchKernelGGL(kern, dim3(grid), dim3(64 * WV), lds, s, a, fps);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+template <int OK, int C, int INF>
+static int launchr_w(const StftLaunch& a, hipStream_t s) {
+    if (ldsr_bytes(a, 12) <= 163840) return launchr_k<OK, C, INF, 12>(a, s);
+    return launchr_k<OK, C, INF, 8>(a, s);
+}
+
+template <int C, int INF>
+static int launchr_c(const StftLaunch& a, hipStream_t s) {
+    if (a.out_kind == OUT_COMPLEX) return launchr_w<0, C, INF>(a, s);
+    if (a.out_kind == OUT_MEL || a.out_kind == OUT_MEL_AMP_DB) {
+        if (a.melr_chunks <= 0) return -2;
+        return launchr_w<2, C, INF>(a, s);
+    }
+    return launchr_w<1, C, INF>(a, s);
+}
+
+bool stftr_supports(int n_fft, int win, int hop, int in_format, int channels) {
+    return n_fft == 2048 && win == n_fft && hop * 4 == n_fft && (in_format == IN_F32 || in_format == IN_S16) &&
+           (channels == 1 || channels == 2);
+}
+
+int stftr_lds_bytes(const StftLaunch& a) { return ldsr_bytes(a, 8); }
+
+int launch_stftr(const StftLaunch& a, hipStream_t s) {
+    if (!stftr_supports(a.n_fft, a.win, a.hop, a.in_format, a.channels)) return -2;
+    if (a.in_format == IN_S16) return a.channels == 2 ? launchr_c<2, IN_S16>(a, s) : launchr_c<1, IN_S16>(a, s);
+    return a.channels == 2 ? launchr_c<2, IN_F32>(a, s) : launchr_c<1, IN_F32>(a, s);
+}
+
+}  // namespace thesia
