@@ -34,39 +34,14 @@ void DevBuf::release() {
     bytes = 0;
 }
 
-// The library's own stream-ordered memory pool per device (hipMemPoolCreate, not the device's
-// default pool: no other allocator in the process is affected). Its release threshold is
-// unlimited, so a block freed by hipFreeAsync stays reserved for the library's next allocation
-// without a device synchronisation; trim_pool() hands the unused reserve back to the device
-// (MultiTrack destroy / compaction, thesia_pool_trim, and before an allocation is retried
-// after running out of memory). nullptr where pools are unavailable.
-static hipMemPool_t lib_pool() {
-    static std::mutex mu;
-    static std::map<int, hipMemPool_t> pools;
-    int dev = 0;
-    (void)hipGetDevice(&dev);
-    std::lock_guard<std::mutex> lk(mu);
-    auto it = pools.find(dev);
-    if (it != pools.end()) return it->second;
-    hipMemPool_t pool = nullptr;
-    hipMemPoolProps props{};
-    props.allocType = hipMemAllocationTypePinned;
-    props.handleTypes = hipMemHandleTypeNone;
-    props.location.type = hipMemLocationTypeDevice;
-    props.location.id = dev;
-    if (hipMemPoolCreate(&pool, &props) == hipSuccess && pool) {
-        uint64_t thr = ~uint64_t(0);
-        if (hipMemPoolSetAttribute(pool, hipMemPoolAttrReleaseThreshold, &thr) != hipSuccess) {
-            (void)hipMemPoolDestroy(pool);
-            pool = nullptr;
-        }
-    } else {
-        pool = nullptr;
-    }
-    (void)hipGetLastError();
-    pools[dev] = pool;  // never destroyed: library buffers may outlive any owner object
-    return pool;
-}
+// The library's stream-ordered memory pool (rounds 3-4: hipMemPoolCreate + hipMallocFromPoolAsync /
+// hipFreeAsync on the library stream, so add_tracks paid no hipFree) is OFF: on this runtime
+// (ROCm 7.2) kernel writes into pool blocks past the first ~32-64 MiB of a call's allocations
+// were lost (MultiTrack greys of a 16-track call read back as zeros, the images as garbage, an
+// illegal memory access once), while the same calls with hipMalloc are exact
+// (scripts/diag_mt_grey5.py). DevBuf allocates with hipMalloc / hipFree;
+// trim_pool / pool_bytes stay as no-ops of the C ABI.
+static hipMemPool_t lib_pool() { return nullptr; }
 
 int trim_pool() {
     hipMemPool_t pool = lib_pool();
@@ -124,11 +99,36 @@ int DevBuf::upload(const void* host, size_t n) {
     return THESIA_OK;
 }
 
+bool host_pinned(const void* p) {
+    hipPointerAttribute_t a{};
+    if (!p || hipPointerGetAttributes(&a, p) != hipSuccess) {
+        (void)hipGetLastError();
+        return false;
+    }
+    return a.type == hipMemoryTypeHost;
+}
+
 // A blocking copy ordered after everything already enqueued on the library stream (a plain
-// hipMemcpy runs on the null stream, which does not wait for the non-blocking library stream)
+// hipMemcpy runs on the null stream, which does not wait for the non-blocking library stream).
+// Page-locked host memory: an async copy on the library stream + its synchronisation. Pageable
+// host memory: the runtime stages such a copy and its DMA is not ordered with the library stream
+// (round 5: MultiTrack uploads of pageable PCM into pool buffers were still landing after the
+// stream's synchronisation -- grey images overwritten after they were formed, and an illegal
+// memory access once the pool reused / trimmed the block); so the stream is drained first, the
+// copy is the blocking hipMemcpy, and the device is synchronised after it.
+hipError_t copy_on(void* dst, const void* src, size_t bytes, hipMemcpyKind kind, hipStream_t s) {
+    if (!bytes) return hipSuccess;
+    const void* host = kind == hipMemcpyHostToDevice ? src : kind == hipMemcpyDeviceToHost ? dst : nullptr;
+    if (!host || host_pinned(host)) return hipMemcpyAsync(dst, src, bytes, kind, s);
+    hipError_t e = hipStreamSynchronize(s);
+    if (e == hipSuccess) e = hipMemcpy(dst, src, bytes, kind);
+    if (e == hipSuccess && kind == hipMemcpyHostToDevice) e = hipDeviceSynchronize();
+    return e;
+}
+
 hipError_t copy_ordered(void* dst, const void* src, size_t bytes, hipMemcpyKind kind) {
     hipStream_t s = default_stream();
-    hipError_t e = hipMemcpyAsync(dst, src, bytes, kind, s);
+    hipError_t e = copy_on(dst, src, bytes, kind, s);
     if (e == hipSuccess) e = hipStreamSynchronize(s);
     return e;
 }
@@ -1030,7 +1030,7 @@ int set_batches_policy(int policy) {
 int ranges_read(const int* d_range, size_t n, float* mx, float* mn, int* nan, hipStream_t s) {
     if (n == 0) return THESIA_OK;
     std::vector<int> h(3 * n);
-    THESIA_HIP(hipMemcpyAsync(h.data(), d_range, h.size() * sizeof(int), hipMemcpyDeviceToHost, s));
+    THESIA_HIP(copy_on(h.data(), d_range, h.size() * sizeof(int), hipMemcpyDeviceToHost, s));
     THESIA_HIP(hipStreamSynchronize(s));
     for (size_t i = 0; i < n; ++i) {
         mx[i] = range_unord(h[3 * i]);
@@ -1060,8 +1060,8 @@ int minmax_device(const float* d_x, uint64_t n, float* mx, float* mn, bool* nan,
         return set_error(THESIA_ERR_DEVICE, "minmax launch failed");
     std::vector<float> h((size_t)nblk * 2);
     int hf = 0;
-    THESIA_HIP(hipMemcpyAsync(h.data(), part.p, h.size() * sizeof(float), hipMemcpyDeviceToHost, s));
-    THESIA_HIP(hipMemcpyAsync(&hf, flag.p, sizeof(int), hipMemcpyDeviceToHost, s));
+    THESIA_HIP(copy_on(h.data(), part.p, h.size() * sizeof(float), hipMemcpyDeviceToHost, s));
+    THESIA_HIP(copy_on(&hf, flag.p, sizeof(int), hipMemcpyDeviceToHost, s));
     THESIA_HIP(hipStreamSynchronize(s));
     float a = -INFINITY, b = INFINITY;
     for (int i = 0; i < nblk; ++i) {
@@ -1315,14 +1315,14 @@ static int minmax_segments_core(size_t n_groups, const float* const* d_x, const 
     if (!rc) rc = grow(ws.part, ntr * nper * 2 * sizeof(float));
     if (!rc) rc = grow(ws.flag, ntr * sizeof(int));
     if (rc) return rc;
-    THESIA_HIP(hipMemcpyAsync(ws.seg.p, bounds.data(), bounds.size() * 8, hipMemcpyHostToDevice, s));
+    THESIA_HIP(copy_on(ws.seg.p, bounds.data(), bounds.size() * 8, hipMemcpyHostToDevice, s));
     THESIA_HIP(hipMemsetAsync(ws.flag.p, 0, ntr * sizeof(int), s));
     if (launch_minmax_seg(base, ws.seg.as<uint64_t>(), (int)ntr, nper, ws.part.as<float>(), ws.flag.as<int>(), s))
         return set_error(THESIA_ERR_DEVICE, "minmax_seg launch failed");
     std::vector<float> h(ntr * nper * 2);
     std::vector<int> hf(ntr);
-    THESIA_HIP(hipMemcpyAsync(h.data(), ws.part.p, h.size() * sizeof(float), hipMemcpyDeviceToHost, s));
-    THESIA_HIP(hipMemcpyAsync(hf.data(), ws.flag.p, ntr * sizeof(int), hipMemcpyDeviceToHost, s));
+    THESIA_HIP(copy_on(h.data(), ws.part.p, h.size() * sizeof(float), hipMemcpyDeviceToHost, s));
+    THESIA_HIP(copy_on(hf.data(), ws.flag.p, ntr * sizeof(int), hipMemcpyDeviceToHost, s));
     THESIA_HIP(hipStreamSynchronize(s));
     for (size_t i = 0; i < ntr; ++i) {
         float a = -INFINITY, b = INFINITY;  // empty track: ndarray-stats EmptyInput -> -inf / +inf
@@ -1888,8 +1888,7 @@ int render_rgb_batch_device(const float* d_spec, const uint64_t* row0, size_t bi
         if (!rc) rc = grow(ws.tmp, tmp_tot * sizeof(float));
         if (!rc) rc = grow(ws.desc, desc.size() * sizeof(RenderDesc));
         if (rc) return rc;
-        THESIA_HIP(hipMemcpyAsync(ws.desc.p, desc.data(), desc.size() * sizeof(RenderDesc),
-                                  hipMemcpyHostToDevice, s));
+        THESIA_HIP(copy_on(ws.desc.p, desc.data(), desc.size() * sizeof(RenderDesc), hipMemcpyHostToDevice, s));
         DevBuf& grey = ws.grey;
         DevBuf& tmp = ws.tmp;
         DevBuf& ddesc = ws.desc;
@@ -1951,7 +1950,7 @@ int wav_to_image_device(const float* d_wav, uint64_t n, uint32_t nwidth, uint32_
     if (launch_wav_image(d_wav, n, up.p ? up.as<float>() : nullptr, n_up, nwidth, nheight, spp,
                          amp_min, amp_max, d_out, flag.as<int>(), s))
         return set_error(THESIA_ERR_DEVICE, "wav image launch failed");
-    THESIA_HIP(hipMemcpyAsync(panicked, flag.p, sizeof(int), hipMemcpyDeviceToHost, s));
+    THESIA_HIP(copy_on(panicked, flag.p, sizeof(int), hipMemcpyDeviceToHost, s));
     THESIA_HIP(hipStreamSynchronize(s));
     return THESIA_OK;
 }

@@ -66,6 +66,10 @@ hipStream_t default_stream();  // library stream of the current device
 int trim_pool();
 int pool_bytes(uint64_t* reserved, uint64_t* used);
 hipError_t copy_ordered(void* dst, const void* src, size_t bytes, hipMemcpyKind kind);
+bool host_pinned(const void* p);  // page-locked (hipHostMalloc / hipHostRegister) host memory
+// a copy on stream s: async where the host side is page-locked (or device to device); a pageable
+// host side takes the blocking copy after s drains (+ a device synchronisation for uploads)
+hipError_t copy_on(void* dst, const void* src, size_t bytes, hipMemcpyKind kind, hipStream_t s);
 
 // ---- plan ----
 struct Plan {

@@ -163,7 +163,7 @@ int stft5_lds_bytes(const StftLaunch& a);
 int launch_stftr(const StftLaunch& a, hipStream_t stream);
 bool stftr_supports(int n_fft, int win, int hop, int in_format, int channels);
 int stftr_lds_bytes(const StftLaunch& a);
-constexpr int stftr_region_floats() { return 16 * 136; }  // GeoR::REGION
+constexpr int stftr_region_floats() { return 16 * 130; }  // GeoR::REGION
 // LDS bytes / frames per block pass / lanes per frame of the kernel for n_fft.
 int stft_kernel_info(int n_fft, int* lds_bytes, int* tile_frames, int* lanes_per_frame);
 

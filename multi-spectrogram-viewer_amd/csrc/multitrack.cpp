@@ -151,11 +151,28 @@ int MultiTrack::add_tracks(const std::vector<uint64_t>& ids, const std::vector<P
         if (!rc) rc = wav->alloc(std::max<uint64_t>(wf, 1) * sizeof(float));
         if (!rc) rc = spec->alloc(std::max<uint64_t>(T_all * g.bins, 1) * sizeof(float));
         if (rc) return rc;
+        // uploads: page-locked sources (the file path's staging) as async copies on the library
+        // stream; pageable ones (decoded PCM handed in by the caller) by the blocking copy after
+        // the stream has drained, then a device synchronisation before any kernel reads them
+        // (copy_ordered: a pageable copy's DMA is not ordered with the library stream)
+        bool pageable = false;
         for (size_t k = 0; k < idx.size(); ++k) {
             const PcmIn& in = pcm[idx[k]];
             const uint64_t bytes = in.n_samples * in.channels * pcm_bytes(in.kind);
             uint8_t* dst = raw.as<uint8_t>() + roff[k];
-            if (bytes) THESIA_HIP(hipMemcpyAsync(dst, in.data, bytes, hipMemcpyHostToDevice, s));
+            if (!bytes) continue;
+            if (host_pinned(in.data)) {
+                THESIA_HIP(hipMemcpyAsync(dst, in.data, bytes, hipMemcpyHostToDevice, s));
+            } else {
+                if (!pageable) THESIA_HIP(hipStreamSynchronize(s));
+                pageable = true;
+                THESIA_HIP(hipMemcpy(dst, in.data, bytes, hipMemcpyHostToDevice));
+            }
+        }
+        if (pageable) THESIA_HIP(hipDeviceSynchronize());
+        for (size_t k = 0; k < idx.size(); ++k) {
+            const PcmIn& in = pcm[idx[k]];
+            uint8_t* dst = raw.as<uint8_t>() + roff[k];
             if (launch_decode_downmix(dst, in.kind, in.scale, (int)in.channels, in.n_samples,
                                       wav->as<float>() + g.off[k], s))
                 return set_error(THESIA_ERR_DEVICE, "decode / downmix launch failed");

@@ -21,8 +21,8 @@
 //                 register = d1 + 4 d2.
 //   level 2       in registers (d2; twiddles per lane from the LDS table).
 //   transpose     LDS, one row of 64 complex per p >> 6: lane l writes its 16 points into row
-//                 d3 + 4 d4 (columns d0 + 4 n), lane reads column c = p mod 64 (row stride 136
-//                 floats: the 64 lanes' stores land 4 per bank, the row reads are contiguous).
+//                 d3 + 4 d4 (columns d0 + 4 n), lane reads column c = p mod 64 (row stride 130
+//                 floats: conflict-free stores and contiguous row reads).
 //   levels 3, 4   in registers (d3, d4): register r holds Z[c + 64 r] (natural order).
 //   untangle      realfft.rs:142-157 on the pairs (k, NC - k): the partner of column c is 64 - c,
 //                 and lanes are numbered so that it is lane +- 32 (c <= 32: lane c; c > 32: lane
@@ -42,8 +42,12 @@ namespace thesia {
 
 struct GeoR {
     static constexpr int NC = 1024, L = 64, P = 16, F = NC + 1, SH = 4, KEEP = P - SH;
-    static constexpr int RS = 136;             // transpose row stride (floats): 128 + 8
-    static constexpr int REGION = 16 * RS;     // per-wave LDS region (floats): 2176
+    // transpose row stride (floats): 128 + 2. A ds_write_b64 serves 16 contiguous lanes per LDS
+    // cycle with banks (a/4) mod 32; those lanes write one column of 16 different rows, so rows
+    // 2 dwords apart mod 32 put the 16 lanes on all 32 banks once. The reads (ds_read_b64, 32
+    // lanes, banks mod 64) take 64 contiguous dwords of a row.
+    static constexpr int RS = 130;
+    static constexpr int REGION = 16 * RS;     // per-wave LDS region (floats): 2080
     static constexpr int WL_STRIDE = 2 * P + 4;  // window row of a lane (floats)
     static constexpr int WL_FLOATS = L * WL_STRIDE;
     static constexpr int TW_FLOATS = 2 * NC + 4;   // rustfft twiddles tw[0 .. NC)
@@ -95,22 +99,29 @@ __device__ __forceinline__ void rbfly4(float2& a0, float2& a1, float2& a2, float
     a3 = v3;
 }
 
-__device__ __forceinline__ float2 pl16(float2& x, float2& y) {  // swap odd rows of x with even rows of y
-    auto rx = __builtin_amdgcn_permlane16_swap(__builtin_bit_cast(unsigned, x.x), __builtin_bit_cast(unsigned, y.x),
-                                               false, false);
-    auto ry = __builtin_amdgcn_permlane16_swap(__builtin_bit_cast(unsigned, x.y), __builtin_bit_cast(unsigned, y.y),
-                                               false, false);
-    x = make_float2(__builtin_bit_cast(float, rx[0]), __builtin_bit_cast(float, ry[0]));
-    y = make_float2(__builtin_bit_cast(float, rx[1]), __builtin_bit_cast(float, ry[1]));
-    return x;
+// v_permlane16_swap / v_permlane32_swap as inline asm. The builtins are mis-optimised by this
+// compiler (ROCm 7.2): a lane select between the two results, `lane < 32 ? r[1] : r[0]`, folds
+// to r[0], and half of a run of swaps disappeared (scripts/probes/permlane_probe.hip pins the
+// hardware semantics; the fold is visible in the .s). asm keeps every swap and both results.
+// s_nop 1: the two wait states a VALU write of an operand needs before the swap reads it (the
+// compiler's hazard recognizer does not look inside asm).
+// pl16: the odd 16-lane rows of x <-> the even rows of y; pl32: lanes 32..63 of x <-> lanes 0..31 of y
+__device__ __forceinline__ void pl16(float2& x, float2& y) {
+    asm volatile("s_nop 1\n\tv_permlane16_swap_b32 %0, %2\n\tv_permlane16_swap_b32 %1, %3"
+                 : "+v"(x.x), "+v"(x.y), "+v"(y.x), "+v"(y.y));
 }
-__device__ __forceinline__ void pl32(float2& x, float2& y) {  // lanes 32..63 of x <-> lanes 0..31 of y
-    auto rx = __builtin_amdgcn_permlane32_swap(__builtin_bit_cast(unsigned, x.x), __builtin_bit_cast(unsigned, y.x),
-                                               false, false);
-    auto ry = __builtin_amdgcn_permlane32_swap(__builtin_bit_cast(unsigned, x.y), __builtin_bit_cast(unsigned, y.y),
-                                               false, false);
-    x = make_float2(__builtin_bit_cast(float, rx[0]), __builtin_bit_cast(float, ry[0]));
-    y = make_float2(__builtin_bit_cast(float, rx[1]), __builtin_bit_cast(float, ry[1]));
+__device__ __forceinline__ void pl32(float2& x, float2& y) {
+    asm volatile("s_nop 1\n\tv_permlane32_swap_b32 %0, %2\n\tv_permlane32_swap_b32 %1, %3"
+                 : "+v"(x.x), "+v"(x.y), "+v"(y.x), "+v"(y.y));
+}
+
+// branch-free lane select (v_bfi_b32): m all ones -> a, m zero -> b (a ternary on float2 values
+// next to the asm swaps became exec-mask branches)
+__device__ __forceinline__ float bsel(unsigned m, float a, float b) {
+    return __builtin_bit_cast(float, (__builtin_bit_cast(unsigned, a) & m) | (__builtin_bit_cast(unsigned, b) & ~m));
+}
+__device__ __forceinline__ float2 bsel2(unsigned m, float2 a, float2 b) {
+    return make_float2(bsel(m, a.x, b.x), bsel(m, a.y, b.y));
 }
 
 // decibel.rs:49-55 (ref 1: log_ref = 0) then the factor pass (:65 / :75), glibc log10f
@@ -216,8 +227,8 @@ stftr_kernel(StftLaunch a, uint64_t fps) {
     // lane roles: the column this lane holds after the transpose (partner column 64 - c is lane
     // +- 32), the row it writes in the transpose, its digit d0 after the swap
     const int col = lane <= 32 ? lane : 96 - lane;
-    const bool lo_half = lane < 32;
-    const bool lane0 = lane == 0, special = lane == 0 || lane == 32;
+    const bool lane0 = lane == 0;
+    const unsigned m_lo = lane < 32 ? ~0u : 0u, m_sp = (lane & 31) == 0 ? ~0u : 0u, m_l0 = lane0 ? ~0u : 0u;
     const int wrow = ((lane >> 2) & 3) + 4 * (lane & 3);  // d3 + 4 d4
     const int d0s = lane >> 4;                             // d0 after the swap
     // level-3 twiddles: tw[c t 4], t = 1..3 (fixed per lane)
@@ -352,8 +363,7 @@ stftr_kernel(StftLaunch a, uint64_t fps) {
             float2 x = v[8 + i], y = v[8 + i];
             pl32(x, y);
             // lanes < 32 receive into y, lanes >= 32 into x; lanes 0 and 32 keep their own
-            float2 t = lo_half ? y : x;
-            pr[i] = special ? v[8 + i] : t;
+            pr[i] = bsel2(m_sp, v[8 + i], bsel2(m_lo, y, x));
         }
         // partner of own register r (r < 8): general and lane 32: pr[7 - r] (= Z_partner[15 - r]);
         // lane 0: Z[(16 - r) & 15] = r == 0 ? v[0] : pr[8 - r]
@@ -391,13 +401,11 @@ stftr_kernel(StftLaunch a, uint64_t fps) {
 #pragma unroll
         for (int r = 0; r < 8; ++r) {
             const int k = col + 64 * r;
-            float2 rr = pr[7 - r];
-            if (r == 0) rr = lane0 ? v[0] : rr;
-            else rr = lane0 ? pr[8 - r] : rr;
+            const float2 rr = bsel2(m_l0, r == 0 ? v[0] : pr[8 - r], pr[7 - r]);
             const int kp = NC - k;  // lane 0, r = 0: bin NC (set below)
             float2 xk, xkp;
             pair(v[r], rr, sc_at(k), sc_at(kp), xk, xkp);
-            if (r == 0 && lane0) xkp = make_float2(v[0].x - v[0].y, 0.0f);  // realfft.rs:157
+            if (r == 0) xkp = bsel2(m_l0, make_float2(v[0].x - v[0].y, 0.0f), xkp);  // realfft.rs:157
             emit(k, xk);
             emit(kp, xkp);
         }

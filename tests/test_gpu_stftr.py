@@ -107,7 +107,7 @@ KINDS = [engine.OUT_COMPLEX, engine.OUT_MAG, engine.OUT_POWER, engine.OUT_AMP_DB
 @pytest.mark.parametrize("gap,max_blocks", [(0, 0), (3, 1)])
 def test_linear_kinds_bit_exact(kind, channels, fmt, gap, max_blocks):
     rng = np.random.default_rng(kind * 17 + channels * 5 + fmt + gap)
-    lens = [WIN // 2 + 1, WIN - 1, WIN + 3, 5 * N_FFT + 7, 97 * HOP + 2, 211 * HOP + 11]
+    lens = [WIN - 1, WIN, WIN + 3, 5 * N_FFT + 7, 97 * HOP + 2, 211 * HOP + 11]
     tracks = _tracks(rng, lens, channels, fmt, wide=True)
     _check(kind, tracks, _run(kind, tracks, channels, fmt, gap, max_blocks), fmt)
 
