@@ -729,9 +729,13 @@ int batch_create(Plan* plan, const thesia_batch_desc& d, Batch** out) {
     }
     b->frame0[d.n_tracks] = acc;
     b->total_frames = acc;
-    int rc = b->d_in_off.upload(b->in_off.data(), b->in_off.size() * 8);
-    if (!rc) rc = b->d_len.upload(b->len.data(), b->len.size() * 8);
-    if (!rc) rc = b->d_frame0.upload(b->frame0.data(), b->frame0.size() * 8);
+    // the three per-track tables in one allocation (one hipMalloc / hipFree per batch)
+    std::vector<uint64_t> tabs;
+    tabs.reserve(3 * d.n_tracks + 1);
+    tabs.insert(tabs.end(), b->in_off.begin(), b->in_off.end());
+    tabs.insert(tabs.end(), b->len.begin(), b->len.end());
+    tabs.insert(tabs.end(), b->frame0.begin(), b->frame0.end());
+    int rc = b->d_tabs.upload(tabs.data(), tabs.size() * 8);
     if (rc) {
         delete b;
         return rc;
@@ -746,9 +750,9 @@ int batch_create(Plan* plan, const thesia_batch_desc& d, Batch** out) {
     L.channels = (int)d.channels;
     L.fold = (d.channels > 1 || d.fold_mono || d.input_format == THESIA_IN_S16) ? 1 : 0;
     L.in = d.d_input;
-    L.trk_in_off = b->d_in_off.as<uint64_t>();
-    L.trk_len = b->d_len.as<uint64_t>();
-    L.trk_frame0 = b->d_frame0.as<uint64_t>();
+    L.trk_in_off = b->d_tabs.as<uint64_t>();
+    L.trk_len = L.trk_in_off + d.n_tracks;
+    L.trk_frame0 = L.trk_len + d.n_tracks;
     L.n_tracks = (int)d.n_tracks;
     L.total_frames = b->total_frames;
     L.wpad = plan->wpad.as<float>();
@@ -917,7 +921,7 @@ int batch_run(Batch* b, hipStream_t s) {
                                                         hipGetErrorString(hipGetLastError()));
     }
     if (b->range && !in_kernel &&
-        launch_range_rows(static_cast<const float*>(b->desc.d_output), b->d_frame0.as<uint64_t>(), n_tr,
+        launch_range_rows(static_cast<const float*>(b->desc.d_output), b->launch.trk_frame0, n_tr,
                           (uint32_t)b->plan->row_bins(), b->range, s))
         return set_error(THESIA_ERR_DEVICE, "range launch failed");
     return THESIA_OK;

@@ -111,7 +111,7 @@ struct Batch {
     Plan* plan = nullptr;
     thesia_batch_desc desc{};
     std::vector<uint64_t> in_off, len, frame0;
-    DevBuf d_in_off, d_len, d_frame0;
+    DevBuf d_tabs;  // [in_off | len | frame0] on the device (launch.trk_* point into it)
     uint64_t total_frames = 0;
     StftLaunch launch{};
     // 1 stft_kernel, 2 stft2_kernel, 3 stft3_kernel, 5 stft5_kernel (streaming), 7 stftr_kernel

@@ -96,11 +96,67 @@ THESIA_HD inline float log10f_glibc(float x) {
     return z + y * log10_2hi;
 }
 
+// log10f_glibc for positive NORMAL finite x without branches: the subnormal scalings of
+// log10f / logf never apply, and logf's early return for x == 1 gives the same +0 as the
+// general path (table entry 9 is {1, 0}: r = 0, y = 0). Equal to log10f_glibc (and glibc) on
+// every positive normal float (tests/test_exact_math.py, exhaustive).
+THESIA_HD inline float log10f_normal(float x) {
+    const float ivln10 = 4.3429449201e-01f, log10_2hi = 3.0102920532e-01f, log10_2lo = 7.9034151668e-07f;
+    const double Ln2 = 0x1.62e42fefa39efp-1;
+    const double A0 = -0x1.00ea348b88334p-2, A1 = 0x1.5575b0be00b6ap-2, A2 = -0x1.ffffef20a4123p-2;
+    const int32_t hx = (int32_t)f32_bits(x);
+    const int32_t k0 = (hx >> 23) - 127;
+    const int32_t i0 = (int32_t)(((uint32_t)k0 & 0x80000000u) >> 31);
+    const uint32_t ix = (uint32_t)((hx & 0x007fffff) | ((0x7f - i0) << 23));  // x' in [1, 2) or [0.5, 1)
+    const float y = (float)(k0 + i0);
+    // logf(x') (optimized-routines logf.c)
+    const uint32_t tmp = ix - 0x3f330000u;
+    const int i = (int)((tmp >> (23 - 4)) % 16);
+    const int k = (int32_t)tmp >> 23;
+    const uint32_t iz = ix - (tmp & (0x1ffu << 23));
+    const double invc = kLogfT[i].invc, logc = kLogfT[i].logc;
+    const double z = (double)bits_f32(iz);
+    const double r = z * invc - 1.0;
+    const double y0 = logc + (double)k * Ln2;
+    const double r2 = r * r;
+    double q = A1 * r + A2;
+    q = A0 * r2 + q;
+    q = q * r2 + (y0 + r);
+    const float lx = (float)q;
+    const float zz = y * log10_2lo + ivln10 * lx;
+    return zz + y * log10_2hi;
+}
+
 // hypotf for finite x, y (glibc 2.35: double evaluation, one rounding)
 THESIA_HD inline float hypotf_glibc(float x, float y) {
     const double dx = (double)x, dy = (double)y;
     return (float)__builtin_sqrt(dx * dx + dy * dy);
 }
+
+#ifdef __HIP_DEVICE_COMPILE__
+// hypotf_glibc on the device without the sqrt's denormal scaling and class branches: S = x^2 +
+// y^2 of finite f32 values is 0 or at least 2^-298 (far above the 2^-767 where the compiler's
+// correctly rounded sqrt rescales), so v_rsq_f64 + the same Newton steps give its bits; S = 0
+// gives +0. dx * dx is exact in double, so fma(dx, dx, dy * dy) is dx * dx + dy * dy rounded
+// once. (scripts/probes/hypot_probe.hip: equal to __builtin_sqrt on 2^24 random pairs.)
+__device__ inline __attribute__((always_inline)) float hypotf_cr(float x, float y) {
+    const double dx = (double)x, dy = (double)y;
+    const double S = __builtin_fma(dx, dx, dy * dy);
+    const double y0 = __builtin_amdgcn_rsq(S);
+    double g = S * y0, h = 0.5 * y0;
+    const double r = __builtin_fma(-h, g, 0.5);
+    g = __builtin_fma(g, r, g);
+    h = __builtin_fma(h, r, h);
+    double d = __builtin_fma(-g, g, S);
+    g = __builtin_fma(d, h, g);
+    d = __builtin_fma(-g, g, S);
+    g = __builtin_fma(d, h, g);
+    const float f = (float)g;
+    return S == 0.0 ? 0.0f : f;
+}
+#elif defined(__HIPCC__)
+__host__ inline float hypotf_cr(float x, float y) { return hypotf_glibc(x, y); }  // (host pass)
+#endif
 
 }  // namespace exact
 }  // namespace thesia

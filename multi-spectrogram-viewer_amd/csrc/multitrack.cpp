@@ -110,7 +110,6 @@ int MultiTrack::add_tracks(const std::vector<uint64_t>& ids, const std::vector<P
     std::map<uint32_t, std::vector<size_t>> by_sr;
     for (size_t i = 0; i < nt.size(); ++i) by_sr[nt[i].sr].push_back(i);
     std::map<uint32_t, std::unique_ptr<Plan>> new_plans;
-    std::vector<std::unique_ptr<DevBuf>> raws;  // upload staging, freed after the sync
     struct Group {
         std::unique_ptr<Batch> batch;
         std::vector<uint64_t> off, len;
@@ -119,6 +118,7 @@ int MultiTrack::add_tracks(const std::vector<uint64_t>& ids, const std::vector<P
         std::vector<size_t> idx;
     };
     std::vector<Group> groups;
+    std::vector<std::unique_ptr<DevBuf>> big_raws;  // uploads of calls beyond kStageKeep
     for (auto& [sr, idx] : by_sr) {
         Plan* plan = nullptr;
         auto pit = plans_.find(sr);
@@ -142,12 +142,15 @@ int MultiTrack::add_tracks(const std::vector<uint64_t>& ids, const std::vector<P
             wf += (nt[idx[k]].n + 63) & ~uint64_t(63);
             T_all += stft_n_frames(nt[idx[k]].n, nt[idx[k]].win, nt[idx[k]].hop);
         }
-        raws.push_back(std::make_unique<DevBuf>());
-        DevBuf& raw = *raws.back();
+        // the upload scratch is the handle's, grow-only (a hipFree synchronises and costs
+        // ~0.16 ms); a later group's copies are ordered behind this group's decodes on s
+        // (a call larger than kStageKeep gets a scratch of its own, freed after the call's sync)
+        if (rb > kStageKeep) big_raws.push_back(std::make_unique<DevBuf>());
+        DevBuf& raw = rb > kStageKeep ? *big_raws.back() : raw_;
         auto wav = std::make_shared<DevBuf>();
         auto spec = std::make_shared<DevBuf>();
         g.bins = plan->row_bins();
-        int rc = raw.alloc(std::max<uint64_t>(rb, 1));
+        int rc = raw.bytes >= rb && raw.p ? 0 : raw.alloc(std::max<uint64_t>(rb, 1));
         if (!rc) rc = wav->alloc(std::max<uint64_t>(wf, 1) * sizeof(float));
         if (!rc) rc = spec->alloc(std::max<uint64_t>(T_all * g.bins, 1) * sizeof(float));
         if (rc) return rc;
@@ -214,7 +217,6 @@ int MultiTrack::add_tracks(const std::vector<uint64_t>& ids, const std::vector<P
         hipError_t e = hipStreamSynchronize(s);
         if (e != hipSuccess) return set_error(THESIA_ERR_DEVICE, hipGetErrorString(e));
     }
-    raws.clear();
     // 3) per-track max / min (lib.rs:197-200; a NaN makes ndarray-stats return Err -> +-inf):
     //    one launch over every group
     {

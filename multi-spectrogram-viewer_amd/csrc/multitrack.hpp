@@ -105,6 +105,7 @@ class MultiTrack {
     uint64_t id_max_sec_ = 0;
     uint32_t max_sr_ = 0;
     DevBuf img_;  // image scratch (grow-only)
+    DevBuf raw_;  // add_tracks' upload scratch (grow-only: no hipMalloc / hipFree per call)
     uint8_t* stage_ = nullptr;  // hipHostMalloc'd, stage_bytes_
     size_t stage_bytes_ = 0;
 };

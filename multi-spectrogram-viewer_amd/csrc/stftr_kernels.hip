@@ -124,9 +124,12 @@ __device__ __forceinline__ float2 bsel2(unsigned m, float2 a, float2 b) {
     return make_float2(bsel(m, a.x, b.x), bsel(m, a.y, b.y));
 }
 
-// decibel.rs:49-55 (ref 1: log_ref = 0) then the factor pass (:65 / :75), glibc log10f
+// decibel.rs:49-55 (ref 1: log_ref = 0) then the factor pass (:65 / :75), glibc log10f. Branch-free:
+// log10f_normal runs on max(x, amin) (amin = 1e-18 / 1e-36, normal floats; the log of x > amin is
+// glibc's, the other branch is the plan's log_amin) and the select keeps the reference's order.
 __device__ __forceinline__ float rdb(float x, float log_amin, float amin, float factor) {
-    const float y = x > amin ? exact::log10f_glibc(x) - 0.0f : log_amin - 0.0f;
+    const float l = exact::log10f_normal(x > amin ? x : amin);
+    const float y = x > amin ? l - 0.0f : log_amin - 0.0f;
     return factor * y;
 }
 
@@ -186,9 +189,10 @@ __device__ __forceinline__ void melr_stream(const int4* meta, const float4* wt, 
 
 }  // namespace
 
-// OK: 0 complex, 1 linear kinds, 2 mel kinds. C: 1 mono, 2 stereo (interleaved); INF: f32 / s16.
-// WV waves per block (one block per CU): 12 (3 waves per SIMD) or 8.
-template <int OK, int C, int INF, int WV>
+// KIND: the output kind (kernels.hpp OUT_*), a template parameter so every path is straight-line
+// code. C: 1 mono, 2 stereo (interleaved); INF: f32 / s16. WV waves per block (one block per CU):
+// 12 (3 waves per SIMD) or 8 (when the mel tables leave no room for 12 regions).
+template <int KIND, int C, int INF, int WV>
 __global__ void __launch_bounds__(64 * WV)
 stftr_kernel(StftLaunch a, uint64_t fps) {
     using G = GeoR;
@@ -196,15 +200,16 @@ stftr_kernel(StftLaunch a, uint64_t fps) {
     using CT = typename CK::T;
     using ET = typename std::conditional<INF == IN_S16, int16_t, float>::type;
     constexpr int NC = G::NC, P = G::P, L = G::L, F = G::F, SH = G::SH, KEEP = G::KEEP, RS = G::RS;
+    constexpr bool MEL = KIND == OUT_MEL || KIND == OUT_MEL_AMP_DB;
+    constexpr bool CPLX = KIND == OUT_COMPLEX;
 
     extern __shared__ __attribute__((aligned(16))) float lds[];
     float* wtl = lds;
     float2* twl = reinterpret_cast<float2*>(lds + G::WL_FLOATS);
     float2* scl = reinterpret_cast<float2*>(lds + G::WL_FLOATS + G::TW_FLOATS);
     float* work = lds + G::TAB_FLOATS;
-    const bool mel = OK == 2;
     int4* pm_lds = reinterpret_cast<int4*>(work + WV * G::REGION);
-    float4* pw_lds = reinterpret_cast<float4*>(pm_lds + (mel ? (a.melr_chunks + 2) * L : 0));
+    float4* pw_lds = reinterpret_cast<float4*>(pm_lds + (MEL ? (a.melr_chunks + 2) * L : 0));
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     constexpr int kBlock = 64 * WV;
 
@@ -217,22 +222,12 @@ stftr_kernel(StftLaunch a, uint64_t fps) {
         scl[i] = a.sincos[i];
     }
     if (threadIdx.x == 0) scl[NC] = make_float2(0.f, 0.f);
-    if constexpr (OK == 2) {
+    if constexpr (MEL) {
         for (int i = threadIdx.x; i < (a.melr_chunks + 2) * L; i += kBlock) pm_lds[i] = a.melr_meta[i];
         const int nw = (a.melr_chunks + 1) * a.melr_steps * L;
         for (int i = threadIdx.x; i < nw; i += kBlock) pw_lds[i] = a.melr_wt[i];
     }
     __syncthreads();
-
-    // lane roles: the column this lane holds after the transpose (partner column 64 - c is lane
-    // +- 32), the row it writes in the transpose, its digit d0 after the swap
-    const int col = lane <= 32 ? lane : 96 - lane;
-    const bool lane0 = lane == 0;
-    const unsigned m_lo = lane < 32 ? ~0u : 0u, m_sp = (lane & 31) == 0 ? ~0u : 0u, m_l0 = lane0 ? ~0u : 0u;
-    const int wrow = ((lane >> 2) & 3) + 4 * (lane & 3);  // d3 + 4 d4
-    const int d0s = lane >> 4;                             // d0 after the swap
-    // level-3 twiddles: tw[c t 4], t = 1..3 (fixed per lane)
-    const float2 w3a = twl[col * 4], w3b = twl[col * 8], w3c = twl[col * 12];
 
     const uint64_t total = a.total_frames;
     const uint64_t stream = (uint64_t)blockIdx.x * WV + wave;
@@ -251,6 +246,8 @@ stftr_kernel(StftLaunch a, uint64_t fps) {
     for (uint64_t it = 0; it < fps; ++it) {  // wave-uniform trip count
         const uint64_t g = g0 + it;
         const bool valid = g < g1;
+        // the lane index opaque per frame: the per-lane table addresses are formed in the loop
+        // instead of held across it in registers
         int lj = lane;
         asm volatile("" : "+v"(lj));
         int64_t start = 0;
@@ -329,18 +326,22 @@ stftr_kernel(StftLaunch a, uint64_t fps) {
 #pragma unroll
         for (int q = 0; q < 8; ++q) pl32(v[q], v[q + 8]);
         // ---- level 2: butterfly_4 over d2 (registers d1 + 4 d2), j = d0 + 4 d1 ----
-#pragma unroll
-        for (int d1 = 0; d1 < 4; ++d1) {
-            const int j = d0s + 4 * d1;
-            rbfly(v[d1], v[d1 + 4], v[d1 + 8], v[d1 + 12], twl[16 * j], twl[32 * j], twl[48 * j]);
-        }
-        // ---- LDS transpose: row d3 + 4 d4, column d0 + 4 n'; read column col ----
-        wave_lds_sync();
         {
+            const int d0s = lj >> 4;  // d0 after the swap
+#pragma unroll
+            for (int d1 = 0; d1 < 4; ++d1) {
+                const int j = d0s + 4 * d1;
+                rbfly(v[d1], v[d1 + 4], v[d1 + 8], v[d1 + 12], twl[16 * j], twl[32 * j], twl[48 * j]);
+            }
+            // ---- LDS transpose: row d3 + 4 d4, column d0 + 4 n'; read column col ----
+            wave_lds_sync();
+            const int wrow = ((lj >> 2) & 3) + 4 * (lj & 3);
             float2* wb = reinterpret_cast<float2*>(region + wrow * RS) + d0s;
 #pragma unroll
             for (int q = 0; q < P; ++q) wb[4 * q] = v[q];
         }
+        // the lane's column after the transpose: its partner column 64 - col is lane +- 32
+        const int col = lj <= 32 ? lj : 96 - lj;
         wave_lds_sync();
         {
             const float2* rb = reinterpret_cast<const float2*>(region) + col;
@@ -348,28 +349,32 @@ stftr_kernel(StftLaunch a, uint64_t fps) {
             for (int r = 0; r < P; ++r) v[r] = rb[r * (RS / 2)];
         }
         // ---- level 3: butterfly_4 over d3 (registers d3 + 4 d4), j = col ----
+        {
+            const float2 w3a = twl[col * 4], w3b = twl[col * 8], w3c = twl[col * 12];
 #pragma unroll
-        for (int d4 = 0; d4 < 4; ++d4) rbfly(v[4 * d4], v[4 * d4 + 1], v[4 * d4 + 2], v[4 * d4 + 3], w3a, w3b, w3c);
+            for (int d4 = 0; d4 < 4; ++d4)
+                rbfly(v[4 * d4], v[4 * d4 + 1], v[4 * d4 + 2], v[4 * d4 + 3], w3a, w3b, w3c);
+        }
         // ---- level 4: butterfly_4 over d4, j = col + 64 d3 ----
 #pragma unroll
         for (int d3 = 0; d3 < 4; ++d3) {
             const int j = col + 64 * d3;
             rbfly(v[d3], v[d3 + 4], v[d3 + 8], v[d3 + 12], twl[j], twl[2 * j], twl[3 * j]);
         }
-        // v[r] = Z[col + 64 r]. ---- the partner column's Z[8 .. 15] (lanes +- 32) ----
+        // v[r] = Z[col + 64 r]. ---- untangle (realfft.rs:142-157) on pairs (k, NC - k) ----
+        // the partner column's Z[8 .. 15] by one v_permlane32_swap per dword (lanes < 32 receive
+        // into the second operand, lanes >= 32 into the first); lanes 0 and 32 pair inside their
+        // own column. Partner of own register r < 8: general and lane 32: Z_partner[15 - r]
+        // (= pr[7 - r]); lane 0: Z[(16 - r) & 15] = r == 0 ? v[0] : pr[8 - r]
+        const unsigned m_lo = lj < 32 ? ~0u : 0u, m_sp = (lj & 31) == 0 ? ~0u : 0u, m_l0 = lj == 0 ? ~0u : 0u;
         float2 pr[8];
 #pragma unroll
         for (int i = 0; i < 8; ++i) {
             float2 x = v[8 + i], y = v[8 + i];
             pl32(x, y);
-            // lanes < 32 receive into y, lanes >= 32 into x; lanes 0 and 32 keep their own
             pr[i] = bsel2(m_sp, v[8 + i], bsel2(m_lo, y, x));
         }
-        // partner of own register r (r < 8): general and lane 32: pr[7 - r] (= Z_partner[15 - r]);
-        // lane 0: Z[(16 - r) & 15] = r == 0 ? v[0] : pr[8 - r]
         wave_lds_sync();  // the transpose's reads are done: the region takes the output row
-        auto sc_at = [&](int k) { return scl[k]; };
-        // realfft.rs:142-156 for bins k (own) and NC - k (partner), the 1/2 last
         auto pair = [&](float2 b, float2 rr, float2 sck, float2 sckp, float2& xk, float2& xkp) {
             const float sre = b.x + rr.x, sim = b.y + rr.y;
             const float dre = b.x - rr.x, dim = b.y - rr.y;
@@ -380,44 +385,44 @@ stftr_kernel(StftLaunch a, uint64_t fps) {
             xkp.y = 0.5f * (((-dim) - sckp.x * sim) - sckp.y * (-dre));
         };
         float* row = region;
-        const int sh = OK == 2 ? 0
-                     : (int)((reinterpret_cast<uintptr_t>(static_cast<float*>(a.out) + g * (uint64_t)(OK == 0 ? 2 * F : F)) >> 2) & 3);
+        const int sh = MEL ? 0
+                     : (int)((reinterpret_cast<uintptr_t>(static_cast<float*>(a.out) + g * (uint64_t)(CPLX ? 2 * F : F)) >> 2) & 3);
         auto emit = [&](int k, float2 x) {
-            if constexpr (OK == 0) {
+            if constexpr (CPLX) {
                 *reinterpret_cast<float2*>(row + sh + 2 * k) = x;
             } else {
-                const int kind = a.out_kind;
                 float val;
-                if (kind == OUT_POWER || kind == OUT_POWER_DB) {
+                if constexpr (KIND == OUT_POWER || KIND == OUT_POWER_DB) {
                     val = x.x * x.x + x.y * x.y;  // num-complex norm_sqr
-                    if (kind == OUT_POWER_DB) val = rdb(val, a.log_amin, 1e-36f, 10.0f);
+                    if constexpr (KIND == OUT_POWER_DB) val = rdb(val, a.log_amin, 1e-36f, 10.0f);
                 } else {
-                    val = exact::hypotf_glibc(x.x, x.y);  // num-complex norm (lib.rs:124)
-                    if (kind == OUT_AMP_DB) val = rdb(val, a.log_amin, 1e-18f, 20.0f);
+                    val = exact::hypotf_cr(x.x, x.y);  // num-complex norm (lib.rs:124)
+                    if constexpr (KIND == OUT_AMP_DB) val = rdb(val, a.log_amin, 1e-18f, 20.0f);
                 }
                 row[sh + k] = val;
             }
         };
+        const float2* scc = scl + col;              // sin_cos of bins col + 64 r
+        const float2* scp = scl + (NC - 448 - col);  // ... of NC - col - 64 r = scp[64 (7 - r)]
 #pragma unroll
         for (int r = 0; r < 8; ++r) {
             const int k = col + 64 * r;
             const float2 rr = bsel2(m_l0, r == 0 ? v[0] : pr[8 - r], pr[7 - r]);
-            const int kp = NC - k;  // lane 0, r = 0: bin NC (set below)
             float2 xk, xkp;
-            pair(v[r], rr, sc_at(k), sc_at(kp), xk, xkp);
+            pair(v[r], rr, scc[64 * r], scp[64 * (7 - r)], xk, xkp);
             if (r == 0) xkp = bsel2(m_l0, make_float2(v[0].x - v[0].y, 0.0f), xkp);  // realfft.rs:157
             emit(k, xk);
-            emit(kp, xkp);
+            emit(NC - k, xkp);  // (lane 0, r = 0: bin NC)
         }
         {  // lane 0: bin NC / 2 pairs with itself (realfft.rs:142-156 with b = r = Z[NC/2])
             float2 xk, xkp;
-            pair(v[8], v[8], sc_at(NC / 2), sc_at(NC / 2), xk, xkp);
-            if (lane0) emit(NC / 2, xk);
+            pair(v[8], v[8], scl[NC / 2], scl[NC / 2], xk, xkp);
+            if (lj == 0) emit(NC / 2, xk);
         }
         wave_lds_sync();
-        if constexpr (OK == 2) {
+        if constexpr (MEL) {
             // lib.rs:131 (the packed stream) then amp dB (decibel.rs:79-88)
-            if (lane0) {
+            if (lj == 0) {
 #pragma unroll
                 for (int k = F; k < kMelpOut; ++k) row[k] = 0.0f;
             }
@@ -426,14 +431,13 @@ stftr_kernel(StftLaunch a, uint64_t fps) {
             else melr_stream<3>(pm_lds, pw_lds, region, lj, a.melr_chunks);
             wave_lds_sync();
             const int n_mels = a.n_mels;
-            const bool db = a.out_kind == OUT_MEL_AMP_DB;
             float* out = static_cast<float*>(a.out) + g * (uint64_t)n_mels;
             for (int m = lj; m < n_mels; m += L) {
                 const float x = region[kMelpOut + m];
-                if (valid) out[m] = db ? rdb(x, a.log_amin, 1e-18f, 20.0f) : x;
+                if (valid) out[m] = KIND == OUT_MEL_AMP_DB ? rdb(x, a.log_amin, 1e-18f, 20.0f) : x;
             }
         } else {
-            constexpr int nfl = OK == 0 ? 2 * F : F;
+            constexpr int nfl = CPLX ? 2 * F : F;
             float* frow = static_cast<float*>(a.out) + g * (uint64_t)nfl;
             if (valid) store_row_b128<L>(frow, sh, region, nfl, lj);
         }
@@ -449,11 +453,11 @@ static int ldsr_bytes(const StftLaunch& a, int wv) {
     return (GeoR::TAB_FLOATS + wv * GeoR::REGION) * 4 + meltab;
 }
 
-template <int OK, int C, int INF, int WV>
+template <int KIND, int C, int INF, int WV>
 static int launchr_k(const StftLaunch& a, hipStream_t s) {
     const int lds = ldsr_bytes(a, WV);
     if (lds > 163840) return -2;
-    auto kern = stftr_kernel<OK, C, INF, WV>;
+    auto kern = stftr_kernel<KIND, C, INF, WV>;
     if (hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize, lds) !=
         hipSuccess)
         return -1;
@@ -467,20 +471,29 @@ static int launchr_k(const StftLaunch& a, hipStream_t s) {
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
-template <int OK, int C, int INF>
+// the spectrum kinds always fit 12 regions (125 KiB); the mel kinds fall back to 8 when their
+// tables leave no room
+template <int KIND, int C, int INF>
 static int launchr_w(const StftLaunch& a, hipStream_t s) {
-    if (ldsr_bytes(a, 12) <= 163840) return launchr_k<OK, C, INF, 12>(a, s);
-    return launchr_k<OK, C, INF, 8>(a, s);
+    if constexpr (KIND == OUT_MEL || KIND == OUT_MEL_AMP_DB) {
+        if (a.melr_chunks <= 0) return -2;
+        if (ldsr_bytes(a, 12) > 163840) return launchr_k<KIND, C, INF, 8>(a, s);
+    }
+    return launchr_k<KIND, C, INF, 12>(a, s);
 }
 
 template <int C, int INF>
 static int launchr_c(const StftLaunch& a, hipStream_t s) {
-    if (a.out_kind == OUT_COMPLEX) return launchr_w<0, C, INF>(a, s);
-    if (a.out_kind == OUT_MEL || a.out_kind == OUT_MEL_AMP_DB) {
-        if (a.melr_chunks <= 0) return -2;
-        return launchr_w<2, C, INF>(a, s);
+    switch (a.out_kind) {
+        case OUT_COMPLEX: return launchr_w<OUT_COMPLEX, C, INF>(a, s);
+        case OUT_MAG: return launchr_w<OUT_MAG, C, INF>(a, s);
+        case OUT_POWER: return launchr_w<OUT_POWER, C, INF>(a, s);
+        case OUT_AMP_DB: return launchr_w<OUT_AMP_DB, C, INF>(a, s);
+        case OUT_POWER_DB: return launchr_w<OUT_POWER_DB, C, INF>(a, s);
+        case OUT_MEL: return launchr_w<OUT_MEL, C, INF>(a, s);
+        case OUT_MEL_AMP_DB: return launchr_w<OUT_MEL_AMP_DB, C, INF>(a, s);
+        default: return -2;
     }
-    return launchr_w<1, C, INF>(a, s);
 }
 
 bool stftr_supports(int n_fft, int win, int hop, int in_format, int channels) {

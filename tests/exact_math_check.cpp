@@ -10,13 +10,16 @@
 
 int main(int argc, char** argv) {
     const unsigned stride = argc > 1 ? (unsigned)atoi(argv[1]) : 1;
-    long n = 0, bad_log = 0, bad_log10 = 0, bad_hyp = 0;
+    long n = 0, bad_log = 0, bad_log10 = 0, bad_hyp = 0, bad_norm = 0;
     for (unsigned long u = 1; u < 0x7f800000ul; u += stride) {
         float x;
         const unsigned v = (unsigned)u;
         memcpy(&x, &v, 4);
         if (thesia::exact::f32_bits(logf(x)) != thesia::exact::f32_bits(thesia::exact::logf_glibc(x))) ++bad_log;
         if (thesia::exact::f32_bits(log10f(x)) != thesia::exact::f32_bits(thesia::exact::log10f_glibc(x))) ++bad_log10;
+        if (v >= 0x00800000u &&
+            thesia::exact::f32_bits(log10f(x)) != thesia::exact::f32_bits(thesia::exact::log10f_normal(x)))
+            ++bad_norm;  // the branch-free form, normal floats
         ++n;
     }
     unsigned s = 12345u;
@@ -31,6 +34,6 @@ int main(int argc, char** argv) {
         memcpy(&y, &b, 4);
         if (thesia::exact::f32_bits(hypotf(x, y)) != thesia::exact::f32_bits(thesia::exact::hypotf_glibc(x, y))) ++bad_hyp;
     }
-    printf("%ld %ld %ld %ld\n", n, bad_log, bad_log10, bad_hyp);
+    printf("%ld %ld %ld %ld %ld\n", n, bad_log, bad_log10, bad_hyp, bad_norm);
     return 0;
 }
