@@ -37,6 +37,7 @@
 #include "stft3_core.hpp"
 
 #include <type_traits>
+#include <cstdlib>
 
 namespace thesia {
 
@@ -191,8 +192,10 @@ __device__ __forceinline__ void melr_stream(const int4* meta, const float4* wt, 
 
 // KIND: the output kind (kernels.hpp OUT_*), a template parameter so every path is straight-line
 // code. C: 1 mono, 2 stereo (interleaved); INF: f32 / s16. WV waves per block (one block per CU):
-// 12 (3 waves per SIMD) or 8 (when the mel tables leave no room for 12 regions).
-template <int KIND, int C, int INF, int WV>
+// 12 (3 waves per SIMD) or 8 (when the mel tables leave no room for 12 regions). VAR: ablations
+// of the experiment library only (wrong output by design): 1 |X| by the f32 sqrt, 2 no mel
+// stream, 4 no untangle / |X| / mel (the FFT alone).
+template <int KIND, int C, int INF, int WV, int VAR = 0>
 __global__ void __launch_bounds__(64 * WV)
 stftr_kernel(StftLaunch a, uint64_t fps) {
     using G = GeoR;
@@ -396,7 +399,8 @@ stftr_kernel(StftLaunch a, uint64_t fps) {
                     val = x.x * x.x + x.y * x.y;  // num-complex norm_sqr
                     if constexpr (KIND == OUT_POWER_DB) val = rdb(val, a.log_amin, 1e-36f, 10.0f);
                 } else {
-                    val = exact::hypotf_cr(x.x, x.y);  // num-complex norm (lib.rs:124)
+                    if constexpr ((VAR & 1) != 0) val = __builtin_amdgcn_sqrtf(x.x * x.x + x.y * x.y);
+                    else val = exact::hypotf_cr(x.x, x.y);  // num-complex norm (lib.rs:124)
                     if constexpr (KIND == OUT_AMP_DB) val = rdb(val, a.log_amin, 1e-18f, 20.0f);
                 }
                 row[sh + k] = val;
@@ -405,7 +409,7 @@ stftr_kernel(StftLaunch a, uint64_t fps) {
         const float2* scc = scl + col;              // sin_cos of bins col + 64 r
         const float2* scp = scl + (NC - 448 - col);  // ... of NC - col - 64 r = scp[64 (7 - r)]
 #pragma unroll
-        for (int r = 0; r < 8; ++r) {
+        for (int r = 0; r < ((VAR & 4) != 0 ? 0 : 8); ++r) {
             const int k = col + 64 * r;
             const float2 rr = bsel2(m_l0, r == 0 ? v[0] : pr[8 - r], pr[7 - r]);
             float2 xk, xkp;
@@ -427,8 +431,10 @@ stftr_kernel(StftLaunch a, uint64_t fps) {
                 for (int k = F; k < kMelpOut; ++k) row[k] = 0.0f;
             }
             wave_lds_sync();
-            if (a.melr_steps == 2) melr_stream<2>(pm_lds, pw_lds, region, lj, a.melr_chunks);
-            else melr_stream<3>(pm_lds, pw_lds, region, lj, a.melr_chunks);
+            if constexpr ((VAR & 6) == 0) {
+                if (a.melr_steps == 2) melr_stream<2>(pm_lds, pw_lds, region, lj, a.melr_chunks);
+                else melr_stream<3>(pm_lds, pw_lds, region, lj, a.melr_chunks);
+            }
             wave_lds_sync();
             const int n_mels = a.n_mels;
             float* out = static_cast<float*>(a.out) + g * (uint64_t)n_mels;
@@ -453,11 +459,21 @@ static int ldsr_bytes(const StftLaunch& a, int wv) {
     return (GeoR::TAB_FLOATS + wv * GeoR::REGION) * 4 + meltab;
 }
 
-template <int KIND, int C, int INF, int WV>
+template <int KIND, int C, int INF, int WV, int VAR = 0>
 static int launchr_k(const StftLaunch& a, hipStream_t s) {
+#ifdef THESIA_EXPERIMENTS
+    if constexpr (VAR == 0 && KIND == OUT_MEL_AMP_DB && C == 2 && INF == IN_F32 && WV == 12) {
+        const char* e = getenv("THESIA_STFT_VARIANT");
+        const int v = e ? atoi(e) : 0;
+        if (v == 1) return launchr_k<KIND, C, INF, WV, 1>(a, s);
+        if (v == 2) return launchr_k<KIND, C, INF, WV, 2>(a, s);
+        if (v == 4) return launchr_k<KIND, C, INF, WV, 4>(a, s);
+        if (v == 3) return launchr_k<KIND, C, INF, WV, 3>(a, s);
+    }
+#endif
     const int lds = ldsr_bytes(a, WV);
     if (lds > 163840) return -2;
-    auto kern = stftr_kernel<KIND, C, INF, WV>;
+    auto kern = stftr_kernel<KIND, C, INF, WV, VAR>;
     if (hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize, lds) !=
         hipSuccess)
         return -1;
