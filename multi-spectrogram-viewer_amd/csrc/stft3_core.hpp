@@ -15,7 +15,21 @@ struct Geo3 {
     static constexpr int L = G2::L, P = G2::P, FPW = G2::FPW;
     // the wide (ds_read_b128) transpose for the headline size, L = 32 (fft2 WIDE)
     static constexpr bool WIDE = L == 32;
-    static constexpr int RS = WIDE ? (P * fft2_stride<NC>(true) + 3) / 4 * 4 : G2::RS;
+    // Per-frame region stride and slot offset (gfx950 banking, MI355X_MICROARCH.md LDS table).
+    // The narrow transpose writes a frame's L lanes as ds_write_b32 (32-lane groups, bank = dword
+    // mod 32) and reads them back as ds_read2_b64 (16-lane groups, 2 dwords each, mod 32). With
+    // L = 16 the two frames of a 32-lane group must sit 16 banks apart (stride = 16 mod 32); with
+    // L = 8 the four frames must take bank offsets {0, 16, 8, 24} (writes) while the two frames
+    // of a 16-lane read group sit 16 apart (row stride L + 2 = 10 fills the other 16 even banks):
+    // stride = 16 mod 32 and 8 more floats for slots 2, 3 mod 4. (The previous strides, = 0 mod
+    // 32 for L = 16 and without the slot offset for L = 8, put every transpose write at 2-way.)
+    static constexpr bool SWZ8 = !WIDE && L == 8;
+    static constexpr int SWZ_MAX = SWZ8 ? 8 : 0;
+    __host__ __device__ static constexpr int swz(int slot) { return SWZ8 ? 8 * ((slot >> 1) & 1) : 0; }
+    static constexpr bool BANKED = !WIDE && (L == 8 || L == 16);
+    static constexpr int stride_for(int need) { return BANKED ? round_to_mod32(need + SWZ_MAX, 16) : need; }
+    static constexpr int RS = WIDE ? (P * fft2_stride<NC>(true) + 3) / 4 * 4
+                                   : BANKED ? stride_for(G2::XREG > G2::F4 ? G2::XREG : G2::F4) : G2::RS;
     static constexpr int SH = P / 4;                      // points per lane a hop moves
     static constexpr int BLOCK = 64 * WV;
     static constexpr int STREAMS = WV * FPW;              // streams (= frames in flight) per block
@@ -30,10 +44,14 @@ struct Geo3 {
     static constexpr int ROW_FLOATS_OK(int ok) { return ok == 0 ? 2 * G2::F : G2::F; }
     // (+32: a row staged from its 128-byte line start, line_rows, is up to 31 floats in)
     static constexpr int RS_OK(bool staged, int ok) {
-        return !staged ? RS : (RS > (ROW_FLOATS_OK(ok) + 32 + 3) / 4 * 4 ? RS : (ROW_FLOATS_OK(ok) + 32 + 3) / 4 * 4);
+        return !staged ? RS
+               : (RS >= (ROW_FLOATS_OK(ok) + 32 + 3) / 4 * 4 + SWZ_MAX ? RS
+                                                                      : stride_for((ROW_FLOATS_OK(ok) + 32 + 3) / 4 * 4));
     }
     static constexpr int BASE_FLOATS_OK(bool staged, int ok) { return WL_FLOATS + TW_FLOATS + STREAMS * RS_OK(staged, ok); }
     static_assert(P % 4 == 0, "hop = n_fft/4 must move whole points per lane");
+    static_assert(RS % 4 == 0 && SWZ_MAX % 4 == 0, "16-byte aligned regions");
+    static_assert(RS >= G2::XREG + SWZ_MAX && RS >= G2::F4 + SWZ_MAX, "a slot's offset region stays in its stride");
 };
 
 // Which kinds stage their output row (measured): linear kinds yes (power dB 6.25

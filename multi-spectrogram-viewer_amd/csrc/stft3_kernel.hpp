@@ -105,7 +105,7 @@ stft3_kernel(StftLaunch a, uint64_t fps) {
     const uint64_t gpar = ODD ? (stream & 1) : 0;
     const int hop = a.hop;
     const int hop_s = ODD ? 2 * hop : hop;  // samples between a stream's frames
-    float* region = work + (wave * FPW + slot) * G3::RS_OK(stage_rows(OK, VAR), OK);
+    float* region = work + (wave * FPW + slot) * G3::RS_OK(stage_rows(OK, VAR), OK) + G3::swz(slot);
     const ET* in = static_cast<const ET*>(a.in);
 
     float2 raw[P];
