@@ -28,35 +28,101 @@ const char* last_error() { return g_err.c_str(); }
 // ------------------------------------------------------------------------------------
 // device buffers / streams
 // ------------------------------------------------------------------------------------
+// The library's block cache (round 5). Rounds 3-4 used a stream-ordered memory pool
+// (hipMemPoolCreate + hipMallocFromPoolAsync / hipFreeAsync) so that add_tracks paid no hipFree
+// (each one synchronises the device: ~160 us, profiles/r03_viewer). On this runtime (ROCm 7.2)
+// kernel writes into pool blocks past the first ~32-64 MiB of a call's allocations were lost
+// (MultiTrack greys of a 16-track call read back as zeros, the images as garbage, an illegal
+// memory access once; scripts/diag_mt_grey5.py), so blocks now come from plain
+// hipMalloc and freed ones are kept here for reuse, keyed by device and size class:
+//   * a block is handed out again only on the stream it was released on (in-order behind the
+//     work that used it) or once an event recorded at its release has completed -- the same
+//     stream-ordering contract as hipFreeAsync;
+//   * classes are 2^k and 3 * 2^(k-2) (<= 33 % slack) up to 64 MiB, whole 2 MiB steps above;
+//   * the cache holds at most kCacheCap bytes per device (a release past it is a hipFree) and
+//     is emptied by trim_pool() (thesia_pool_trim, MultiTrack destruction, and before a failed
+//     hipMalloc is retried).
+namespace {
+struct CachedBlock {
+    void* p;
+    size_t cap;
+    hipStream_t st;
+    hipEvent_t ev;
+};
+struct DevCache {
+    std::vector<CachedBlock> free;
+    size_t cached = 0;  // bytes in free
+    size_t live = 0;    // bytes handed out
+};
+std::mutex g_cache_mu;
+std::map<int, DevCache> g_cache;
+constexpr size_t kCacheCap = size_t(4) << 30;
+
+size_t cache_class(size_t n) {
+    constexpr size_t kMin = 4096, kBig = size_t(64) << 20, kStep = size_t(2) << 20;
+    if (n <= kMin) return kMin;
+    if (n > kBig) return (n + kStep - 1) / kStep * kStep;
+    size_t b = kMin;
+    while (b < n) b <<= 1;  // 2^k >= n
+    return (b / 4) * 3 >= n ? (b / 4) * 3 : b;
+}
+
+int current_device() {
+    int d = 0;
+    if (hipGetDevice(&d) != hipSuccess) {
+        (void)hipGetLastError();
+        d = 0;
+    }
+    return d;
+}
+}  // namespace
+
 void DevBuf::release() {
-    if (p) (void)(pooled ? hipFreeAsync(p, st) : hipFree(p));
+    if (!p) return;
+    if (pooled) {
+        const size_t cap = cache_class(bytes);
+        std::lock_guard<std::mutex> g(g_cache_mu);
+        DevCache& c = g_cache[dev];
+        c.live -= cap;
+        hipEvent_t ev = nullptr;
+        if (c.cached + cap <= kCacheCap && hipEventCreateWithFlags(&ev, hipEventDisableTiming) == hipSuccess &&
+            hipEventRecord(ev, st) == hipSuccess) {
+            c.free.push_back(CachedBlock{p, cap, st, ev});
+            c.cached += cap;
+        } else {
+            (void)hipGetLastError();
+            if (ev) (void)hipEventDestroy(ev);
+            (void)hipFree(p);
+        }
+    } else {
+        (void)hipFree(p);
+    }
     p = nullptr;
     bytes = 0;
 }
 
-// The library's stream-ordered memory pool (rounds 3-4: hipMemPoolCreate + hipMallocFromPoolAsync /
-// hipFreeAsync on the library stream, so add_tracks paid no hipFree) is OFF: on this runtime
-// (ROCm 7.2) kernel writes into pool blocks past the first ~32-64 MiB of a call's allocations
-// were lost (MultiTrack greys of a 16-track call read back as zeros, the images as garbage, an
-// illegal memory access once), while the same calls with hipMalloc are exact
-// (scripts/diag_mt_grey5.py). DevBuf allocates with hipMalloc / hipFree;
-// trim_pool / pool_bytes stay as no-ops of the C ABI.
-static hipMemPool_t lib_pool() { return nullptr; }
-
 int trim_pool() {
-    hipMemPool_t pool = lib_pool();
-    if (!pool) return THESIA_OK;
-    // frees are stream-ordered on the library stream: let them complete first
-    THESIA_HIP(hipStreamSynchronize(default_stream()));
-    THESIA_HIP(hipMemPoolTrimTo(pool, 0));
+    std::lock_guard<std::mutex> g(g_cache_mu);
+    for (auto& kv : g_cache) {
+        for (CachedBlock& b : kv.second.free) {
+            (void)hipEventSynchronize(b.ev);
+            (void)hipEventDestroy(b.ev);
+            (void)hipFree(b.p);
+        }
+        kv.second.free.clear();
+        kv.second.cached = 0;
+    }
+    (void)hipGetLastError();
     return THESIA_OK;
 }
 
 int pool_bytes(uint64_t* reserved, uint64_t* used) {
+    std::lock_guard<std::mutex> g(g_cache_mu);
     uint64_t r = 0, u = 0;
-    if (hipMemPool_t pool = lib_pool()) {
-        THESIA_HIP(hipMemPoolGetAttribute(pool, hipMemPoolAttrReservedMemCurrent, &r));
-        THESIA_HIP(hipMemPoolGetAttribute(pool, hipMemPoolAttrUsedMemCurrent, &u));
+    auto it = g_cache.find(current_device());
+    if (it != g_cache.end()) {
+        u = it->second.live;
+        r = it->second.live + it->second.cached;
     }
     if (reserved) *reserved = r;
     if (used) *used = u;
@@ -67,26 +133,45 @@ int DevBuf::alloc(size_t n) {
     release();
     if (n == 0) n = 16;
     hipStream_t s = default_stream();
-    hipError_t e = hipErrorNotSupported;
-    hipMemPool_t pool = lib_pool();
-    if (pool) {
-        e = hipMallocFromPoolAsync(&p, n, pool, s);
-        if (e == hipErrorOutOfMemory || e == hipErrorMemoryAllocation) {
-            // the reserve of other sizes may be what is missing: hand it back and retry once
-            (void)hipGetLastError();
-            if (trim_pool() == THESIA_OK) e = hipMallocFromPoolAsync(&p, n, pool, s);
+    const int d = current_device();
+    const size_t cap = cache_class(n);
+    {
+        std::lock_guard<std::mutex> g(g_cache_mu);
+        DevCache& c = g_cache[d];
+        for (size_t i = c.free.size(); i-- > 0;) {  // the most recently released first
+            CachedBlock& b = c.free[i];
+            if (b.cap != cap) continue;
+            if (b.st != s) {
+                const hipError_t q = hipEventQuery(b.ev);
+                if (q != hipSuccess) {
+                    (void)hipGetLastError();
+                    continue;
+                }
+            }
+            p = b.p;
+            (void)hipEventDestroy(b.ev);
+            c.free.erase(c.free.begin() + (std::ptrdiff_t)i);
+            c.cached -= cap;
+            c.live += cap;
+            break;
         }
     }
-    pooled = e == hipSuccess;
-    if (!pooled) {
-        (void)hipGetLastError();
-        if (pool) (void)trim_pool();
-        e = hipMalloc(&p, n);
+    if (!p) {
+        hipError_t e = hipMalloc(&p, cap);
+        if (e == hipErrorOutOfMemory || e == hipErrorMemoryAllocation) {
+            // the cache's idle blocks may be what is missing: hand them back, retry once
+            (void)hipGetLastError();
+            if (trim_pool() == THESIA_OK) e = hipMalloc(&p, cap);
+        }
+        if (e != hipSuccess) {
+            p = nullptr;
+            return set_error(THESIA_ERR_DEVICE, std::string("hipMalloc: ") + hipGetErrorString(e));
+        }
+        std::lock_guard<std::mutex> g(g_cache_mu);
+        g_cache[d].live += cap;
     }
-    if (e != hipSuccess) {
-        p = nullptr;
-        return set_error(THESIA_ERR_DEVICE, std::string("hipMalloc: ") + hipGetErrorString(e));
-    }
+    pooled = true;
+    dev = d;
     st = s;
     bytes = n;
     return THESIA_OK;

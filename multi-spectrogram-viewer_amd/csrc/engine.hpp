@@ -28,27 +28,28 @@ const char* last_error();
     } while (0)
 
 // ---- device buffer (move-only RAII) ----
-// Stream-ordered on the library stream of the device it was made on (hipMallocFromPoolAsync /
-// hipFreeAsync from the library's own memory pool, which keeps freed blocks for reuse until
-// trim_pool()): a release is ordered after the work already enqueued there and costs no device
-// synchronisation (a hipFree took ~160 us each: 1.5 ms of a 4.4 ms MultiTrack add_tracks call,
-// profiles/r03_viewer). Falls back to hipMalloc / hipFree where pools are unavailable.
+// hipMalloc'd blocks kept by the library's block cache (engine.cpp) once released: a release is
+// stream-ordered on the library stream it was allocated on (an event, no device
+// synchronisation: a hipFree costs ~160 us, profiles/r03_viewer), and the block is handed out
+// again to the next allocation of its size class on that stream (or on any stream once the
+// event has completed).
 struct DevBuf {
     void* p = nullptr;
     size_t bytes = 0;
     hipStream_t st = nullptr;  // the stream its allocation (and so its release) is ordered on
-    bool pooled = false;
+    bool pooled = false;       // a block of the cache (else a plain hipFree on release)
+    int dev = 0;               // the device it was allocated on
     DevBuf() = default;
     DevBuf(const DevBuf&) = delete;
     DevBuf& operator=(const DevBuf&) = delete;
-    DevBuf(DevBuf&& o) noexcept : p(o.p), bytes(o.bytes), st(o.st), pooled(o.pooled) {
+    DevBuf(DevBuf&& o) noexcept : p(o.p), bytes(o.bytes), st(o.st), pooled(o.pooled), dev(o.dev) {
         o.p = nullptr;
         o.bytes = 0;
     }
     DevBuf& operator=(DevBuf&& o) noexcept {
         if (this != &o) {
             release();
-            p = o.p; bytes = o.bytes; st = o.st; pooled = o.pooled;
+            p = o.p; bytes = o.bytes; st = o.st; pooled = o.pooled; dev = o.dev;
             o.p = nullptr; o.bytes = 0;
         }
         return *this;
@@ -61,8 +62,8 @@ struct DevBuf {
 };
 
 hipStream_t default_stream();  // library stream of the current device
-// the library pool of the current device: hand its unused reserve back to the device (after the
-// library stream's frees complete); its reserved / in-use bytes
+// the block cache: hand every idle block back to the device (after the work ordered before
+// their release completes); the current device's cached + handed-out / handed-out bytes
 int trim_pool();
 int pool_bytes(uint64_t* reserved, uint64_t* used);
 hipError_t copy_ordered(void* dst, const void* src, size_t bytes, hipMemcpyKind kind);

@@ -146,11 +146,12 @@ def test_remove_frees_shared_pools():
     assert len(mt.get_spec_image(9, 100.0, 64)) == int(np.float32(100.0) * np.float32(len(pcm[9])) / np.float32(24000)) * 64 * 3
 
 
-def test_no_stream_ordered_pool(excerpts, tmp_path):
-    """Round 5: library buffers are plain hipMalloc allocations. The stream-ordered pool of
-    rounds 3-4 lost kernel writes past the first tens of MiB of a call's allocations on this
-    runtime (test_greys_of_a_many_track_call); thesia_pool_trim / thesia_pool_bytes remain in the
-    C ABI and report an empty pool."""
+def test_block_cache(excerpts, tmp_path):
+    """Round 5: library buffers are plain hipMalloc blocks (the stream-ordered pool of rounds 3-4
+    lost kernel writes past the first tens of MiB of a call's allocations on this runtime,
+    test_greys_of_a_many_track_call), kept for reuse by the library's block cache: a second
+    identical add_tracks reuses the first one's released blocks (no new reserve), the handle's
+    destruction leaves only idle blocks, and thesia_pool_trim hands them back."""
     import ctypes as C
     from thesia._lib import lib, check
     res, used = C.c_uint64(), C.c_uint64()
@@ -159,14 +160,28 @@ def test_no_stream_ordered_pool(excerpts, tmp_path):
         p = str(tmp_path / f"s_{t}.wav")
         _write_wav(p, *excerpts[t])
         paths.append(p)
+    check(lib.thesia_pool_trim())
+    check(lib.thesia_pool_bytes(C.byref(res), C.byref(used)))
+    base_used = used.value
     mt = thesia.MultiTrack()
     mt.add_tracks([0, 1], "\n".join(paths))
     check(lib.thesia_pool_bytes(C.byref(res), C.byref(used)))
-    assert res.value == 0 and used.value == 0
-    assert mt.device_bytes() > 0
+    assert used.value > base_used and res.value >= used.value
+    held = mt.device_bytes()
+    assert held > 0
+    g0 = [mt.get_grey(0).copy(), mt.get_grey(1).copy()]
+    mt.add_tracks([0, 1], "\n".join(paths))  # replaces both tracks: the same sizes again
+    check(lib.thesia_pool_bytes(C.byref(res2 := C.c_uint64()), C.byref(used2 := C.c_uint64())))
+    assert res2.value <= res.value + (64 << 20), (res.value, res2.value)
+    for i in range(2):
+        assert np.array_equal(mt.get_grey(i), g0[i]), i
     mt.remove_track(0)
     mt.close()
+    check(lib.thesia_pool_bytes(C.byref(res), C.byref(used)))
+    assert used.value == base_used
     check(lib.thesia_pool_trim())
+    check(lib.thesia_pool_bytes(C.byref(res), C.byref(used)))
+    assert res.value == used.value == base_used
 
 
 @pytest.mark.parametrize("fast", [False, True])
