@@ -879,8 +879,9 @@ int batch_create(Plan* plan, const thesia_batch_desc& d, Batch** out) {
         b->apply_mel_path();
     }
     b->k5_ok = k5_geo && stft5_lds_bytes(L) <= 163840;
-    // the reference-order streaming kernel (stftr): canonical n_fft 2048 geometry; mel kinds
-    // need its packed stream (64 lanes per frame)
+    // the reference-order streaming kernels (kernel 7): stftr at the canonical n_fft 2048
+    // geometry (mel kinds need its packed stream, 64 lanes per frame), stftq at n_fft 256 / 512 /
+    // 1024
     if (plan->melr_best >= 0) {
         const Plan::Melp& m = plan->melr[plan->melr_best];
         L.melr_chunks = m.chunks;
@@ -889,8 +890,10 @@ int batch_create(Plan* plan, const thesia_batch_desc& d, Batch** out) {
         L.melr_wt = m.wt.as<float4>();
     }
     const bool mel_kind = L.out_kind == OUT_MEL || L.out_kind == OUT_MEL_AMP_DB;
-    b->kr_ok = stftr_supports((int)plan->n_fft, (int)plan->win, (int)plan->hop, d.input_format, (int)d.channels) &&
-               (!mel_kind || L.melr_chunks > 0) && stftr_lds_bytes(L) <= 163840;
+    b->kr_ok = (stftr_supports((int)plan->n_fft, (int)plan->win, (int)plan->hop, d.input_format, (int)d.channels) &&
+                (!mel_kind || L.melr_chunks > 0) && stftr_lds_bytes(L) <= 163840) ||
+               (stftq_supports((int)plan->n_fft, (int)plan->win, (int)plan->hop, d.input_format, (int)d.channels) &&
+                stftq_lds_bytes(L) <= 163840);
     b->k5_view = view5;
     b->kernel = b->auto_kernel();
     if (hipEventCreate(&b->ev0) != hipSuccess || hipEventCreate(&b->ev1) != hipSuccess) {
@@ -988,7 +991,7 @@ int batch_run(Batch* b, hipStream_t s) {
         rc = launch_stftx(b->launch, s);
         if (rc) return set_error(rc == -2 ? THESIA_ERR_UNSUPPORTED : THESIA_ERR_DEVICE, "stftx launch failed");
     } else if (b->kernel == 7) {
-        rc = launch_stftr(b->launch, s);
+        rc = b->plan->n_fft == 2048 ? launch_stftr(b->launch, s) : launch_stftq(b->launch, s);
         if (rc) return set_error(rc == -2 ? THESIA_ERR_UNSUPPORTED : THESIA_ERR_DEVICE, "stftr launch failed");
     } else {
         if (b->kernel == 5) rc = launch_stft5(b->launch, s);

@@ -164,6 +164,11 @@ int launch_stftr(const StftLaunch& a, hipStream_t stream);
 bool stftr_supports(int n_fft, int win, int hop, int in_format, int channels);
 int stftr_lds_bytes(const StftLaunch& a);
 constexpr int stftr_region_floats() { return 16 * 130; }  // GeoR::REGION
+// stftq_kernel (the same contract for n_fft 256 / 512 / 1024, win = n_fft, hop = n_fft / 4;
+// stftq_kernels.hip): batch kernel 7 at those sizes
+int launch_stftq(const StftLaunch& a, hipStream_t stream);
+bool stftq_supports(int n_fft, int win, int hop, int in_format, int channels);
+int stftq_lds_bytes(const StftLaunch& a);
 // LDS bytes / frames per block pass / lanes per frame of the kernel for n_fft.
 int stft_kernel_info(int n_fft, int* lds_bytes, int* tile_frames, int* lanes_per_frame);
 

@@ -71,8 +71,9 @@ class RenderPipeline:
         """pinned_output: read the RGB images back into one page-locked host buffer (one
         DMA-rate copy per render); the returned images are then views that the next
         render() overwrites. Default: fresh pageable arrays per render().
-        kernel: the spectrogram kernel of every batch (0 = automatic; 9 = the reference-order
-        kernel, whose images equal the oracle pipeline's bytes; thesia_batch_set_option)."""
+        kernel: the spectrogram kernel of every batch (0 = automatic; 7 = the streaming
+        reference-order kernels (stftr / stftq), 9 = the one-wave-per-frame one: images equal to
+        the oracle pipeline's bytes; thesia_batch_set_option)."""
         self.tracks = list(tracks)
         self.pinned_output = pinned_output
         self._pinned = {}  # group -> registered host array
@@ -279,11 +280,12 @@ class RenderPipeline:
 
 
 def render_tracks(tracks: Sequence[Track], px_per_sec: float = 100.0, nheight: int = 500,
-                  db_range: float = 120.0, keep_db: bool = False, group=None) -> List[Rendered]:
+                  db_range: float = 120.0, keep_db: bool = False, group=None, kernel: int = 0) -> List[Rendered]:
     """Spectrogram (amp dB) + global range + grey + Lanczos3 + colormap for every track; one
     kernel launch per geometry group. `group`: torch.distributed group for the range exchange
-    when tracks are sharded over ranks (None = default group if initialised)."""
-    p = RenderPipeline(tracks, px_per_sec, nheight, db_range)
+    when tracks are sharded over ranks (None = default group if initialised). `kernel`: as
+    RenderPipeline's (7 / 9: the reference-order kernels, images equal to the oracle's bytes)."""
+    p = RenderPipeline(tracks, px_per_sec, nheight, db_range, kernel=kernel)
     try:
         p.run_spectrograms()
         return p.render(group=group, keep_db=keep_db)

@@ -103,6 +103,25 @@ def test_e2e_rgb_c5_generator():
     assert worst <= E2E_MAX_LSB and diff_px / total_px <= E2E_MAX_FRAC, (worst, diff_px, total_px)
 
 
+@pytest.mark.parametrize("kernel", [7, 9])
+def test_e2e_rgb_c5_generator_exact(kernel):
+    """The C5 generator through the reference-order kernels (7: the streaming stftr / stftq, 9:
+    stftx): the device RGB bytes equal the all-oracle pipeline's, every pixel of every track
+    (north_star: bit-exact for the final u8 buffer), n_fft 256 / 512 / 1024 / 2048 at six rates."""
+    tracks = pipeline.c5_tracks(12, seconds=2.0)
+    nh = 200
+    out = pipeline.render_tracks(tracks, px_per_sec=100.0, nheight=nh, kernel=kernel)
+    ref_db = [_oracle_amp_db(t) for t in tracks]
+    gmax, gmin, max_sr = shard.global_db_range(max(float(d.max()) for d in ref_db),
+                                               min(float(d.min()) for d in ref_db),
+                                               max(t.sr for t in tracks))
+    for i, (t, r, db) in enumerate(zip(tracks, out, ref_db)):
+        grey = O.spec_to_grey(db, shard.up_ratio(t.sr, max_sr, freq_scale_mel=False), gmax, gmin)
+        img, _ = O.grey_to_rgb(grey, r.nwidth, nh)
+        assert np.array_equal(np.asarray(r.rgb, np.uint8).reshape(-1), np.asarray(img, np.uint8).reshape(-1)), \
+            (i, t.sr, t.n_fft, _rgb_diff(r.rgb, img))
+
+
 def _oracle_specs(pcm, srs, scale, with_f64=False):
     """Per track: the oracle's amp-dB rows (|X| [, mel], dB; lib.rs:112-136) and, with_f64, the
     same rows from the float64 spectrum (tolerances.stft_f64), i.e. what both the reference's f32
