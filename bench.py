@@ -37,6 +37,13 @@ KERNEL_NAMES = {1: "thesia::stft_kernel (general)", 2: "thesia::stft2_kernel (ge
                 9: "thesia::stftx_kernel (reference order, bit-exact)"}
 
 
+def kernel_name(k, n_fft):
+    """Batch kernel 7 is stftr at n_fft 2048 and stftq at 256 / 512 / 1024."""
+    if k == 7 and n_fft != 2048:
+        return "thesia::stftq_kernel (streaming, reference order, bit-exact)"
+    return KERNEL_NAMES.get(k, str(k))
+
+
 def parse():
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
@@ -402,7 +409,7 @@ def rfft_roofline(args, din, offs, lens, fmt, n_local, n_samples):
                      kernel=args.kernel, row_store=args.row_store)
     b.run_timed(2)
     kms = b.run_timed(5) / 5
-    kname = KERNEL_NAMES.get(b.kernel, "?")
+    kname = kernel_name(b.kernel, args.n_fft)
     in_el = 4 if args.input == "f32" else 2
     in_bytes = n_local * n_samples * args.channels * in_el
     abytes = in_bytes + out_bytes
@@ -635,7 +642,7 @@ def main_c5(args, ws, rank, pg, device):
                          "overlapped_ms": kms_overlap,
                          "batches_policy_ms": pol_ms,
                          "per_batch_max_blocks_ms": mb_ms,
-                         "per_batch": [{"n_fft": nf, "frames": fr, "kernel_ms": t, "kernel": KERNEL_NAMES.get(k, str(k))}
+                         "per_batch": [{"n_fft": nf, "frames": fr, "kernel_ms": t, "kernel": kernel_name(k, nf)}
                                        for nf, fr, t, k in kms_batches],
                          "overlapped_note": "the step's spectrogram phase: the batches on the library "
                                             "streams (thesia_batches_run), HIP events on the library stream"},
@@ -1000,7 +1007,7 @@ def main_worker(args):
             "frac": achieved / HBM_PEAK_GBS,
             "traffic": rec.get("hbm_bytes_per_launch") if rec else None,
             "traffic_source": provenance(rec) if rec else "no stored PMC record of this exact workload",
-            "kernel": KERNEL_NAMES.get(batch.kernel, "?")
+            "kernel": kernel_name(batch.kernel, args.n_fft)
                       + ": downmix+frame+window+rFFT+" + {"mel_db": "|X|+mel+dB", "amp_db": "|X|+dB",
                                                            "power_db": "|X|^2+dB", "complex": "complex out"}[args.output]
                       + ", one launch",

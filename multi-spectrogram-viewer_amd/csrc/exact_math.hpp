@@ -100,7 +100,7 @@ THESIA_HD inline float log10f_glibc(float x) {
 // log10f / logf never apply, and logf's early return for x == 1 gives the same +0 as the
 // general path (table entry 9 is {1, 0}: r = 0, y = 0). Equal to log10f_glibc (and glibc) on
 // every positive normal float (tests/test_exact_math.py, exhaustive).
-THESIA_HD inline float log10f_normal(float x) {
+THESIA_HD inline float log10f_normal_tab(float x, const LogfEntry* tab) {
     const float ivln10 = 4.3429449201e-01f, log10_2hi = 3.0102920532e-01f, log10_2lo = 7.9034151668e-07f;
     const double Ln2 = 0x1.62e42fefa39efp-1;
     const double A0 = -0x1.00ea348b88334p-2, A1 = 0x1.5575b0be00b6ap-2, A2 = -0x1.ffffef20a4123p-2;
@@ -114,7 +114,7 @@ THESIA_HD inline float log10f_normal(float x) {
     const int i = (int)((tmp >> (23 - 4)) % 16);
     const int k = (int32_t)tmp >> 23;
     const uint32_t iz = ix - (tmp & (0x1ffu << 23));
-    const double invc = kLogfT[i].invc, logc = kLogfT[i].logc;
+    const double invc = tab[i].invc, logc = tab[i].logc;
     const double z = (double)bits_f32(iz);
     const double r = z * invc - 1.0;
     const double y0 = logc + (double)k * Ln2;
@@ -126,6 +126,8 @@ THESIA_HD inline float log10f_normal(float x) {
     const float zz = y * log10_2lo + ivln10 * lx;
     return zz + y * log10_2hi;
 }
+// (the table from constant memory; kernels pass an LDS copy of kLogfT to log10f_normal_tab)
+THESIA_HD inline float log10f_normal(float x) { return log10f_normal_tab(x, kLogfT); }
 
 // hypotf for finite x, y (glibc 2.35: double evaluation, one rounding)
 THESIA_HD inline float hypotf_glibc(float x, float y) {

@@ -40,7 +40,8 @@ struct GeoQ {
     static constexpr int NLEV = (B % 2) ? 1 + (B - 3) / 2 : B / 2;
     static constexpr int WL_STRIDE = 2 * P + 4, WL_FLOATS = L * WL_STRIDE;
     static constexpr int TW_FLOATS = 2 * NC, SC_FLOATS = 2 * NC + 4;
-    static constexpr int TAB_FLOATS = WL_FLOATS + TW_FLOATS + SC_FLOATS;
+    static constexpr int LOGT_FLOATS = 64;  // logf's table (exact_math.hpp kLogfT), LDS copy
+    static constexpr int TAB_FLOATS = WL_FLOATS + TW_FLOATS + SC_FLOATS + LOGT_FLOATS;
     // a frame's region: Z (2 NC floats), later the staged row (complex: 2F floats from sh <= 3)
     static constexpr int RS = (2 * F + 3 + 3) / 4 * 4;
     static_assert(L * P == NC && (1 << NL) == L && (1 << NR) == P && P % 4 == 0, "geometry");
@@ -208,11 +209,14 @@ constexpr int reg_pbits(int r, int ps) {
 
 }  // namespace
 
-// OKQ: 0 complex, 1 linear kinds, 2 mel kinds (the kind inside a class: a wave-uniform select in
-// the epilogue). C: 1 mono, 2 stereo (interleaved); INF: f32 / s16. WV waves per block.
-template <int NC, int OKQ, int C, int INF, int WV>
+// KIND: the output kind (kernels.hpp OUT_*). C: 1 mono, 2 stereo (interleaved); INF: f32 / s16.
+// WV waves per block. VAR:
+// ablations of the experiment library only (wrong output by design): 1 |X| by the f32 sqrt, 2 dB
+// by v_log_f32, 4 no untangle / epilogue (the FFT and the Z row alone).
+template <int NC, int KIND, int C, int INF, int WV, int VAR = 0>
 __global__ void __launch_bounds__(64 * WV)
 stftq_kernel(StftLaunch a, uint64_t fps) {
+    constexpr int OKQ = KIND == OUT_COMPLEX ? 0 : (KIND == OUT_MEL || KIND == OUT_MEL_AMP_DB) ? 2 : 1;
     using G = GeoQ<NC>;
     using CK = Chunk<C, INF>;
     using CT = typename CK::T;
@@ -225,6 +229,7 @@ stftq_kernel(StftLaunch a, uint64_t fps) {
     float2* twl = reinterpret_cast<float2*>(lds + G::WL_FLOATS);
     float2* scl = reinterpret_cast<float2*>(lds + G::WL_FLOATS + G::TW_FLOATS);
     float* work = lds + G::TAB_FLOATS;
+    const exact::LogfEntry* logt = logf_tab_to_lds(lds + G::WL_FLOATS + G::TW_FLOATS + G::SC_FLOATS);
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int slot = lane / L;
     constexpr int kBlock = 64 * WV;
@@ -248,7 +253,6 @@ stftq_kernel(StftLaunch a, uint64_t fps) {
     float* region = work + (wave * FPW + slot) * G::RS;
     const ET* in = static_cast<const ET*>(a.in);
     const float2 w8a = make_float2(a.xw8[0], a.xw8[1]), w8b = make_float2(a.xw8[2], a.xw8[3]);
-    const int kind = a.out_kind;
 
     float2 raw[P];
     CT pre[SH];
@@ -385,17 +389,24 @@ stftq_kernel(StftLaunch a, uint64_t fps) {
             return make_float2(xr, xi);
         };
         auto value = [&](float2 x) {  // the linear kinds (lib.rs:124, decibel.rs)
-            const bool power = kind == OUT_POWER || kind == OUT_POWER_DB;
-            float val = power ? x.x * x.x + x.y * x.y : exact::hypotf_cr(x.x, x.y);
-            if (kind == OUT_POWER_DB) val = rdb(val, a.log_amin, 1e-36f, 10.0f);
-            if (kind == OUT_AMP_DB) val = rdb(val, a.log_amin, 1e-18f, 20.0f);
+            constexpr bool power = KIND == OUT_POWER || KIND == OUT_POWER_DB;
+            float val;
+            if constexpr (power) val = x.x * x.x + x.y * x.y;  // num-complex norm_sqr
+            else if constexpr ((VAR & 1) != 0) val = __builtin_amdgcn_sqrtf(x.x * x.x + x.y * x.y);
+            else val = exact::hypotf_cr(x.x, x.y);  // num-complex norm
+            if constexpr ((VAR & 2) != 0) {
+                if constexpr (KIND == OUT_AMP_DB || KIND == OUT_POWER_DB) val = 20.0f * __builtin_amdgcn_logf(val);
+            } else {
+                if constexpr (KIND == OUT_POWER_DB) val = rdb(val, a.log_amin, 1e-36f, 10.0f, logt);
+                if constexpr (KIND == OUT_AMP_DB) val = rdb(val, a.log_amin, 1e-18f, 20.0f, logt);
+            }
             return val;
         };
         constexpr int NP = P / 2;
         float2 xo[OKQ == 0 ? 2 * NP + 1 : 1];
         float fo[OKQ == 0 ? 1 : 2 * NP + 1];
 #pragma unroll
-        for (int i = 0; i < NP; ++i) {
+        for (int i = 0; i < ((VAR & 4) ? 0 : NP); ++i) {
             const int k = lj + L * i;
             const int kp = (NC - k) & (NC - 1);
             const float2 zk = zc[k], zp = zc[kp];
@@ -432,13 +443,13 @@ stftq_kernel(StftLaunch a, uint64_t fps) {
             wave_lds_sync();
             // lib.rs:131 (the oracle's dot: one k-ascending fma chain per mel over its band)
             const int n_mels = a.n_mels;
-            const bool db = kind == OUT_MEL_AMP_DB;
+            constexpr bool db = KIND == OUT_MEL_AMP_DB;
             float* out = static_cast<float*>(a.out) + g * (uint64_t)n_mels;
             for (int m = lj; m < n_mels; m += L) {
                 const int4 bd = a.xmel_band[m];  // {first bin, bins, weight offset}
                 float acc = 0.0f;
                 for (int t2 = 0; t2 < bd.y; ++t2) acc = __builtin_fmaf(region[bd.x + t2], a.xmel_w[bd.z + t2], acc);
-                if (valid) out[m] = db ? rdb(acc, a.log_amin, 1e-18f, 20.0f) : acc;
+                if (valid) out[m] = db ? rdb(acc, a.log_amin, 1e-18f, 20.0f, logt) : acc;
             }
             wave_lds_sync();
         } else {
@@ -482,11 +493,22 @@ static int ldsq_bytes(int wv) {
     return (GeoQ<NC>::TAB_FLOATS + wv * GeoQ<NC>::FPW * GeoQ<NC>::RS) * 4;
 }
 
-template <int NC, int OKQ, int C, int INF, int WV>
+template <int NC, int KIND, int C, int INF, int WV, int VAR = 0>
 static int launchq_k(const StftLaunch& a, hipStream_t s) {
+#ifdef THESIA_EXPERIMENTS
+    if constexpr (VAR == 0 && KIND == OUT_AMP_DB && C == 1 && INF == IN_S16) {
+        const char* e = getenv("THESIA_STFT_VARIANT");
+        const int v = e ? atoi(e) : 0;
+        if (v == 1) return launchq_k<NC, KIND, C, INF, WV, 1>(a, s);
+        if (v == 3) return launchq_k<NC, KIND, C, INF, WV, 3>(a, s);
+        if (v == 4) return launchq_k<NC, KIND, C, INF, WV, 4>(a, s);
+        if (v == 12 && WV != 12) return launchq_k<NC, KIND, C, INF, 12, 0>(a, s);
+        if (v == 16 && WV != 16) return launchq_k<NC, KIND, C, INF, 16, 0>(a, s);
+    }
+#endif
     const int lds = ldsq_bytes<NC>(WV);
     if (lds > 163840) return -2;
-    auto kern = stftq_kernel<NC, OKQ, C, INF, WV>;
+    auto kern = stftq_kernel<NC, KIND, C, INF, WV, VAR>;
     if (hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize, lds) !=
         hipSuccess)
         return -1;
@@ -503,13 +525,20 @@ static int launchq_k(const StftLaunch& a, hipStream_t s) {
 
 template <int NC, int C, int INF>
 static int launchq_c(const StftLaunch& a, hipStream_t s) {
+    if ((a.out_kind == OUT_MEL || a.out_kind == OUT_MEL_AMP_DB) && (!a.xmel_band || !a.xmel_w)) return -2;
+    // 16-wave blocks (4 waves / SIMD, <= 128 VGPRs) for n_fft 512 / 1024: 3.59 -> 3.48 and 3.88
+    // -> 3.70 ms on 1000 x 10 s amp-dB tracks; n_fft 256 stays at 12 (3.54 vs 3.69;
+    // profiles/r05_stftq/ablations.txt)
+    constexpr int WV = NC == 128 ? 12 : 16;
     switch (a.out_kind) {
-        case OUT_COMPLEX: return launchq_k<NC, 0, C, INF, 12>(a, s);
-        case OUT_MEL:
-        case OUT_MEL_AMP_DB:
-            if (!a.xmel_band || !a.xmel_w) return -2;
-            return launchq_k<NC, 2, C, INF, 12>(a, s);
-        default: return launchq_k<NC, 1, C, INF, 12>(a, s);
+        case OUT_COMPLEX: return launchq_k<NC, OUT_COMPLEX, C, INF, WV>(a, s);
+        case OUT_MAG: return launchq_k<NC, OUT_MAG, C, INF, WV>(a, s);
+        case OUT_POWER: return launchq_k<NC, OUT_POWER, C, INF, WV>(a, s);
+        case OUT_AMP_DB: return launchq_k<NC, OUT_AMP_DB, C, INF, WV>(a, s);
+        case OUT_POWER_DB: return launchq_k<NC, OUT_POWER_DB, C, INF, WV>(a, s);
+        case OUT_MEL: return launchq_k<NC, OUT_MEL, C, INF, WV>(a, s);
+        case OUT_MEL_AMP_DB: return launchq_k<NC, OUT_MEL_AMP_DB, C, INF, WV>(a, s);
+        default: return -2;
     }
 }
 
@@ -525,7 +554,7 @@ bool stftq_supports(int n_fft, int win, int hop, int in_format, int channels) {
 }
 
 int stftq_lds_bytes(const StftLaunch& a) {
-    return a.n_fft == 256 ? ldsq_bytes<128>(12) : a.n_fft == 512 ? ldsq_bytes<256>(12) : ldsq_bytes<512>(12);
+    return a.n_fft == 256 ? ldsq_bytes<128>(12) : a.n_fft == 512 ? ldsq_bytes<256>(16) : ldsq_bytes<512>(16);
 }
 
 int launch_stftq(const StftLaunch& a, hipStream_t s) {

@@ -78,10 +78,18 @@ __device__ __forceinline__ float2 bsel2(unsigned m, float2 a, float2 b) {
 // decibel.rs:49-55 (ref 1: log_ref = 0) then the factor pass (:65 / :75), glibc log10f. Branch-free:
 // log10f_normal runs on max(x, amin) (amin = 1e-18 / 1e-36, normal floats; the log of x > amin is
 // glibc's, the other branch is the plan's log_amin) and the select keeps the reference's order.
-__device__ __forceinline__ float rdb(float x, float log_amin, float amin, float factor) {
-    const float l = exact::log10f_normal(x > amin ? x : amin);
+// tab: logf's 16-entry table (an LDS copy: a per-lane constant-memory lookup is a global load).
+__device__ __forceinline__ float rdb(float x, float log_amin, float amin, float factor,
+                                     const exact::LogfEntry* tab = exact::kLogfT) {
+    const float l = exact::log10f_normal_tab(x > amin ? x : amin, tab);
     const float y = x > amin ? l - 0.0f : log_amin - 0.0f;
     return factor * y;
+}
+// the LDS copy of logf's table (64 floats at lds_tab), filled by the block's threads
+__device__ __forceinline__ const exact::LogfEntry* logf_tab_to_lds(float* lds_tab) {
+    exact::LogfEntry* t = reinterpret_cast<exact::LogfEntry*>(lds_tab);
+    if (threadIdx.x < 16) t[threadIdx.x] = exact::kLogfT[threadIdx.x];
+    return t;
 }
 
 // rustfft butterfly_8 (the base level for odd log2(NC); oracle bfly8): Butterfly4 on the even

@@ -53,7 +53,8 @@ struct GeoR {
     static constexpr int WL_FLOATS = L * WL_STRIDE;
     static constexpr int TW_FLOATS = 2 * NC + 4;   // rustfft twiddles tw[0 .. NC)
     static constexpr int SC_FLOATS = 2 * NC + 4;   // realfft sin_cos, entry NC = padding
-    static constexpr int TAB_FLOATS = WL_FLOATS + TW_FLOATS + SC_FLOATS;
+    static constexpr int LOGT_FLOATS = 64;        // logf's table (exact_math.hpp kLogfT), LDS copy
+    static constexpr int TAB_FLOATS = WL_FLOATS + TW_FLOATS + SC_FLOATS + LOGT_FLOATS;
     static_assert(REGION >= 2 * F + 3 && REGION >= kMelpOut + 16 && REGION == stftr_region_floats(), "region");
 };
 
@@ -136,6 +137,7 @@ stftr_kernel(StftLaunch a, uint64_t fps) {
     float2* twl = reinterpret_cast<float2*>(lds + G::WL_FLOATS);
     float2* scl = reinterpret_cast<float2*>(lds + G::WL_FLOATS + G::TW_FLOATS);
     float* work = lds + G::TAB_FLOATS;
+    const exact::LogfEntry* logt = logf_tab_to_lds(lds + G::WL_FLOATS + G::TW_FLOATS + G::SC_FLOATS);
     int4* pm_lds = reinterpret_cast<int4*>(work + WV * G::REGION);
     float4* pw_lds = reinterpret_cast<float4*>(pm_lds + (MEL ? (a.melr_chunks + 2) * L : 0));
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -322,11 +324,11 @@ stftr_kernel(StftLaunch a, uint64_t fps) {
                 float val;
                 if constexpr (KIND == OUT_POWER || KIND == OUT_POWER_DB) {
                     val = x.x * x.x + x.y * x.y;  // num-complex norm_sqr
-                    if constexpr (KIND == OUT_POWER_DB) val = rdb(val, a.log_amin, 1e-36f, 10.0f);
+                    if constexpr (KIND == OUT_POWER_DB) val = rdb(val, a.log_amin, 1e-36f, 10.0f, logt);
                 } else {
                     if constexpr ((VAR & 1) != 0) val = __builtin_amdgcn_sqrtf(x.x * x.x + x.y * x.y);
                     else val = exact::hypotf_cr(x.x, x.y);  // num-complex norm (lib.rs:124)
-                    if constexpr (KIND == OUT_AMP_DB) val = rdb(val, a.log_amin, 1e-18f, 20.0f);
+                    if constexpr (KIND == OUT_AMP_DB) val = rdb(val, a.log_amin, 1e-18f, 20.0f, logt);
                 }
                 row[sh + k] = val;
             }
@@ -365,7 +367,7 @@ stftr_kernel(StftLaunch a, uint64_t fps) {
             float* out = static_cast<float*>(a.out) + g * (uint64_t)n_mels;
             for (int m = lj; m < n_mels; m += L) {
                 const float x = region[kMelpOut + m];
-                if (valid) out[m] = KIND == OUT_MEL_AMP_DB ? rdb(x, a.log_amin, 1e-18f, 20.0f) : x;
+                if (valid) out[m] = KIND == OUT_MEL_AMP_DB ? rdb(x, a.log_amin, 1e-18f, 20.0f, logt) : x;
             }
         } else {
             constexpr int nfl = CPLX ? 2 * F : F;
