@@ -66,6 +66,8 @@ def parse():
     p.add_argument("--n-mels", type=int, default=128)
     p.add_argument("--output", choices=["mel_db", "amp_db", "power_db", "complex"], default="mel_db")
     p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--no-exact", action="store_true",
+                   help="skip the bit-exact (reference-order kernel 7) line reported beside the default one")
     p.add_argument("--no-e2e", action="store_true", help="skip the PCIe-inclusive end-to-end sample")
     p.add_argument("--no-rfft-roofline", action="store_true",
                    help="skip the extra complex-output (window+rFFT kernel) roofline measurement")
@@ -613,6 +615,31 @@ def main_c5(args, ws, rank, pg, device):
         if rank == 0:
             print(json.dumps({"render_paths_ms": {str(q): {"median": float(np.median(t)), "min": float(min(t))}
                                                   for q, t in res.items()}}), flush=True)
+    exact = None
+    if args.kernel == 0 and ws == 1 and not args.no_exact:
+        # the same step with every batch on the reference-order streaming kernels (7: stftr at
+        # n_fft 2048, stftq at 256 / 512 / 1024): RGB bytes equal to the oracle pipeline's
+        # (tests/test_gpu_parity.py test_e2e_rgb_c5_generator_exact); reported beside the line
+        for _, _, _, b in p.groups:
+            b.set_option(engine.OPT_KERNEL, 7)
+        step()
+        engine.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(max(3, args.steps // 2)):
+            step()
+        engine.synchronize()
+        ex_dt = (time.perf_counter() - t0) / max(3, args.steps // 2)
+        ex_batches = [(pl.n_fft, b.run_timed(3) / 3, b.kernel) for pl, _, _, b in p.groups]
+        p.run_spectrograms()
+        with engine.EventTimer() as tm:
+            for _ in range(3):
+                p.run_spectrograms()
+        exact = {"kernel": 7, "ms_per_step": ex_dt * 1e3, "frames_per_s": p.total_frames / ex_dt,
+                 "spectrogram_overlapped_ms": tm.ms / 3,
+                 "per_batch": [{"n_fft": nf, "kernel_ms": t, "kernel": kernel_name(k, nf)} for nf, t, k in ex_batches],
+                 "note": "reference operation order end to end: the RGB bytes equal the oracle pipeline's"}
+        for _, _, _, b in p.groups:
+            b.set_option(engine.OPT_KERNEL, 0)
     in_bytes = sum(t.pcm.nbytes for t in tracks)
     out_bytes = sum(b.total_frames * pl.row_bins * 4 for pl, _, _, b in p.groups)
     achieved = (in_bytes + out_bytes) / (kms * 1e-3) / 1e9
@@ -644,6 +671,7 @@ def main_c5(args, ws, rank, pg, device):
                          "per_batch_max_blocks_ms": mb_ms,
                          "per_batch": [{"n_fft": nf, "frames": fr, "kernel_ms": t, "kernel": kernel_name(k, nf)}
                                        for nf, fr, t, k in kms_batches],
+                         "bit_exact": exact,
                          "overlapped_note": "the step's spectrogram phase: the batches on the library "
                                             "streams (thesia_batches_run), HIP events on the library stream"},
             "roofline_display": disp,
@@ -1024,6 +1052,19 @@ def main_worker(args):
             result["roofline_valu_issue"] = ic
         if kind != engine.OUT_COMPLEX and not args.no_rfft_roofline:
             result["roofline_window_rfft"] = rfft_roofline(args, din, offs, lens, fmt, n_local, n_samples)
+        if ws == 1 and args.kernel == 0 and not args.no_exact:
+            # the same launch on the reference-order streaming kernel (rows equal the oracle's bit
+            # for bit, tests/test_gpu_stftr.py / test_gpu_stftq.py), reported beside the line
+            try:
+                batch.set_option(engine.OPT_KERNEL, 7)
+                batch.run_timed(1)
+                ems = batch.run_timed(max(3, args.steps // 2)) / max(3, args.steps // 2)
+                result["bit_exact"] = {"kernel": kernel_name(7, args.n_fft), "kernel_ms": ems,
+                                       "frames_per_s": frames / (ems * 1e-3),
+                                       "roofline_frac": abytes / (ems * 1e-3) / 1e9 / HBM_PEAK_GBS}
+                batch.set_option(engine.OPT_KERNEL, 0)
+            except Exception as e:  # (a geometry kernel 7 does not cover)
+                result["bit_exact"] = {"unsupported": str(e)}
         if ws == 1 and not args.no_cpu_baseline:
             result["cpu_baseline"] = cpu_baseline(args, n_samples)
         if ws == 1 and not args.no_c1:
