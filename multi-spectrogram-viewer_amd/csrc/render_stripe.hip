@@ -32,6 +32,12 @@ namespace thesia {
 
 namespace {
 
+#ifdef THESIA_MARKS
+#define SMARK(x) asm volatile("; MARK " #x)
+#else
+#define SMARK(x)
+#endif
+
 constexpr int kRgbStride = 13;  // dwords per row of a wave's RGB staging (16 columns = 12 dwords)
 constexpr int kSumStride = 17;  // floats per row of a wave's finished sums (16 columns)
 constexpr int kLutFloats = 32;  // the colormap as 10 x {stop i, stop i + 1} (8 bytes each)
@@ -309,12 +315,15 @@ __global__ void __launch_bounds__(64 * WV) render_stripe_kernel(StripeLaunch L) 
     // slot a <-> column ca(s) + a of the step's table (columns before c0, finished by the strip
     // on the left, and from c1 on are summed too and never stored)
     for (int k = 0; k < nchunks; ++k) {
+        SMARK(issue);
         if (k + 1 < nchunks && nb && !(abl & 1)) issue(k + 1);
+        SMARK(steps);
         const float* t = tile + q * TS;
         for (int u8 = 0; u8 < SPC; ++u8) {
             const int si = k * SPC + u8;
             if (si >= nst) break;  // uniform
             const int ca = rfl(hdr[si]);
+            SMARK(vert);
             // vertical sums of the step's 8 frames (resize_v_px order), 4 frames at a time: one
             // ds_read_b128 per tap, a batch of taps' reads in flight
             float v[8];
@@ -349,6 +358,7 @@ __global__ void __launch_bounds__(64 * WV) render_stripe_kernel(StripeLaunch L) 
             // horizontal: every slot's chain takes the step's frames in ascending order (the
             // resize_h order; slots outside a column's support add (+0 weight) x v = +-0); the
             // weights of frame u + 1 are read while frame u is summed
+            SMARK(horiz);
             constexpr int A4 = (A + 3) / 4;  // float4 weight reads per frame
             const float4* wu = reinterpret_cast<const float4*>(wts + si * 8 * AW);
             float4 xc[A4];
@@ -379,6 +389,7 @@ __global__ void __launch_bounds__(64 * WV) render_stripe_kernel(StripeLaunch L) 
             }
             // the columns whose supports end in this step (all of the strip's at its last):
             // finished, the slots shift down
+            SMARK(close);
             const int cn = si + 1 < nst ? rfl(hdr[si + 1]) : (int)c1;
             for (int c = ca; c < cn; ++c) {  // uniform
                 if (c >= (int)c0 && c < (int)c1) close_col((uint32_t)c, acc[0]);
@@ -387,6 +398,7 @@ __global__ void __launch_bounds__(64 * WV) render_stripe_kernel(StripeLaunch L) 
                 acc[A - 1] = 0.0f;
             }
         }
+        SMARK(commit);
         if (k + 1 < nchunks && nb && !(abl & 1)) {
             wave_sync();  // every lane's reads of the buffer chunk k + 1 overwrites are done
             commit(k + 1);

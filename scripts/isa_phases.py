@@ -12,7 +12,8 @@ def main():
     minv = int(sys.argv[3]) if len(sys.argv) > 3 else 0
     text = open(path).read()
     m = re.search(r"^(_Z\S*" + re.escape(sub) + r"\S*):\s*;\s*@", text, re.M)
-    body = text[m.end():text.find("s_endpgm", m.end())]
+    # to the function's end (an early return puts an s_endpgm in the middle of the body)
+    body = text[m.end():text.find(".Lfunc_end", m.end())]
     cur, order, cnt = "entry", ["entry"], {}
     for line in body.split("\n"):
         t = line.strip()
