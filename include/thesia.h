@@ -203,14 +203,17 @@ int thesia_batch_kernel_info(const thesia_batch* batch, int* lds_bytes, int* til
 
 /* Which fused kernel runs the batch: 1 stft_kernel (general), 2 stft2_kernel (4 waves/SIMD),
  * 3 stft3_kernel (streaming; win = n_fft, hop = n_fft/4), 5 stft5_kernel (streaming, n_fft 2048:
- * untangle pairs co-resident in a lane), 9 stftx_kernel (the reference's operation order). */
+ * untangle pairs co-resident in a lane), 7 the streaming reference-order kernels (stftr_kernel at
+ * n_fft 2048, stftq_kernel at 256 / 512 / 1024; win = n_fft, hop = n_fft/4: rows equal the
+ * reference's bit for bit), 9 stftx_kernel (the reference's operation order, any geometry). */
 int thesia_batch_kernel(const thesia_batch* batch, int* kernel);
 
 /* Named alternatives of a batch (none changes what is computed, only how; all results stay
  * within the parity contract). Not part of the reference surface. */
 typedef enum {
-    /* 0 = automatic (streaming kernel where its geometry allows), 1 / 2 / 3 / 5 / 9 = force
-     * that kernel (THESIA_ERR_UNSUPPORTED if it cannot run the geometry) */
+    /* 0 = automatic (streaming kernel where its geometry allows), 1 / 2 / 3 / 5 / 7 / 9 = force
+     * that kernel (THESIA_ERR_UNSUPPORTED if it cannot run the geometry); 7 and 9 compute in
+     * the reference's operation order (bit-exact rows) */
     THESIA_BATCH_OPT_KERNEL = 1,
     /* at most this many workgroups per launch (0 = one full occupancy wave of the device);
      * small values make every frame stream walk many frames */
