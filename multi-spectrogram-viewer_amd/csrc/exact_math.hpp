@@ -82,6 +82,7 @@ THESIA_HD inline float log10f_glibc(float x) {
     const float two25 = 3.3554432000e+07f, ivln10 = 4.3429449201e-01f;
     const float log10_2hi = 3.0102920532e-01f, log10_2lo = 7.9034151668e-07f;
     int32_t hx = (int32_t)f32_bits(x), k = 0;
+    if (hx >= 0x7f800000) return x + x;  // +inf, NaN (e_log10f.c)
     if (hx < 0x00800000) {  // subnormal: scale up
         k -= 25;
         x *= two25;
@@ -124,13 +125,16 @@ THESIA_HD inline float log10f_normal_tab(float x, const LogfEntry* tab) {
     q = q * r2 + (y0 + r);
     const float lx = (float)q;
     const float zz = y * log10_2lo + ivln10 * lx;
-    return zz + y * log10_2hi;
+    const float res = zz + y * log10_2hi;
+    return hx >= 0x7f800000 ? x + x : res;  // +inf, NaN (e_log10f.c), as a select
 }
 // (the table from constant memory; kernels pass an LDS copy of kLogfT to log10f_normal_tab)
 THESIA_HD inline float log10f_normal(float x) { return log10f_normal_tab(x, kLogfT); }
 
-// hypotf for finite x, y (glibc 2.35: double evaluation, one rounding)
+// hypotf (glibc 2.35 e_hypotf.c: an infinite argument gives +inf, even beside a NaN; else double
+// evaluation, one rounding)
 THESIA_HD inline float hypotf_glibc(float x, float y) {
+    if (__builtin_fabsf(x) == __builtin_inff() || __builtin_fabsf(y) == __builtin_inff()) return __builtin_inff();
     const double dx = (double)x, dy = (double)y;
     return (float)__builtin_sqrt(dx * dx + dy * dy);
 }
@@ -154,7 +158,8 @@ __device__ inline __attribute__((always_inline)) float hypotf_cr(float x, float 
     d = __builtin_fma(-g, g, S);
     g = __builtin_fma(d, h, g);
     const float f = (float)g;
-    return S == 0.0 ? 0.0f : f;
+    const bool inf = __builtin_fabsf(x) == __builtin_inff() || __builtin_fabsf(y) == __builtin_inff();
+    return inf ? __builtin_inff() : S == 0.0 ? 0.0f : f;
 }
 #elif defined(__HIPCC__)
 __host__ inline float hypotf_cr(float x, float y) { return hypotf_glibc(x, y); }  // (host pass)

@@ -34,6 +34,22 @@ int main(int argc, char** argv) {
         memcpy(&y, &b, 4);
         if (thesia::exact::f32_bits(hypotf(x, y)) != thesia::exact::f32_bits(thesia::exact::hypotf_glibc(x, y))) ++bad_hyp;
     }
-    printf("%ld %ld %ld %ld %ld\n", n, bad_log, bad_log10, bad_hyp, bad_norm);
+    // non-finite and zero arguments (e_hypotf.c / e_log10f.c special cases; NaN results compared
+    // as NaN, not by payload)
+    long bad_special = 0;
+    const float sp[] = {0.0f, -0.0f, 1.5f, -3.25e-20f, 7.0e30f, __builtin_inff(), -__builtin_inff(), __builtin_nanf("")};
+    auto same = [](float a, float b) {
+        return (a != a && b != b) || thesia::exact::f32_bits(a) == thesia::exact::f32_bits(b);
+    };
+    for (float x : sp) {
+        for (float y : sp)
+            if (!same(hypotf(x, y), thesia::exact::hypotf_glibc(x, y))) ++bad_special;
+        if (x > 0.0f || x != x) {
+            if (!same(log10f(x), thesia::exact::log10f_glibc(x))) ++bad_special;
+            if (x >= 1.17549435e-38f || x != x)
+                if (!same(log10f(x), thesia::exact::log10f_normal(x))) ++bad_special;
+        }
+    }
+    printf("%ld %ld %ld %ld %ld %ld\n", n, bad_log, bad_log10, bad_hyp, bad_norm, bad_special);
     return 0;
 }

@@ -141,3 +141,36 @@ def test_equals_stftx_on_long_tracks(n_fft):
     b = _run(n_fft, engine.OUT_AMP_DB, tracks, 1, engine.IN_S16, kernel=9)
     for x, y in zip(a, b):
         assert np.array_equal(x.view(np.uint32), y.view(np.uint32))
+
+
+def _same_nan_aware(got, want):
+    gn, wn = np.isnan(got.view(np.float32)), np.isnan(want.view(np.float32))
+    assert np.array_equal(gn, wn), int((gn != wn).sum())
+    g, w = got.view(np.uint32), want.view(np.uint32)
+    keep = ~gn.reshape(g.shape)
+    assert np.array_equal(g[keep], w[keep]), int((g[keep] != w[keep]).sum())
+
+
+@pytest.mark.parametrize("kernel", [7, 9])
+@pytest.mark.parametrize("n_fft", [512, 2048])
+@pytest.mark.parametrize("kind", [engine.OUT_COMPLEX, engine.OUT_MAG, engine.OUT_POWER, engine.OUT_MEL])
+def test_non_finite_samples(kernel, n_fft, kind):
+    """f32 tracks holding +inf / -inf / NaN samples (a float WAV can carry them): the
+    reference-order kernels follow glibc's special cases (hypotf of an infinity is +inf even
+    beside a NaN) -- equal to the oracle bit for bit wherever the value is not NaN, NaN exactly
+    where the oracle's is. (The dB kinds are not compared: such frames hold NaN bins, on which
+    the reference's amp_to_db asserts, decibel.rs:34; the engine reports them through the range
+    NaN flag instead.)"""
+    rng = np.random.default_rng(n_fft + kind)
+    tracks = _tracks(rng, [9 * n_fft + 5, 4 * n_fft], 1, engine.IN_F32)
+    tracks[0][3 * n_fft // 2, 0] = np.inf
+    tracks[0][6 * n_fft, 0] = -np.inf
+    tracks[1][n_fft + 7, 0] = np.nan
+    fb = O.calc_mel_fb(48000, n_fft, 64) if kind == engine.OUT_MEL else None
+    rows = _run(n_fft, kind, tracks, 1, engine.IN_F32, n_mels=64 if fb is not None else 0, kernel=kernel)
+    w = (O.hann(n_fft) / np.float32(n_fft)).astype(np.float32)
+    for t, got in zip(tracks, rows):
+        with np.errstate(invalid="ignore", over="ignore"):
+            want = _want(kind, O.perform_stft(_ref_input(t, engine.IN_F32), n_fft, n_fft // 4, n_fft, window=w), fb)
+        assert got.shape == want.shape
+        _same_nan_aware(np.ascontiguousarray(got), np.ascontiguousarray(want))
