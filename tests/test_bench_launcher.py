@@ -61,7 +61,7 @@ def test_profile_records_behind_the_bench_line():
     rec = bench.profile_record(bench.workload_params(args, 5))
     assert rec is not None and rec["hbm_bytes_per_launch"] > 12.96e9  # >= the algorithmic bytes
     src = bench.provenance(rec)
-    assert src["measured_in_this_run"] is False and src["profile"].startswith("profiles/r04_close")
+    assert src["measured_in_this_run"] is False and src["profile"].startswith("profiles/r05_close")
     ic = bench.issue_ceiling(rec, 4.0)
     assert ic["bound"] == "valu-issue" and ic["peak"] == 1228.8
     assert abs(ic["achieved"] - ic["valu_insts_per_launch"] / 4e-3 / 1e9) < 1e-9 * ic["achieved"]
