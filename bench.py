@@ -575,6 +575,22 @@ def main_c5(args, ws, rank, pg, device):
     disp["traffic"] = drec["hbm_bytes_per_launch"] if drec else None
     disp["traffic_source"] = provenance(drec) if drec else "no stored PMC record of this exact workload"
     disp_ic = issue_ceiling(drec, disp["display_ms"]) if drec else None
+    spec_ceiling = None
+    if ws == 1:
+        # each phase's same-process copy ceiling: the display's algorithmic
+        # bytes (the dB rows read once, the RGB written once) and the spectrogram phase's (PCM read
+        # once, rows written once) moved by thesia_hbm_ceiling's coalesced float4 copy
+        db = disp["algorithmic_bytes"]
+        scratch = engine.DeviceBuffer(db["spec_read"])
+        disp.update(hbm_ceiling(scratch, db["spec_read"], p._rgb, db["rgb_write"]))
+        disp["frac_of_ceiling"] = disp["achieved"] / disp["ceiling_gbs"]
+        scratch.close()
+        sin = sum(t.pcm.nbytes for t in tracks)
+        sout = sum(b.total_frames * pl.row_bins * 4 for pl, _, _, b in p.groups)
+        s_in, s_out = engine.DeviceBuffer(sin), engine.DeviceBuffer(sout)
+        spec_ceiling = hbm_ceiling(s_in, sin, s_out, sout)
+        s_in.close()
+        s_out.close()
     pol_ms = None
     if args.spec_policies:
         import numpy as np
@@ -667,6 +683,9 @@ def main_c5(args, ws, rank, pg, device):
                          "kernel_ms": kms, "algorithmic_bytes_per_launch": in_bytes + out_bytes,
                          "kernel_ms_note": "sum of the batches' launches, each timed alone",
                          "overlapped_ms": kms_overlap,
+                         "copy_ceiling": spec_ceiling,
+                         "frac_of_ceiling": ((in_bytes + out_bytes) / (kms_overlap * 1e-3) / 1e9 / spec_ceiling["ceiling_gbs"])
+                                            if spec_ceiling else None,
                          "batches_policy_ms": pol_ms,
                          "per_batch_max_blocks_ms": mb_ms,
                          "per_batch": [{"n_fft": nf, "frames": fr, "kernel_ms": t, "kernel": kernel_name(k, nf)}
