@@ -43,7 +43,11 @@ struct GeoQ {
     static constexpr int LOGT_FLOATS = 64;  // logf's table (exact_math.hpp kLogfT), LDS copy
     static constexpr int TAB_FLOATS = WL_FLOATS + TW_FLOATS + SC_FLOATS + LOGT_FLOATS;
     // a frame's region: Z (2 NC floats), later the staged row (complex: 2F floats from sh <= 3)
-    static constexpr int RS = (2 * F + 3 + 3) / 4 * 4;
+    // (or, during the FFT, the relayout of the NC points: 2 NC floats plus one float2 of padding
+    // per 16, relayout_pad)
+    static constexpr int RS_ROW = (2 * F + 3 + 3) / 4 * 4;
+    static constexpr int RS_RELAYOUT = (2 * (NC + NC / 16) + 3) / 4 * 4;
+    static constexpr int RS = RS_ROW > RS_RELAYOUT ? RS_ROW : RS_RELAYOUT;
     static_assert(L * P == NC && (1 << NL) == L && (1 << NR) == P && P % 4 == 0, "geometry");
     static_assert(RS >= 2 * NC && RS % 4 == 0, "region");
 };
@@ -176,6 +180,39 @@ __device__ __forceinline__ void qswap(float2 (&v)[P], int lj) {
     }
 }
 
+// The layout of a level's input (T > 0: the previous level's, after its swaps; T = 0: point m =
+// lane + L register) and of its own (after its swaps): the point index m held at (lane, register)
+// is lane_mbits + reg_mbits (disjoint bits).
+template <int NC, int T, bool NEW>
+__device__ __forceinline__ int lane_mbits(int lj) {
+    using G = GeoQ<NC>;
+    int m = 0;
+    static_for<0, G::B>([&](auto bc) {
+        constexpr int b = decltype(bc)::value;
+        constexpr bool init = !NEW && T == 0;
+        constexpr int kind = init ? (b < G::NL ? 0 : 1) : QS<NC>::S.lev[NEW ? T : T - 1].kind[b];
+        constexpr int bit = init ? (b < G::NL ? b : b - G::NL) : QS<NC>::S.lev[NEW ? T : T - 1].bit[b];
+        if constexpr (kind == 0) m |= ((lj >> bit) & 1) << b;
+    });
+    return m;
+}
+template <int NC, int T, bool NEW>
+constexpr int reg_mbits(int r) {
+    using G = GeoQ<NC>;
+    int m = 0;
+    for (int b = 0; b < G::B; ++b) {
+        const bool init = !NEW && T == 0;
+        const int kind = init ? (b < G::NL ? 0 : 1) : QS<NC>::S.lev[NEW ? T : T - 1].kind[b];
+        const int bit = init ? (b < G::NL ? b : b - G::NL) : QS<NC>::S.lev[NEW ? T : T - 1].bit[b];
+        if (kind == 1) m |= ((r >> bit) & 1) << b;
+    }
+    return m;
+}
+// LDS slot of point m: one float2 of padding per 16 (the lane bits of a later level's layout
+// are m's higher bits: unpadded, a store or load of 16 lanes would hit one bank group).
+// Separable: pad(ml | mr) = pad(ml) + pad(mr) for disjoint bits.
+__host__ __device__ constexpr int relayout_pad(int m) { return m + (m >> 4); }
+
 // the lane part of sum over m bits b with pbit[b] < PS held in lane bits of ((lane bit) << pbit)
 template <int NC, int T, bool BELOW>
 __device__ __forceinline__ int lane_pbits(int lj, int ps) {
@@ -212,7 +249,8 @@ constexpr int reg_pbits(int r, int ps) {
 // KIND: the output kind (kernels.hpp OUT_*). C: 1 mono, 2 stereo (interleaved); INF: f32 / s16.
 // WV waves per block. VAR:
 // ablations of the experiment library only (wrong output by design): 1 |X| by the f32 sqrt, 2 dB
-// by v_log_f32, 4 no untangle / epilogue (the FFT and the Z row alone).
+// by v_log_f32, 4 no untangle / epilogue (the FFT and the Z row alone); 16 (exact, A/B): every
+// swap as lane exchanges instead of the LDS relayout.
 template <int NC, int KIND, int C, int INF, int WV, int VAR = 0>
 __global__ void __launch_bounds__(64 * WV)
 stftq_kernel(StftLaunch a, uint64_t fps) {
@@ -331,10 +369,36 @@ stftq_kernel(StftLaunch a, uint64_t fps) {
         static_for<0, G::NLEV>([&](auto tc) {
             constexpr int t = decltype(tc)::value;
             constexpr QLev q = S.lev[t];
-            static_for<0, q.nsw>([&](auto sc) {
-                constexpr int s = decltype(sc)::value;
-                qswap<q.swx[s], q.swy[s], P>(v, lj);
-            });
+            // the level's lane-bit <-> register-bit swaps: v_permlane16_swap for lane bit 4 (one
+            // VALU per dword); the others as one LDS round trip of the frame's points (written at
+            // their m, read back in the new layout: P stores + P loads where the DPP / bpermute
+            // swaps cost 4-5 VALU per dword and swap)
+            constexpr bool kPerm = q.nsw > 0 && q.swx[0] == 4 && (q.nsw < 2 || q.swx[1] == 4) &&
+                                   (q.nsw < 3 || q.swx[2] == 4);
+            if constexpr (q.nsw > 0 && ((VAR & 16) != 0 || kPerm)) {
+                static_for<0, q.nsw>([&](auto sc) {
+                    constexpr int s = decltype(sc)::value;
+                    qswap<q.swx[s], q.swy[s], P>(v, lj);
+                });
+            } else if constexpr (q.nsw > 0) {
+                float2* zb = reinterpret_cast<float2*>(region);
+                wave_lds_sync();  // the region's previous readers are done
+                {
+                    float2* wb = zb + relayout_pad(lane_mbits<NC, t, false>(lj));
+                    static_for<0, P>([&](auto rc) {
+                        constexpr int r = decltype(rc)::value;
+                        wb[relayout_pad(reg_mbits<NC, t, false>(r))] = v[r];
+                    });
+                }
+                wave_lds_sync();
+                {
+                    const float2* rb = zb + relayout_pad(lane_mbits<NC, t, true>(lj));
+                    static_for<0, P>([&](auto rc) {
+                        constexpr int r = decltype(rc)::value;
+                        v[r] = rb[relayout_pad(reg_mbits<NC, t, true>(r))];
+                    });
+                }
+            }
             constexpr int R = 1 << q.nd;
             constexpr int dmask = (1 << q.bit[q.dig[0]]) | (1 << q.bit[q.dig[1]]) | (q.nd == 3 ? (1 << q.bit[q.dig[2]]) : 0);
             constexpr int tstride = NC >> (q.pstart + 2);
@@ -503,7 +567,7 @@ static int launchq_k(const StftLaunch& a, hipStream_t s) {
         if (v == 3) return launchq_k<NC, KIND, C, INF, WV, 3>(a, s);
         if (v == 4) return launchq_k<NC, KIND, C, INF, WV, 4>(a, s);
         if (v == 12 && WV != 12) return launchq_k<NC, KIND, C, INF, 12, 0>(a, s);
-        if (v == 16 && WV != 16) return launchq_k<NC, KIND, C, INF, 16, 0>(a, s);
+        if (v == 16) return launchq_k<NC, KIND, C, INF, WV, 16>(a, s);
     }
 #endif
     const int lds = ldsq_bytes<NC>(WV);
