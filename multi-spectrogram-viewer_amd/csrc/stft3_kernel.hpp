@@ -21,6 +21,10 @@ namespace thesia {
 // bit12 = no wave-priority phases (s_setprio; previous); bit13 / bit14 = the FFT's twiddle reads
 // and transposes at priority 1 / 2; bit15 = the mel rounds at priority 3; bit16 = the prefetch
 // loads issued at priority 3.
+// Product bits: 18-20 = the linear kind fixed at compile time (OUT_AMP .. OUT_POWER_DB; 0 = the
+// launch's out_kind at run time), bit21 = the per-track range fold compiled in (with a fixed kind:
+// a.trk_range is set). Without them every bin of the epilogue runs uniform branches on the kind
+// and on the range flag (four s_cbranch per bin at amp dB).
 #ifdef THESIA_MARKS
 #define MARK(x) asm volatile("; MARK " #x)
 #else
@@ -348,13 +352,14 @@ stft3_kernel(StftLaunch a, uint64_t fps) {
             wave_lds_sync();
             if (valid) store_row_b128<L>(crow, sh, region, 2 * F, j);
         } else if constexpr (stage_rows(OK, VAR)) {
-            const int kind = a.out_kind;
+            constexpr int KD = (VAR >> 18) & 7;
+            const int kind = KD ? KD : a.out_kind;
             const bool power = kind == OUT_POWER || kind == OUT_POWER_DB;
             const bool db = kind == OUT_AMP_DB || kind == OUT_POWER_DB;
             float* frow = static_cast<float*>(a.out) + g * F;
             const int sh = (int)((reinterpret_cast<uintptr_t>(frow) >> 2) & 3);
             float* st = region + sh;
-            const bool rng = a.trk_range != nullptr;  // uniform
+            const bool rng = KD ? (VAR & (1 << 21)) != 0 : a.trk_range != nullptr;  // uniform
             if (rng) {
                 const int t = valid ? hint : -1;
                 if (t != r_trk) {  // uniform over the frame's lanes

@@ -107,6 +107,15 @@ static int launch3_c(const StftLaunch& a, hipStream_t s) {
     constexpr int WVS = NC <= 256 && C == 1 ? THESIA_WV3_SMALL : kWaves;
     if (a.out_kind == OUT_COMPLEX) return launch3_k<NC, 0, C, INF>(a, s);
     if (a.out_kind == OUT_MEL || a.out_kind == OUT_MEL_AMP_DB) return launch3_k<NC, 2, C, INF>(a, s);
+    // amp dB (the default kind, the C5 / viewer rows): the kind and the range fold at compile
+    // time (stft3_kernel.hpp, VAR bits 18-21)
+    bool fixed = a.out_kind == OUT_AMP_DB && a.row_alt == 0;
+#ifdef THESIA_EXPERIMENTS
+    if (getenv("THESIA_STFT3_RTKIND")) fixed = false;  // A/B: the run-time kind
+#endif
+    constexpr int KDB = OUT_AMP_DB << 18, KRG = 1 << 21;
+    if (fixed)
+        return a.trk_range ? launch3_k<NC, 1, C, INF, KDB | KRG, WVS>(a, s) : launch3_k<NC, 1, C, INF, KDB, WVS>(a, s);
     return launch3_k<NC, 1, C, INF, 0, WVS>(a, s);
 }
 
