@@ -51,6 +51,12 @@ int launch3v_c(const StftLaunch& a, hipStream_t s) {
     constexpr int WVS = NC <= 256 && C == 1 ? 12 : kWaves;
     if (a.out_kind == OUT_COMPLEX) return launch3v_k<NC, HQ, 0, C, INF, VODD ? 1024 : 2048, kWaves, VODD>(a, s);
     if (a.out_kind == OUT_MEL || a.out_kind == OUT_MEL_AMP_DB) return launch3v_k<NC, HQ, 2, C, INF, 0, kWaves, VODD>(a, s);
+    // amp dB rows without the range fold (the viewer's): the kind at compile time (VAR bits 18-20)
+    bool fixed = a.out_kind == OUT_AMP_DB && !a.trk_range;
+#ifdef THESIA_EXPERIMENTS
+    if (getenv("THESIA_STFT3_RTKIND")) fixed = false;  // A/B: the run-time kind
+#endif
+    if (fixed) return launch3v_k<NC, HQ, 1, C, INF, OUT_AMP_DB << 18, WVS, VODD>(a, s);
     return launch3v_k<NC, HQ, 1, C, INF, 0, WVS, VODD>(a, s);
 }
 

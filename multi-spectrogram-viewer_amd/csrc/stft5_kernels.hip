@@ -222,6 +222,8 @@ __device__ __forceinline__ void melp5(const StftLaunch& a, float* region, const 
 }
 
 // OK: 0 complex, 1 linear kinds, 2 mel kinds. C: 1 mono, 2 stereo (interleaved); INF: f32 / s16.
+// VAR bits 18-20: the linear kind fixed at compile time (as stft3_kernel.hpp: no per-bin uniform
+// branches on the kind; amp dB, the default kind, is instantiated so).
 // VAR bit 0 (experiment): the register ring rotates instead of shifting -- logical point group t
 // (points 8 t .. 8 t + 7 of the lane's 32) lives in physical group (t + ph) & 3, the hop's new
 // samples overwrite the oldest group and ph advances (no 48 v_mov per frame pair); the first
@@ -606,7 +608,8 @@ stft5_kernel(StftLaunch a, uint64_t fps, int rs) {
             }
         } else {
             static_assert(kStage, "linear kinds stage their rows");
-            const int kind = a.out_kind;
+            constexpr int KD = (VAR >> 18) & 7;  // the kind fixed at compile time (0: run time)
+            const int kind = KD ? KD : a.out_kind;
             const bool power = kind == OUT_POWER || kind == OUT_POWER_DB;
             const bool db = kind == OUT_AMP_DB || kind == OUT_POWER_DB;
             float* frow = static_cast<float*>(a.out) + g * F;
@@ -692,13 +695,19 @@ static bool view5(const StftLaunch& a) { return !(a.win == 2048 && a.hop * 4 == 
 template <int C, int INF>
 static int launch5_c(const StftLaunch& a, hipStream_t s) {
     const bool mel = a.out_kind == OUT_MEL || a.out_kind == OUT_MEL_AMP_DB;
+    bool fixed = a.out_kind == OUT_AMP_DB;  // amp dB rows: the kind at compile time
+#ifdef THESIA_EXPERIMENTS
+    if (getenv("THESIA_STFT3_RTKIND")) fixed = false;  // A/B: the run-time kind
+#endif
+    constexpr int KDB = OUT_AMP_DB << 18;
     if (view5(a)) {
         if (a.out_kind == OUT_COMPLEX) return -2;
-        return mel ? launch5_k<2, C, INF, 0, 7>(a, s) : launch5_k<1, C, INF, 0, 7>(a, s);
+        if (mel) return launch5_k<2, C, INF, 0, 7>(a, s);
+        return fixed ? launch5_k<1, C, INF, KDB, 7>(a, s) : launch5_k<1, C, INF, 0, 7>(a, s);
     }
     if (a.out_kind == OUT_COMPLEX) return launch5_k<0, C, INF>(a, s);
     if (mel) return launch5_k<2, C, INF>(a, s);
-    return launch5_k<1, C, INF>(a, s);
+    return fixed ? launch5_k<1, C, INF, KDB>(a, s) : launch5_k<1, C, INF>(a, s);
 }
 
 int stft5_lds_bytes(const StftLaunch& a) {
