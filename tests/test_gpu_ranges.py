@@ -77,3 +77,43 @@ def test_auto_kernel_follows_the_range_option():
             r = rows[int(b.frame0[i]):int(b.frame0[i + 1])]
             assert mx[i] == r.max() and mn[i] == r.min() and not nan[i]
         outs.append(rows)
+
+
+@pytest.mark.parametrize("n_fft", [256, 512, 1024, 2048])
+@pytest.mark.parametrize("ch,fmt", [(1, "f32"), (2, "f32"), (1, "s16"), (2, "s16")])
+def test_amp_db_fold_instances(n_fft, ch, fmt):
+    """Amp dB rows run stft3 instances with the kind and the range fold fixed at compile time
+    (stft3_kernel.hpp VAR bits 18-21): with the range option (fold compiled in)
+    and without it (fold compiled out) the rows are the same bits, and the folded ranges equal
+    the rows' max / min, for every n_fft, channel count and input format."""
+    rng = np.random.default_rng(n_fft * 7 + ch)
+    lens = [n_fft * 5 + 3, n_fft * 23 + 101, n_fft + 1, n_fft * 9]
+    if fmt == "f32":
+        tracks = [(rng.standard_normal((n, ch)) * 0.3).astype(np.float32) for n in lens]
+        inf = engine.IN_F32
+    else:
+        tracks = [(rng.standard_normal((n, ch)) * 3000).clip(-32768, 32767).astype(np.int16) for n in lens]
+        inf = engine.IN_S16
+    flat = np.concatenate([t.reshape(-1) for t in tracks])
+    offs = np.cumsum([0] + [t.size for t in tracks[:-1]]).astype(np.uint64)
+    plan = engine.Plan(n_fft, n_fft, n_fft // 4, engine.OUT_AMP_DB, sr=48000)
+    T = engine.Batch.frames_for(plan, lens)
+    din = engine.DeviceBuffer.from_host(flat)
+    rows = []
+    for fold in (False, True):
+        dout = engine.DeviceBuffer(T * plan.row_bins * 4)
+        b = engine.Batch(plan, din, offs, lens, dout, input_format=inf, channels=ch, fold_mono=True,
+                         kernel=3, max_blocks=3)
+        drange = engine.DeviceBuffer(12 * len(lens))
+        if fold:
+            b.set_option(engine.OPT_RANGE, drange.ptr.value)
+        b.run()
+        engine.synchronize()
+        r = dout.to_host(np.float32, (T, plan.row_bins))
+        rows.append(r)
+        if fold:
+            mx, mn, nan = engine.ranges_read(drange, len(lens))
+            for i in range(len(lens)):
+                ri = r[int(b.frame0[i]):int(b.frame0[i + 1])]
+                assert not nan[i] and mx[i] == ri.max() and mn[i] == ri.min(), i
+    assert np.array_equal(rows[0], rows[1])
