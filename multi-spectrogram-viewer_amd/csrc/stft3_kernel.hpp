@@ -353,9 +353,6 @@ stft3_kernel(StftLaunch a, uint64_t fps) {
             if (valid) store_row_b128<L>(crow, sh, region, 2 * F, j);
         } else if constexpr (stage_rows(OK, VAR)) {
             constexpr int KD = (VAR >> 18) & 7;
-            const int kind = KD ? KD : a.out_kind;
-            const bool power = kind == OUT_POWER || kind == OUT_POWER_DB;
-            const bool db = kind == OUT_AMP_DB || kind == OUT_POWER_DB;
             float* frow = static_cast<float*>(a.out) + g * F;
             const int sh = (int)((reinterpret_cast<uintptr_t>(frow) >> 2) & 3);
             float* st = region + sh;
@@ -367,18 +364,37 @@ stft3_kernel(StftLaunch a, uint64_t fps) {
                     r_trk = t;
                 }
             }
-            untangle2<NC, kBatch>(v, j, partner, ub, [&](int k, float xr, float xi) {
-                const float p2 = __builtin_fmaf(xr, xr, xi * xi);
-                // amp dB from |X|^2 (amp_db_of: no v_sqrt); amp / power as is
-                const float val = db ? (power ? db_of(p2, a.log_amin, 1e-36f, 10.0f) : amp_db_of(p2, a.log_amin))
-                                     : (power ? p2 : __builtin_amdgcn_sqrtf(p2));
-                st[k] = val;
-                if (rng) {
-                    r_max = fmaxf(r_max, val);
-                    r_min = fminf(r_min, val);
-                    r_nan |= val != val;
+            // the row's values for kind K (compile time: no per-bin branches). A fixed kind takes
+            // the range ops per VAR bit 21; the run-time kind switches once per frame and always
+            // forms them (committed only with a.trk_range)
+            auto rows = [&](auto kc) {
+                constexpr int K = decltype(kc)::value;
+                constexpr bool power = K == OUT_POWER || K == OUT_POWER_DB;
+                constexpr bool db = K == OUT_AMP_DB || K == OUT_POWER_DB;
+                constexpr bool R = KD ? (VAR & (1 << 21)) != 0 : true;
+                untangle2<NC, kBatch>(v, j, partner, ub, [&](int k, float xr, float xi) {
+                    const float p2 = __builtin_fmaf(xr, xr, xi * xi);
+                    // amp dB from |X|^2 (amp_db_of: no v_sqrt); amp / power as is
+                    const float val = db ? (power ? db_of(p2, a.log_amin, 1e-36f, 10.0f) : amp_db_of(p2, a.log_amin))
+                                         : (power ? p2 : __builtin_amdgcn_sqrtf(p2));
+                    st[k] = val;
+                    if constexpr (R) {
+                        r_max = fmaxf(r_max, val);
+                        r_min = fminf(r_min, val);
+                        r_nan |= val != val;
+                    }
+                });
+            };
+            if constexpr (KD != 0) {
+                rows(std::integral_constant<int, KD>{});
+            } else {
+                switch (a.out_kind) {
+                    case OUT_MAG: rows(std::integral_constant<int, OUT_MAG>{}); break;
+                    case OUT_POWER: rows(std::integral_constant<int, OUT_POWER>{}); break;
+                    case OUT_AMP_DB: rows(std::integral_constant<int, OUT_AMP_DB>{}); break;
+                    default: rows(std::integral_constant<int, OUT_POWER_DB>{}); break;
                 }
-            });
+            }
             wave_lds_sync();
             if (valid) store_row_b128<L>(frow, sh, region, F, j);
         } else {  // lane-wise 4-byte stores

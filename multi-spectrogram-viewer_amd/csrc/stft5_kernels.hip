@@ -609,26 +609,40 @@ stft5_kernel(StftLaunch a, uint64_t fps, int rs) {
         } else {
             static_assert(kStage, "linear kinds stage their rows");
             constexpr int KD = (VAR >> 18) & 7;  // the kind fixed at compile time (0: run time)
-            const int kind = KD ? KD : a.out_kind;
-            const bool power = kind == OUT_POWER || kind == OUT_POWER_DB;
-            const bool db = kind == OUT_AMP_DB || kind == OUT_POWER_DB;
             float* frow = static_cast<float*>(a.out) + g * F;
             const int sh = (int)((reinterpret_cast<uintptr_t>(frow) >> 2) & 3);
             float* stg = region + sh;
-            auto val_of = [&](float xr, float xi) {
-                const float p2 = __builtin_fmaf(xr, xr, xi * xi);
-                // amp dB from |X|^2 (amp_db_of: no v_sqrt); amp / power as is
-                return db ? (power ? db_of(p2, a.log_amin, 1e-36f, 10.0f) : amp_db_of(p2, a.log_amin))
-                          : (power ? p2 : __builtin_amdgcn_sqrtf(p2));
+            // the row for kind K (compile time: no per-bin branches); the run-time kind switches
+            // once per frame
+            auto rows = [&](auto kc) {
+                constexpr int K = decltype(kc)::value;
+                constexpr bool power = K == OUT_POWER || K == OUT_POWER_DB;
+                constexpr bool db = K == OUT_AMP_DB || K == OUT_POWER_DB;
+                auto val_of = [&](float xr, float xi) {
+                    const float p2 = __builtin_fmaf(xr, xr, xi * xi);
+                    // amp dB from |X|^2 (amp_db_of: no v_sqrt); amp / power as is
+                    return db ? (power ? db_of(p2, a.log_amin, 1e-36f, 10.0f) : amp_db_of(p2, a.log_amin))
+                              : (power ? p2 : __builtin_amdgcn_sqrtf(p2));
+                };
+                untangle5<0, 16>(v, lane0, rot, wkb, wj, [&](int k, float xr, float xi, auto) {
+                    stg[k] = val_of(xr, xi);
+                });
+                if (lane0) {
+                    const float2 e0 = v[0];
+                    const float ar = e0.x + e0.x, bi = e0.y + e0.y;
+                    stg[0] = val_of(ar + bi, 0.0f);
+                    stg[NC] = val_of(ar - bi, 0.0f);
+                }
             };
-            untangle5<0, 16>(v, lane0, rot, wkb, wj, [&](int k, float xr, float xi, auto) {
-                stg[k] = val_of(xr, xi);
-            });
-            if (lane0) {
-                const float2 e0 = v[0];
-                const float ar = e0.x + e0.x, bi = e0.y + e0.y;
-                stg[0] = val_of(ar + bi, 0.0f);
-                stg[NC] = val_of(ar - bi, 0.0f);
+            if constexpr (KD != 0) {
+                rows(std::integral_constant<int, KD>{});
+            } else {
+                switch (a.out_kind) {
+                    case OUT_MAG: rows(std::integral_constant<int, OUT_MAG>{}); break;
+                    case OUT_POWER: rows(std::integral_constant<int, OUT_POWER>{}); break;
+                    case OUT_AMP_DB: rows(std::integral_constant<int, OUT_AMP_DB>{}); break;
+                    default: rows(std::integral_constant<int, OUT_POWER_DB>{}); break;
+                }
             }
             wave_lds_sync();
             if (valid) store_row_b128<L>(frow, sh, region, F, j);
