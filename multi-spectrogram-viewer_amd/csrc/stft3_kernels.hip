@@ -112,6 +112,8 @@ static int launch3_c(const StftLaunch& a, hipStream_t s) {
     bool fixed = a.out_kind == OUT_AMP_DB && a.row_alt == 0;
 #ifdef THESIA_EXPERIMENTS
     if (getenv("THESIA_STFT3_RTKIND")) fixed = false;  // A/B: the run-time kind
+    // ablation (ranges not written): the fold's cost
+    if (fixed && getenv("THESIA_STFT3_NOFOLD")) return launch3_k<NC, 1, C, INF, OUT_AMP_DB << 18, WVS>(a, s);
 #endif
     constexpr int KDB = OUT_AMP_DB << 18, KRG = 1 << 21;
     if (fixed)
