@@ -309,7 +309,9 @@ int thesia_batch_create(thesia_plan* plan, const thesia_batch_desc* desc, thesia
     GUARD_END
 }
 int thesia_batch_destroy(thesia_batch* batch) {
-    if (batch) (void)hipDeviceSynchronize();  // see thesia_plan_destroy
+    // no device synchronisation: the batch's only device block (its track tables) was last used
+    // on the stream of its last run, where its release is ordered (engine.hpp, the block cache's
+    // invariant); the caller's input / output buffers stay the caller's
     delete reinterpret_cast<Batch*>(batch);
     return THESIA_OK;
 }

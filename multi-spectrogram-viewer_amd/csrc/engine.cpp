@@ -3,6 +3,7 @@
 
 #include <algorithm>
 #include <cmath>
+#include <cstdio>
 #include <cstdlib>
 #include <map>
 #include <mutex>
@@ -28,16 +29,13 @@ const char* last_error() { return g_err.c_str(); }
 // ------------------------------------------------------------------------------------
 // device buffers / streams
 // ------------------------------------------------------------------------------------
-// The library's block cache (round 5). Rounds 3-4 used a stream-ordered memory pool
-// (hipMemPoolCreate + hipMallocFromPoolAsync / hipFreeAsync) so that add_tracks paid no hipFree
-// (each one synchronises the device: ~160 us, profiles/r03_viewer). On this runtime (ROCm 7.2)
-// kernel writes into pool blocks past the first ~32-64 MiB of a call's allocations were lost
-// (MultiTrack greys of a 16-track call read back as zeros, the images as garbage, an illegal
-// memory access once; scripts/diag_mt_grey5.py), so blocks now come from plain
-// hipMalloc and freed ones are kept here for reuse, keyed by device and size class:
-//   * a block is handed out again only on the stream it was released on (in-order behind the
-//     work that used it) or once an event recorded at its release has completed -- the same
-//     stream-ordering contract as hipFreeAsync;
+// The library's block cache (round 5; replaces the stream-ordered memory pool of rounds 3-4, see
+// DESIGN.md §10.1 for what round 5's lost greys were). Blocks come from plain hipMalloc and
+// freed ones are kept here for reuse, keyed by device and size class, so add_tracks pays no
+// hipFree (each one synchronises the device: ~160 us, profiles/r03_viewer):
+//   * a block is handed out again at once only on the stream of its last use (DevBuf::use: in
+//     order behind that work), on any other stream once an event recorded there at its release
+//     has completed (engine.hpp states the invariant);
 //   * classes are 2^k and 3 * 2^(k-2) (<= 33 % slack) up to 64 MiB, whole 2 MiB steps above;
 //   * the cache holds at most kCacheCap bytes per device (a release past it is a hipFree) and
 //     is emptied by trim_pool() (thesia_pool_trim, MultiTrack destruction, and before a failed
@@ -77,17 +75,47 @@ int current_device() {
 }
 }  // namespace
 
+#ifdef THESIA_POOL_DIAG
+// Diagnostic build only (scripts/build_variant.sh pooldiag "-DTHESIA_POOL_DIAG" engine.cpp; round 6,
+// VERDICT r05 item 1): the rounds 3-4 allocator (the library's own stream-ordered pool,
+// hipMallocFromPoolAsync / hipFreeAsync on the allocation stream), every allocation and release
+// logged to stderr with its stream, so a failing call's block lifetimes can be read back.
+static hipMemPool_t diag_pool() {
+    static hipMemPool_t pool = [] {
+        hipMemPool_t q = nullptr;
+        hipMemPoolProps props{};
+        props.allocType = hipMemAllocationTypePinned;
+        props.handleTypes = hipMemHandleTypeNone;
+        props.location.type = hipMemLocationTypeDevice;
+        props.location.id = 0;
+        if (hipMemPoolCreate(&q, &props) != hipSuccess) return (hipMemPool_t) nullptr;
+        uint64_t thr = ~uint64_t(0);
+        (void)hipMemPoolSetAttribute(q, hipMemPoolAttrReleaseThreshold, &thr);
+        return q;
+    }();
+    return pool;
+}
+#endif
+
 void DevBuf::release() {
     if (!p) return;
+#ifdef THESIA_POOL_DIAG
+    fprintf(stderr, "POOLDIAG free %p %zu st %p\n", p, bytes, (void*)st);
+    (void)hipFreeAsync(p, st);
+    p = nullptr;
+    bytes = 0;
+    return;
+#endif
     if (pooled) {
         const size_t cap = cache_class(bytes);
         std::lock_guard<std::mutex> g(g_cache_mu);
         DevCache& c = g_cache[dev];
         c.live -= cap;
         hipEvent_t ev = nullptr;
+        hipStream_t last = use ? use : st;
         if (c.cached + cap <= kCacheCap && hipEventCreateWithFlags(&ev, hipEventDisableTiming) == hipSuccess &&
-            hipEventRecord(ev, st) == hipSuccess) {
-            c.free.push_back(CachedBlock{p, cap, st, ev});
+            hipEventRecord(ev, last) == hipSuccess) {
+            c.free.push_back(CachedBlock{p, cap, last, ev});
             c.cached += cap;
         } else {
             (void)hipGetLastError();
@@ -99,6 +127,7 @@ void DevBuf::release() {
     }
     p = nullptr;
     bytes = 0;
+    use = nullptr;
 }
 
 int trim_pool() {
@@ -134,6 +163,21 @@ int DevBuf::alloc(size_t n) {
     if (n == 0) n = 16;
     hipStream_t s = default_stream();
     const int d = current_device();
+#ifdef THESIA_POOL_DIAG
+    {
+        const hipError_t e = hipMallocFromPoolAsync(&p, n, diag_pool(), s);
+        fprintf(stderr, "POOLDIAG alloc %p %zu st %p rc %d\n", p, n, (void*)s, (int)e);
+        if (e != hipSuccess) {
+            p = nullptr;
+            return set_error(THESIA_ERR_DEVICE, "hipMallocFromPoolAsync failed");
+        }
+        pooled = true;
+        dev = d;
+        st = s;
+        bytes = n;
+        return THESIA_OK;
+    }
+#endif
     const size_t cap = cache_class(n);
     {
         std::lock_guard<std::mutex> g(g_cache_mu);
@@ -173,6 +217,7 @@ int DevBuf::alloc(size_t n) {
     pooled = true;
     dev = d;
     st = s;
+    use = nullptr;
     bytes = n;
     return THESIA_OK;
 }
@@ -193,21 +238,18 @@ bool host_pinned(const void* p) {
     return a.type == hipMemoryTypeHost;
 }
 
-// A blocking copy ordered after everything already enqueued on the library stream (a plain
-// hipMemcpy runs on the null stream, which does not wait for the non-blocking library stream).
-// Page-locked host memory: an async copy on the library stream + its synchronisation. Pageable
-// host memory: the runtime stages such a copy and its DMA is not ordered with the library stream
-// (round 5: MultiTrack uploads of pageable PCM into pool buffers were still landing after the
-// stream's synchronisation -- grey images overwritten after they were formed, and an illegal
-// memory access once the pool reused / trimmed the block); so the stream is drained first, the
-// copy is the blocking hipMemcpy, and the device is synchronised after it.
+// A copy ordered after everything already enqueued on stream s. Page-locked host memory (or
+// device to device): an async copy on s. Pageable host memory: the same async copy on s, then s is
+// synchronised, so the caller may reuse or free the host range when this returns. (Round 5 had
+// the pageable case drain s, make a blocking null-stream copy and synchronise the whole device,
+// after a diagnosis that blamed the ordering of pageable copies for lost greys; round 6's probe,
+// scripts/probes/pool_probe.hip, found pageable uploads on a non-blocking stream ordered with the
+// kernels behind them, 4 x 92 MiB, profiles/r06_pool/pool_probe.txt.)
 hipError_t copy_on(void* dst, const void* src, size_t bytes, hipMemcpyKind kind, hipStream_t s) {
     if (!bytes) return hipSuccess;
     const void* host = kind == hipMemcpyHostToDevice ? src : kind == hipMemcpyDeviceToHost ? dst : nullptr;
-    if (!host || host_pinned(host)) return hipMemcpyAsync(dst, src, bytes, kind, s);
-    hipError_t e = hipStreamSynchronize(s);
-    if (e == hipSuccess) e = hipMemcpy(dst, src, bytes, kind);
-    if (e == hipSuccess && kind == hipMemcpyHostToDevice) e = hipDeviceSynchronize();
+    hipError_t e = hipMemcpyAsync(dst, src, bytes, kind, s);
+    if (e == hipSuccess && host && !host_pinned(host)) e = hipStreamSynchronize(s);
     return e;
 }
 
@@ -978,6 +1020,9 @@ int batch_set_option(Batch* b, int option, int64_t value) {
 
 int batch_run(Batch* b, hipStream_t s) {
     if (!s) s = default_stream();
+#ifndef THESIA_DIAG_NO_LAST_USE  // (diagnostic build: the round-5 cache, for the test's control)
+    b->d_tabs.used_on(s);  // the kernels read the track tables on s: a release is ordered there
+#endif
     // per-track output ranges: folded into stft3's staged-row epilogue (linear kinds), else one
     // reduction pass over the rows after the spectrogram launch
     const uint64_t n_tr = b->frame0.empty() ? 0 : b->frame0.size() - 1;
@@ -991,8 +1036,11 @@ int batch_run(Batch* b, hipStream_t s) {
         rc = launch_stftx(b->launch, s);
         if (rc) return set_error(rc == -2 ? THESIA_ERR_UNSUPPORTED : THESIA_ERR_DEVICE, "stftx launch failed");
     } else if (b->kernel == 7) {
-        rc = b->plan->n_fft == 2048 ? launch_stftr(b->launch, s) : launch_stftq(b->launch, s);
-        if (rc) return set_error(rc == -2 ? THESIA_ERR_UNSUPPORTED : THESIA_ERR_DEVICE, "stftr launch failed");
+        const bool r = b->plan->n_fft == 2048;
+        rc = r ? launch_stftr(b->launch, s) : launch_stftq(b->launch, s);
+        if (rc)
+            return set_error(rc == -2 ? THESIA_ERR_UNSUPPORTED : THESIA_ERR_DEVICE,
+                             r ? "stftr launch failed" : "stftq launch failed");
     } else {
         if (b->kernel == 5) rc = launch_stft5(b->launch, s);
         if (rc == -2 && b->kernel >= 3) {
@@ -1107,6 +1155,7 @@ int batches_run(Batch* const* b, size_t n, hipStream_t s) {
         b[i]->launch.grid_share = keep;
     }
     const int jrc = p->join_into(s, k);  // join even after an error: `s` never runs ahead of them
+    for (size_t i = 0; i < n; ++i) b[i]->d_tabs.used_on(s);  // the forks are joined into s
     return rc ? rc : jrc;
 }
 

@@ -28,28 +28,37 @@ const char* last_error();
     } while (0)
 
 // ---- device buffer (move-only RAII) ----
-// hipMalloc'd blocks kept by the library's block cache (engine.cpp) once released: a release is
-// stream-ordered on the library stream it was allocated on (an event, no device
-// synchronisation: a hipFree costs ~160 us, profiles/r03_viewer), and the block is handed out
-// again to the next allocation of its size class on that stream (or on any stream once the
-// event has completed).
+// hipMalloc'd blocks kept by the library's block cache (engine.cpp) once released: a release
+// costs no device synchronisation (a hipFree costs ~160 us, profiles/r03_viewer).
+//
+// The cache's invariant (round 6): a block may be handed out again only after every use of it
+// has been ordered before the next user's work. A DevBuf therefore records the stream of its
+// last use (`use`, the allocation stream until used_on() names another); its release records an
+// event on that stream, and the cache hands the block out again at once only to an allocation on
+// that same stream (in-order behind the uses), to any other stream only once the event has
+// completed. Work on other streams must be joined into the last-use stream before the release
+// (the library's stream pool joins its forks back into the caller's stream; batch_run /
+// batches_run call used_on(s) for the batch's track tables). tests/test_gpu_multitrack.py
+// test_block_cache_cross_stream_reuse checks a block released while a kernel on a busy caller
+// stream still reads it.
 struct DevBuf {
     void* p = nullptr;
     size_t bytes = 0;
-    hipStream_t st = nullptr;  // the stream its allocation (and so its release) is ordered on
-    bool pooled = false;       // a block of the cache (else a plain hipFree on release)
-    int dev = 0;               // the device it was allocated on
+    hipStream_t st = nullptr;   // the stream it was allocated on
+    hipStream_t use = nullptr;  // the stream of its last use (nullptr: st)
+    bool pooled = false;        // a block of the cache (else a plain hipFree on release)
+    int dev = 0;                // the device it was allocated on
     DevBuf() = default;
     DevBuf(const DevBuf&) = delete;
     DevBuf& operator=(const DevBuf&) = delete;
-    DevBuf(DevBuf&& o) noexcept : p(o.p), bytes(o.bytes), st(o.st), pooled(o.pooled), dev(o.dev) {
+    DevBuf(DevBuf&& o) noexcept : p(o.p), bytes(o.bytes), st(o.st), use(o.use), pooled(o.pooled), dev(o.dev) {
         o.p = nullptr;
         o.bytes = 0;
     }
     DevBuf& operator=(DevBuf&& o) noexcept {
         if (this != &o) {
             release();
-            p = o.p; bytes = o.bytes; st = o.st; pooled = o.pooled; dev = o.dev;
+            p = o.p; bytes = o.bytes; st = o.st; use = o.use; pooled = o.pooled; dev = o.dev;
             o.p = nullptr; o.bytes = 0;
         }
         return *this;
@@ -58,6 +67,8 @@ struct DevBuf {
     void release();
     int alloc(size_t n);
     int upload(const void* host, size_t n);  // alloc + copy (synchronous)
+    // the block's work now runs on (or is joined into) stream s: its release is ordered there
+    void used_on(hipStream_t s) { use = s; }
     template <class T> T* as() const { return static_cast<T*>(p); }
 };
 
@@ -68,8 +79,9 @@ int trim_pool();
 int pool_bytes(uint64_t* reserved, uint64_t* used);
 hipError_t copy_ordered(void* dst, const void* src, size_t bytes, hipMemcpyKind kind);
 bool host_pinned(const void* p);  // page-locked (hipHostMalloc / hipHostRegister) host memory
-// a copy on stream s: async where the host side is page-locked (or device to device); a pageable
-// host side takes the blocking copy after s drains (+ a device synchronisation for uploads)
+// a copy on stream s: async where the host side is page-locked (or device to device); with a
+// pageable host side the copy is enqueued on s and s is synchronised before the call returns
+// (the host range may be reused at once; nothing else in the process waits)
 hipError_t copy_on(void* dst, const void* src, size_t bytes, hipMemcpyKind kind, hipStream_t s);
 
 // ---- plan ----

@@ -83,6 +83,11 @@ int MultiTrack::make_plan(const Track& tr, Plan** out) const {
 int MultiTrack::add_tracks(const std::vector<uint64_t>& ids, const std::vector<PcmIn>& pcm,
                            int* changed) {
     const hipStream_t s = default_stream();
+    // the call's uploads read the caller's sample buffers: whatever path returns, s has drained
+    struct Drain {
+        hipStream_t s;
+        ~Drain() { (void)hipStreamSynchronize(s); }
+    } drain{s};
     // 1) validate every new track before any device work (the reference returns Err mid-loop,
     //    lib.rs:174-177, leaving earlier tracks inserted without specs; here an error at any
     //    step changes nothing)
@@ -154,25 +159,17 @@ int MultiTrack::add_tracks(const std::vector<uint64_t>& ids, const std::vector<P
         if (!rc) rc = wav->alloc(std::max<uint64_t>(wf, 1) * sizeof(float));
         if (!rc) rc = spec->alloc(std::max<uint64_t>(T_all * g.bins, 1) * sizeof(float));
         if (rc) return rc;
-        // uploads: page-locked sources (the file path's staging) as async copies on the library
-        // stream; pageable ones (decoded PCM handed in by the caller) by the blocking copy after
-        // the stream has drained, then a device synchronisation before any kernel reads them
-        // (copy_ordered: a pageable copy's DMA is not ordered with the library stream)
-        bool pageable = false;
+        // uploads: async copies on the library stream, page-locked sources (the file path's
+        // staging) and pageable ones (decoded PCM handed in by the caller) alike -- stream-ordered
+        // with the decodes behind them (round 6 probe); every return below runs
+        // after `drain` has synchronised s, so no copy outlives the caller's buffers
         for (size_t k = 0; k < idx.size(); ++k) {
             const PcmIn& in = pcm[idx[k]];
             const uint64_t bytes = in.n_samples * in.channels * pcm_bytes(in.kind);
             uint8_t* dst = raw.as<uint8_t>() + roff[k];
             if (!bytes) continue;
-            if (host_pinned(in.data)) {
-                THESIA_HIP(hipMemcpyAsync(dst, in.data, bytes, hipMemcpyHostToDevice, s));
-            } else {
-                if (!pageable) THESIA_HIP(hipStreamSynchronize(s));
-                pageable = true;
-                THESIA_HIP(hipMemcpy(dst, in.data, bytes, hipMemcpyHostToDevice));
-            }
+            THESIA_HIP(hipMemcpyAsync(dst, in.data, bytes, hipMemcpyHostToDevice, s));
         }
-        if (pageable) THESIA_HIP(hipDeviceSynchronize());
         for (size_t k = 0; k < idx.size(); ++k) {
             const PcmIn& in = pcm[idx[k]];
             uint8_t* dst = raw.as<uint8_t>() + roff[k];

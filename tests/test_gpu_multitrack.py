@@ -184,6 +184,59 @@ def test_block_cache(excerpts, tmp_path):
     assert res.value == used.value == base_used
 
 
+def test_block_cache_cross_stream_reuse():
+    """Round 6: the block cache's invariant (engine.hpp DevBuf). Batch A's
+    track tables are a cached block read by A's kernel on a caller stream that is still busy (10
+    x 128 MiB device copies queued ahead of it); A is destroyed at once (no synchronisation), and
+    batch B -- same table size class, other tracks -- is created and run on the library stream
+    while A's kernel has not started. The cache may not hand A's block to B until the work on
+    the stream of its last use (the caller stream) is done: A's rows must equal A run alone."""
+    import ctypes as C
+    from thesia import engine
+
+    hip = C.CDLL("libamdhip64.so.7")  # the runtime libthesia is linked against (same handle)
+    s2 = C.c_void_p()
+    assert hip.hipStreamCreateWithFlags(C.byref(s2), 1) == 0  # hipStreamNonBlocking
+    sr, n_fft, hop = 48000, 2048, 512
+    plan = engine.Plan(n_fft, n_fft, hop, engine.OUT_AMP_DB, sr=sr)
+    rng = np.random.default_rng(6)
+    lens_a, lens_b = [48000, 36000, 60000], [20000, 90000, 41000]
+    x = (rng.standard_normal(sum(lens_a) + sum(lens_b)) * 0.2).astype(np.float32)
+    din = engine.DeviceBuffer.from_host(x)
+    off_a = np.cumsum([0] + lens_a[:-1])
+    off_b = sum(lens_a) + np.cumsum([0] + lens_b[:-1])
+    fa = engine.Batch.frames_for(plan, lens_a)
+    fb = engine.Batch.frames_for(plan, lens_b)
+    bins = plan.row_bins
+    ref = engine.DeviceBuffer(fa * bins * 4)
+    b0 = engine.Batch(plan, din, off_a, lens_a, ref)
+    b0.run()
+    engine.synchronize()
+    want = ref.to_host(np.float32, (fa, bins))
+    b0.close()
+    big = 128 << 20
+    src, dst = engine.DeviceBuffer(big), engine.DeviceBuffer(big)
+    out_a = engine.DeviceBuffer(fa * bins * 4)
+    out_b = engine.DeviceBuffer(fb * bins * 4)
+    out_a.zero()
+    for _ in range(10):  # keep s2 busy: A's kernel starts only after these
+        assert hip.hipMemcpyAsync(dst.ptr, src.ptr, C.c_size_t(big), 3, s2) == 0  # D2D
+    ba = engine.Batch(plan, din, off_a, lens_a, out_a)
+    ba.run(stream=s2)
+    ba.close()  # released while its kernel is still queued on s2
+    bb = engine.Batch(plan, din, off_b, lens_b, out_b)  # same 4 KiB table class
+    bb.run()
+    engine.synchronize()
+    assert hip.hipStreamSynchronize(s2) == 0
+    got = out_a.to_host(np.float32, (fa, bins))
+    bb.close()
+    assert hip.hipStreamDestroy(s2) == 0
+    for b in (src, dst, out_a, out_b, ref, din):
+        b.close()
+    plan.close()
+    assert np.array_equal(got, want)
+
+
 @pytest.mark.parametrize("fast", [False, True])
 @pytest.mark.parametrize("scale", [thesia.FreqScale.Mel, thesia.FreqScale.Linear])
 def test_greys_of_a_many_track_call(fast, scale):
