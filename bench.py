@@ -671,7 +671,7 @@ def main_c5(args, ws, rank, pg, device):
             "config": {"workload": f"C5: {total} mixed-rate tracks (8-48 kHz) x {args.seconds:g} s, "
                                    f"n_fft 256-2048 per track, hop n_fft/4, amp dB + global range + "
                                    f"grey + Lanczos3 + colormap RGB at 100 px/s x 500 px",
-                       "ranks": ws, "per_rank_frames": summ["per_rank_frames"],
+                       "ranks": ws, "devices": summ["devices"], "per_rank_frames": summ["per_rank_frames"],
                        "tracks_per_gpu": len(tracks), "images_per_s": total / dt,
                        "spectrogram_batches": len(p.groups), "display_groups": p._n_disp,
                        "frames_per_gpu": p.total_frames,

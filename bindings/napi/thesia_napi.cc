@@ -115,6 +115,16 @@ bool uint_arg(napi_env env, napi_value v, double max, const char* name, double* 
 }
 constexpr double kU32Max = 4294967295.0;
 constexpr double kLenMax = 268435456.0;  // 2^28 elements: sizes beyond this are refused up front
+// the largest image the addon hands to JS (a Uint8Array of at most 2^31 - 1 bytes, node 12's
+// typed-array limit): a coerced nheight of ~2^32 (a negative height wraps, as wasm-bindgen's u32
+// does) would otherwise size a multi-terabyte host buffer before the library is asked for it
+constexpr size_t kImageMax = 2147483647u;
+bool image_fits(napi_env env, size_t need) {
+    if (need <= kImageMax) return true;
+    napi_throw_range_error(env, "ERR_ARG", ("image of " + std::to_string(need) +
+                                            " bytes: at most 2147483647 accepted").c_str());
+    return false;
+}
 
 bool id_arg(napi_env env, napi_value v, uint64_t* id) {
     double d = 0;
@@ -332,6 +342,7 @@ napi_value MtGetSpecImage(napi_env env, napi_callback_info info) {
     size_t need = 0;
     int rc = thesia_mt_get_spec_image(h, id, (float)pps, (uint32_t)nh, nullptr, 0, &need);
     if (rc != THESIA_OK && rc != THESIA_ERR_BUFFER_TOO_SMALL) return throw_thesia(env, rc);
+    if (!image_fits(env, need)) return nullptr;
     std::vector<uint8_t> buf(need);
     rc = thesia_mt_get_spec_image(h, id, (float)pps, (uint32_t)nh, buf.data(), buf.size(), &need);
     if (rc != THESIA_OK) return throw_thesia(env, rc);
@@ -350,6 +361,7 @@ napi_value MtGetWavImage(napi_env env, napi_callback_info info) {
     size_t need = 0;
     int rc = thesia_mt_get_wav_image(h, id, (float)pps, (uint32_t)nh, (float)amin, (float)amax, nullptr, 0, &need);
     if (rc != THESIA_OK && rc != THESIA_ERR_BUFFER_TOO_SMALL) return throw_thesia(env, rc);
+    if (!image_fits(env, need)) return nullptr;
     std::vector<uint8_t> buf(need);
     rc = thesia_mt_get_wav_image(h, id, (float)pps, (uint32_t)nh, (float)amin, (float)amax, buf.data(),
                                  buf.size(), &need);

@@ -190,12 +190,14 @@ int MultiTrack::add_tracks(const std::vector<uint64_t>& ids, const std::vector<P
         rc = batch_create(plan, bd, &b);
         if (rc) return rc;
         g.batch.reset(b);
-        // the viewer path computes in the reference's operation order (stftx_kernel): its
-        // images are the oracle pipeline's bytes; opt-in (set_fast): the automatic streaming
-        // kernel (stft3 at the viewer geometries; stft5 for the 48 kHz rows of batches of
-        // >= 400 000 frames), held to the e2e contract relative to the reference's own f32
-        // error (tests/test_gpu_parity.py _check_multitrack)
-        rc = batch_set_option(b, THESIA_BATCH_OPT_KERNEL, fast_ ? 0 : 9);
+        // the viewer path computes in the reference's operation order: kernel 7 (stftq / stftr,
+        // round 6: at the viewer's own geometries too, each frame loading its samples) where it
+        // runs the plan, else stftx (one wave per frame); its images are the oracle pipeline's
+        // bytes. Opt-in (set_fast): the automatic streaming kernel (stft3 at the viewer
+        // geometries; stft5 for the 48 kHz rows of batches of >= 400 000 frames), held to the e2e
+        // contract relative to the reference's own f32 error (tests/test_gpu_parity.py
+        // _check_multitrack)
+        rc = batch_set_option(b, THESIA_BATCH_OPT_KERNEL, fast_ ? 0 : b->kr_ok ? 7 : 9);
         if (!rc) rc = batch_run(b, s);
         if (rc) return rc;
         g.spec = spec->as<float>();

@@ -251,7 +251,14 @@ constexpr int reg_pbits(int r, int ps) {
 // ablations of the experiment library only (wrong output by design): 1 |X| by the f32 sqrt, 2 dB
 // by v_log_f32, 4 no untangle / epilogue (the FFT and the Z row alone); 16 (exact, A/B): every
 // swap as lane exchanges instead of the LDS relayout.
-template <int NC, int KIND, int C, int INF, int WV, int VAR = 0>
+// DIR (round 6): any other geometry -- the viewer's win < n_fft and hops (lib.rs:43-46: 80 / 160 / 221 /
+// 240 at n_fft 512 / 1024) -- with the same FFT and epilogue: every frame loads its n_fft samples
+// itself (no ring: L2 holds the overlap; an odd start, where the frame's points straddle the
+// sample pairs, reads its samples one by one), and the window step adds a per-position constant
+// after the product: -0 inside the window (x * w + -0 = x * w, bits unchanged), +0 in the
+// centring pads, where the reference's frame holds +0 (lib.rs:377-385 pads the windowed frame:
+// x * 0 alone would be -0 for x < 0).
+template <int NC, int KIND, int C, int INF, int WV, int VAR = 0, bool DIR = false>
 __global__ void __launch_bounds__(64 * WV)
 stftq_kernel(StftLaunch a, uint64_t fps) {
     constexpr int OKQ = KIND == OUT_COMPLEX ? 0 : (KIND == OUT_MEL || KIND == OUT_MEL_AMP_DB) ? 2 : 1;
@@ -266,7 +273,8 @@ stftq_kernel(StftLaunch a, uint64_t fps) {
     float* wtl = lds;
     float2* twl = reinterpret_cast<float2*>(lds + G::WL_FLOATS);
     float2* scl = reinterpret_cast<float2*>(lds + G::WL_FLOATS + G::TW_FLOATS);
-    float* work = lds + G::TAB_FLOATS;
+    float* wcl = lds + G::TAB_FLOATS;  // DIR: the window step's added constants (same layout)
+    float* work = lds + G::TAB_FLOATS + (DIR ? G::WL_FLOATS : 0);
     const exact::LogfEntry* logt = logf_tab_to_lds(lds + G::WL_FLOATS + G::TW_FLOATS + G::SC_FLOATS);
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int slot = lane / L;
@@ -275,6 +283,7 @@ stftq_kernel(StftLaunch a, uint64_t fps) {
     for (int i = threadIdx.x; i < 2 * NC; i += kBlock) {  // window: lane row (w[2m], w[2m+1])
         const int m = i >> 1, l = m % L, n = m / L;
         wtl[l * G::WL_STRIDE + 2 * n + (i & 1)] = a.wpad[i];
+        if constexpr (DIR) wcl[l * G::WL_STRIDE + 2 * n + (i & 1)] = i >= a.pad_left && i < a.pad_left + a.win ? -0.0f : 0.0f;
     }
     for (int i = threadIdx.x; i < NC; i += kBlock) {
         twl[i] = a.tw1[i];
@@ -315,7 +324,15 @@ stftq_kernel(StftLaunch a, uint64_t fps) {
             start = (int64_t)(g - g_beg) * hop - NC;  // t hop - win / 2 (pad_left = 0)
         }
         // ---- the frame's downmixed samples: ring shift by SH rows + the prefetched hop ----
-        if (pre_ok) {
+        if (DIR && valid && start >= 0 && start + 2 * NC <= n && ((base + (uint64_t)start * C) % (2 * C)) != 0) {
+            // (DIR) an interior frame at an odd start: sample by sample
+#pragma unroll
+            for (int q = 0; q < P; ++q) {
+                const int64_t i0 = start + 2 * (lj + L * q);
+                raw[q] = make_float2(read_sample<INF>(a.in, base, i0, C, a.fold != 0),
+                                     read_sample<INF>(a.in, base, i0 + 1, C, a.fold != 0));
+            }
+        } else if (pre_ok) {
 #pragma unroll
             for (int q = 0; q < KEEP; ++q) raw[q] = raw[q + SH];
 #pragma unroll
@@ -344,7 +361,7 @@ stftq_kernel(StftLaunch a, uint64_t fps) {
         // ---- prefetch the next frame's new points (rows KEEP .. P - 1) ----
         {
             const int64_t nstart = start + hop;
-            const bool nxt = valid && g + 1 < g1 && g + 1 < g_end && nstart + 2 * NC <= n &&
+            const bool nxt = !DIR && valid && g + 1 < g1 && g + 1 < g_end && nstart + 2 * NC <= n &&
                              nstart + 2 * L * KEEP >= 0 &&
                              ((base + (uint64_t)(nstart + 2 * L * KEEP) * C) % (2 * C)) == 0;
             if (nxt) {
@@ -363,6 +380,15 @@ stftq_kernel(StftLaunch a, uint64_t fps) {
                 const float4 w = wr[q];
                 v[2 * q] = make_float2(raw[2 * q].x * w.x, raw[2 * q].y * w.y);
                 v[2 * q + 1] = make_float2(raw[2 * q + 1].x * w.z, raw[2 * q + 1].y * w.w);
+            }
+            if constexpr (DIR) {  // -0 inside the window (bits unchanged), +0 in the pads
+                const float4* cr = reinterpret_cast<const float4*>(wcl + lj * G::WL_STRIDE);
+#pragma unroll
+                for (int q = 0; q < P / 2; ++q) {
+                    const float4 c = cr[q];
+                    v[2 * q] = make_float2(v[2 * q].x + c.x, v[2 * q].y + c.y);
+                    v[2 * q + 1] = make_float2(v[2 * q + 1].x + c.z, v[2 * q + 1].y + c.w);
+                }
             }
         }
         // ---- rustfft Radix4 on the schedule ----
@@ -553,11 +579,11 @@ stftq_kernel(StftLaunch a, uint64_t fps) {
 // host side
 // ------------------------------------------------------------------------------------------
 template <int NC>
-static int ldsq_bytes(int wv) {
-    return (GeoQ<NC>::TAB_FLOATS + wv * GeoQ<NC>::FPW * GeoQ<NC>::RS) * 4;
+static int ldsq_bytes(int wv, bool dir = false) {
+    return (GeoQ<NC>::TAB_FLOATS + (dir ? GeoQ<NC>::WL_FLOATS : 0) + wv * GeoQ<NC>::FPW * GeoQ<NC>::RS) * 4;
 }
 
-template <int NC, int KIND, int C, int INF, int WV, int VAR = 0>
+template <int NC, int KIND, int C, int INF, int WV, int VAR = 0, bool DIR = false>
 static int launchq_k(const StftLaunch& a, hipStream_t s) {
 #ifdef THESIA_EXPERIMENTS
     if constexpr (VAR == 0 && KIND == OUT_AMP_DB && C == 1 && INF == IN_S16) {
@@ -570,9 +596,9 @@ static int launchq_k(const StftLaunch& a, hipStream_t s) {
         if (v == 16) return launchq_k<NC, KIND, C, INF, WV, 16>(a, s);
     }
 #endif
-    const int lds = ldsq_bytes<NC>(WV);
+    const int lds = ldsq_bytes<NC>(WV, DIR);
     if (lds > 163840) return -2;
-    auto kern = stftq_kernel<NC, KIND, C, INF, WV, VAR>;
+    auto kern = stftq_kernel<NC, KIND, C, INF, WV, VAR, DIR>;
     if (hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize, lds) !=
         hipSuccess)
         return -1;
@@ -587,7 +613,7 @@ static int launchq_k(const StftLaunch& a, hipStream_t s) {
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
-template <int NC, int C, int INF>
+template <int NC, int C, int INF, bool DIR = false>
 static int launchq_c(const StftLaunch& a, hipStream_t s) {
     if ((a.out_kind == OUT_MEL || a.out_kind == OUT_MEL_AMP_DB) && (!a.xmel_band || !a.xmel_w)) return -2;
     // 16-wave blocks (4 waves / SIMD, <= 128 VGPRs) for n_fft 512 / 1024: 3.59 -> 3.48 and 3.88
@@ -595,30 +621,39 @@ static int launchq_c(const StftLaunch& a, hipStream_t s) {
     // profiles/r05_stftq/ablations.txt)
     constexpr int WV = NC == 128 ? 12 : 16;
     switch (a.out_kind) {
-        case OUT_COMPLEX: return launchq_k<NC, OUT_COMPLEX, C, INF, WV>(a, s);
-        case OUT_MAG: return launchq_k<NC, OUT_MAG, C, INF, WV>(a, s);
-        case OUT_POWER: return launchq_k<NC, OUT_POWER, C, INF, WV>(a, s);
-        case OUT_AMP_DB: return launchq_k<NC, OUT_AMP_DB, C, INF, WV>(a, s);
-        case OUT_POWER_DB: return launchq_k<NC, OUT_POWER_DB, C, INF, WV>(a, s);
-        case OUT_MEL: return launchq_k<NC, OUT_MEL, C, INF, WV>(a, s);
-        case OUT_MEL_AMP_DB: return launchq_k<NC, OUT_MEL_AMP_DB, C, INF, WV>(a, s);
+        case OUT_COMPLEX: return launchq_k<NC, OUT_COMPLEX, C, INF, WV, 0, DIR>(a, s);
+        case OUT_MAG: return launchq_k<NC, OUT_MAG, C, INF, WV, 0, DIR>(a, s);
+        case OUT_POWER: return launchq_k<NC, OUT_POWER, C, INF, WV, 0, DIR>(a, s);
+        case OUT_AMP_DB: return launchq_k<NC, OUT_AMP_DB, C, INF, WV, 0, DIR>(a, s);
+        case OUT_POWER_DB: return launchq_k<NC, OUT_POWER_DB, C, INF, WV, 0, DIR>(a, s);
+        case OUT_MEL: return launchq_k<NC, OUT_MEL, C, INF, WV, 0, DIR>(a, s);
+        case OUT_MEL_AMP_DB: return launchq_k<NC, OUT_MEL_AMP_DB, C, INF, WV, 0, DIR>(a, s);
         default: return -2;
     }
 }
 
+// the canonical C5 geometry streams (win = n_fft, hop = n_fft / 4); any other (DIR) loads per frame
+static bool q_canon(const StftLaunch& a) { return a.win == a.n_fft && a.hop * 4 == a.n_fft; }
+
 template <int NC>
 static int launchq_n(const StftLaunch& a, hipStream_t s) {
+    if (!q_canon(a))  // the viewer's geometries: f32 mono / stereo (MultiTrack's mono pool)
+        return a.channels == 2 ? launchq_c<NC, 2, IN_F32, true>(a, s) : launchq_c<NC, 1, IN_F32, true>(a, s);
     if (a.in_format == IN_S16) return a.channels == 2 ? launchq_c<NC, 2, IN_S16>(a, s) : launchq_c<NC, 1, IN_S16>(a, s);
     return a.channels == 2 ? launchq_c<NC, 2, IN_F32>(a, s) : launchq_c<NC, 1, IN_F32>(a, s);
 }
 
 bool stftq_supports(int n_fft, int win, int hop, int in_format, int channels) {
-    return (n_fft == 256 || n_fft == 512 || n_fft == 1024) && win == n_fft && hop * 4 == n_fft &&
-           (in_format == IN_F32 || in_format == IN_S16) && (channels == 1 || channels == 2);
+    if (!(n_fft == 256 || n_fft == 512 || n_fft == 1024) || !(channels == 1 || channels == 2)) return false;
+    if (win == n_fft && hop * 4 == n_fft) return in_format == IN_F32 || in_format == IN_S16;
+    // any other geometry (DIR): even win <= n_fft (the frame start t hop - n_fft / 2 is the
+    // reference's t hop - win / 2 - pad_left, lib.rs:400-401), f32
+    return in_format == IN_F32 && hop >= 1 && win >= 2 && win <= n_fft && win % 2 == 0;
 }
 
 int stftq_lds_bytes(const StftLaunch& a) {
-    return a.n_fft == 256 ? ldsq_bytes<128>(12) : a.n_fft == 512 ? ldsq_bytes<256>(16) : ldsq_bytes<512>(16);
+    const bool dir = !q_canon(a);
+    return a.n_fft == 256 ? ldsq_bytes<128>(12, dir) : a.n_fft == 512 ? ldsq_bytes<256>(16, dir) : ldsq_bytes<512>(16, dir);
 }
 
 int launch_stftq(const StftLaunch& a, hipStream_t s) {

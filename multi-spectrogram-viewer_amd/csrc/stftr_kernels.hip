@@ -121,7 +121,11 @@ __device__ __forceinline__ void melr_stream(const int4* meta, const float4* wt, 
 // 12 (3 waves per SIMD) or 8 (when the mel tables leave no room for 12 regions). VAR: ablations
 // of the experiment library only (wrong output by design): 1 |X| by the f32 sqrt, 2 no mel
 // stream, 4 no untangle / |X| / mel (the FFT alone).
-template <int KIND, int C, int INF, int WV, int VAR = 0>
+// DIR (round 6): any other geometry with n_fft 2048 -- the viewer's win 1764 / 1920 and hops 441 /
+// 480 (lib.rs:43-46, 44.1 / 48 kHz) -- as stftq_kernel's DIR: every frame loads its samples itself
+// (no ring; an odd start sample by sample) and the window step adds -0 inside the window, +0 in
+// the centring pads (the reference pads the windowed frame with +0, lib.rs:377-385).
+template <int KIND, int C, int INF, int WV, int VAR = 0, bool DIR = false>
 __global__ void __launch_bounds__(64 * WV)
 stftr_kernel(StftLaunch a, uint64_t fps) {
     using G = GeoR;
@@ -136,7 +140,8 @@ stftr_kernel(StftLaunch a, uint64_t fps) {
     float* wtl = lds;
     float2* twl = reinterpret_cast<float2*>(lds + G::WL_FLOATS);
     float2* scl = reinterpret_cast<float2*>(lds + G::WL_FLOATS + G::TW_FLOATS);
-    float* work = lds + G::TAB_FLOATS;
+    float* wcl = lds + G::TAB_FLOATS;  // DIR: the window step's added constants (same layout)
+    float* work = lds + G::TAB_FLOATS + (DIR ? G::WL_FLOATS : 0);
     const exact::LogfEntry* logt = logf_tab_to_lds(lds + G::WL_FLOATS + G::TW_FLOATS + G::SC_FLOATS);
     int4* pm_lds = reinterpret_cast<int4*>(work + WV * G::REGION);
     float4* pw_lds = reinterpret_cast<float4*>(pm_lds + (MEL ? (a.melr_chunks + 2) * L : 0));
@@ -146,6 +151,7 @@ stftr_kernel(StftLaunch a, uint64_t fps) {
     for (int i = threadIdx.x; i < 2 * NC; i += kBlock) {  // window: lane row (w[2m], w[2m+1])
         const int m = i >> 1, l = m % L, n = m / L;
         wtl[l * G::WL_STRIDE + 2 * n + (i & 1)] = a.wpad[i];
+        if constexpr (DIR) wcl[l * G::WL_STRIDE + 2 * n + (i & 1)] = i >= a.pad_left && i < a.pad_left + a.win ? -0.0f : 0.0f;
     }
     for (int i = threadIdx.x; i < NC; i += kBlock) {
         twl[i] = a.tw1[i];
@@ -192,7 +198,15 @@ stftr_kernel(StftLaunch a, uint64_t fps) {
             start = (int64_t)(g - g_beg) * hop - NC;  // t hop - win / 2 (pad_left = 0)
         }
         // ---- the frame's downmixed samples: ring shift by SH rows + the prefetched hop ----
-        if (pre_ok) {
+        if (DIR && valid && start >= 0 && start + 2 * NC <= n && ((base + (uint64_t)start * C) % (2 * C)) != 0) {
+            // (DIR) an interior frame at an odd start: sample by sample
+#pragma unroll
+            for (int q = 0; q < P; ++q) {
+                const int64_t i0 = start + 2 * (lj + L * q);
+                raw[q] = make_float2(read_sample<INF>(a.in, base, i0, C, a.fold != 0),
+                                     read_sample<INF>(a.in, base, i0 + 1, C, a.fold != 0));
+            }
+        } else if (pre_ok) {
 #pragma unroll
             for (int q = 0; q < KEEP; ++q) raw[q] = raw[q + SH];
 #pragma unroll
@@ -221,7 +235,7 @@ stftr_kernel(StftLaunch a, uint64_t fps) {
         // ---- prefetch the next frame's new points (rows KEEP .. P - 1) ----
         {
             const int64_t nstart = start + hop;
-            const bool nxt = valid && g + 1 < g1 && g + 1 < g_end && nstart + 2 * NC <= n &&
+            const bool nxt = !DIR && valid && g + 1 < g1 && g + 1 < g_end && nstart + 2 * NC <= n &&
                              nstart + 2 * L * KEEP >= 0 &&
                              ((base + (uint64_t)(nstart + 2 * L * KEEP) * C) % (2 * C)) == 0;
             if (nxt) {
@@ -240,6 +254,15 @@ stftr_kernel(StftLaunch a, uint64_t fps) {
                 const float4 w = wr[q];
                 v[2 * q] = make_float2(raw[2 * q].x * w.x, raw[2 * q].y * w.y);
                 v[2 * q + 1] = make_float2(raw[2 * q + 1].x * w.z, raw[2 * q + 1].y * w.w);
+            }
+            if constexpr (DIR) {  // -0 inside the window (bits unchanged), +0 in the pads
+                const float4* cr = reinterpret_cast<const float4*>(wcl + lj * G::WL_STRIDE);
+#pragma unroll
+                for (int q = 0; q < P / 2; ++q) {
+                    const float4 c = cr[q];
+                    v[2 * q] = make_float2(v[2 * q].x + c.x, v[2 * q].y + c.y);
+                    v[2 * q + 1] = make_float2(v[2 * q + 1].x + c.z, v[2 * q + 1].y + c.w);
+                }
             }
         }
         // ---- level 0: Butterfly4 over d0 (registers d1 + 4 d0) ----
@@ -310,9 +333,12 @@ stftr_kernel(StftLaunch a, uint64_t fps) {
             const float dre = b.x - rr.x, dim = b.y - rr.y;
             xk.x = 0.5f * ((sre + sck.y * sim) - sck.x * dre);
             xk.y = 0.5f * ((dim - sck.x * sim) - sck.y * dre);
-            // partner: b' = rr, r' = b: (rr.re + b.re) = sre, (rr.re - b.re) = -dre, ...
-            xkp.x = 0.5f * ((sre + sckp.y * sim) - sckp.x * (-dre));
-            xkp.y = 0.5f * (((-dim) - sckp.x * sim) - sckp.y * (-dre));
+            // partner: b' = rr, r' = b: (rr.re + b.re) = sre (sums commute bit for bit); the
+            // differences formed again (rr.re - b.re is -dre except for a zero: +0 either way,
+            // where -dre would be -0 -- round 6, test_negative_zero_samples_and_silence)
+            const float pdre = rr.x - b.x, pdim = rr.y - b.y;
+            xkp.x = 0.5f * ((sre + sckp.y * sim) - sckp.x * pdre);
+            xkp.y = 0.5f * ((pdim - sckp.x * sim) - sckp.y * pdre);
         };
         float* row = region;
         const int sh = MEL ? 0
@@ -380,13 +406,16 @@ stftr_kernel(StftLaunch a, uint64_t fps) {
 // ------------------------------------------------------------------------------------------
 // host side
 // ------------------------------------------------------------------------------------------
+// the canonical geometry streams (win = n_fft, hop = n_fft / 4); any other (DIR) loads per frame
+static bool r_canon(const StftLaunch& a) { return a.win == a.n_fft && a.hop * 4 == a.n_fft; }
+
 static int ldsr_bytes(const StftLaunch& a, int wv) {
     const bool mel = a.out_kind == OUT_MEL || a.out_kind == OUT_MEL_AMP_DB;
     const int meltab = mel ? ((a.melr_chunks + 2) + (a.melr_chunks + 1) * a.melr_steps) * GeoR::L * 16 : 0;
-    return (GeoR::TAB_FLOATS + wv * GeoR::REGION) * 4 + meltab;
+    return (GeoR::TAB_FLOATS + (r_canon(a) ? 0 : GeoR::WL_FLOATS) + wv * GeoR::REGION) * 4 + meltab;
 }
 
-template <int KIND, int C, int INF, int WV, int VAR = 0>
+template <int KIND, int C, int INF, int WV, int VAR = 0, bool DIR = false>
 static int launchr_k(const StftLaunch& a, hipStream_t s) {
 #ifdef THESIA_EXPERIMENTS
     if constexpr (VAR == 0 && KIND == OUT_MEL_AMP_DB && C == 2 && INF == IN_F32 && WV == 12) {
@@ -400,7 +429,7 @@ static int launchr_k(const StftLaunch& a, hipStream_t s) {
 #endif
     const int lds = ldsr_bytes(a, WV);
     if (lds > 163840) return -2;
-    auto kern = stftr_kernel<KIND, C, INF, WV, VAR>;
+    auto kern = stftr_kernel<KIND, C, INF, WV, VAR, DIR>;
     if (hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize, lds) !=
         hipSuccess)
         return -1;
@@ -416,38 +445,43 @@ static int launchr_k(const StftLaunch& a, hipStream_t s) {
 
 // the spectrum kinds always fit 12 regions (125 KiB); the mel kinds fall back to 8 when their
 // tables leave no room
-template <int KIND, int C, int INF>
+template <int KIND, int C, int INF, bool DIR = false>
 static int launchr_w(const StftLaunch& a, hipStream_t s) {
     if constexpr (KIND == OUT_MEL || KIND == OUT_MEL_AMP_DB) {
         if (a.melr_chunks <= 0) return -2;
-        if (ldsr_bytes(a, 12) > 163840) return launchr_k<KIND, C, INF, 8>(a, s);
+        if (ldsr_bytes(a, 12) > 163840) return launchr_k<KIND, C, INF, 8, 0, DIR>(a, s);
     }
-    return launchr_k<KIND, C, INF, 12>(a, s);
+    return launchr_k<KIND, C, INF, 12, 0, DIR>(a, s);
 }
 
-template <int C, int INF>
+template <int C, int INF, bool DIR = false>
 static int launchr_c(const StftLaunch& a, hipStream_t s) {
     switch (a.out_kind) {
-        case OUT_COMPLEX: return launchr_w<OUT_COMPLEX, C, INF>(a, s);
-        case OUT_MAG: return launchr_w<OUT_MAG, C, INF>(a, s);
-        case OUT_POWER: return launchr_w<OUT_POWER, C, INF>(a, s);
-        case OUT_AMP_DB: return launchr_w<OUT_AMP_DB, C, INF>(a, s);
-        case OUT_POWER_DB: return launchr_w<OUT_POWER_DB, C, INF>(a, s);
-        case OUT_MEL: return launchr_w<OUT_MEL, C, INF>(a, s);
-        case OUT_MEL_AMP_DB: return launchr_w<OUT_MEL_AMP_DB, C, INF>(a, s);
+        case OUT_COMPLEX: return launchr_w<OUT_COMPLEX, C, INF, DIR>(a, s);
+        case OUT_MAG: return launchr_w<OUT_MAG, C, INF, DIR>(a, s);
+        case OUT_POWER: return launchr_w<OUT_POWER, C, INF, DIR>(a, s);
+        case OUT_AMP_DB: return launchr_w<OUT_AMP_DB, C, INF, DIR>(a, s);
+        case OUT_POWER_DB: return launchr_w<OUT_POWER_DB, C, INF, DIR>(a, s);
+        case OUT_MEL: return launchr_w<OUT_MEL, C, INF, DIR>(a, s);
+        case OUT_MEL_AMP_DB: return launchr_w<OUT_MEL_AMP_DB, C, INF, DIR>(a, s);
         default: return -2;
     }
 }
 
 bool stftr_supports(int n_fft, int win, int hop, int in_format, int channels) {
-    return n_fft == 2048 && win == n_fft && hop * 4 == n_fft && (in_format == IN_F32 || in_format == IN_S16) &&
-           (channels == 1 || channels == 2);
+    if (n_fft != 2048 || !(channels == 1 || channels == 2)) return false;
+    if (win == n_fft && hop * 4 == n_fft) return in_format == IN_F32 || in_format == IN_S16;
+    // any other geometry (DIR): even win <= n_fft (the frame start t hop - n_fft / 2 is the
+    // reference's t hop - win / 2 - pad_left, lib.rs:400-401), f32
+    return in_format == IN_F32 && hop >= 1 && win >= 2 && win <= n_fft && win % 2 == 0;
 }
 
 int stftr_lds_bytes(const StftLaunch& a) { return ldsr_bytes(a, 8); }
 
 int launch_stftr(const StftLaunch& a, hipStream_t s) {
     if (!stftr_supports(a.n_fft, a.win, a.hop, a.in_format, a.channels)) return -2;
+    if (!r_canon(a))  // the viewer's geometries: f32 mono / stereo (MultiTrack's mono pool)
+        return a.channels == 2 ? launchr_c<2, IN_F32, true>(a, s) : launchr_c<1, IN_F32, true>(a, s);
     if (a.in_format == IN_S16) return a.channels == 2 ? launchr_c<2, IN_S16>(a, s) : launchr_c<1, IN_S16>(a, s);
     return a.channels == 2 ? launchr_c<2, IN_F32>(a, s) : launchr_c<1, IN_F32>(a, s);
 }

@@ -47,6 +47,9 @@ for (const i of [0, 1, 2]) {{
 }}
 try {{ mt.get_wav_image(0, 100.0, 100, -1.0, 1.0); out.panic = null; }}  // display.rs:95-108 panics
 catch (e) {{ out.panic = e.code; }}
+const grab = f => {{ try {{ f(); return null; }} catch (e) {{ return [e.constructor.name, e.code]; }} }};
+out.neg_spec = grab(() => mt.get_spec_image(0, 100.0, -5));  // nheight wraps to 2^32 - 5 (ToUint32)
+out.neg_wav = grab(() => mt.get_wav_image(0, 100.0, -5, -2.0, 2.0));
 out.removed = mt.remove_track(1);
 out.after = mt.get_max_db();
 mt.free();
@@ -79,4 +82,7 @@ console.log(JSON.stringify(out));
         got = np.frombuffer(base64.b64decode(r["wav"][str(i)]), np.uint8)
         assert np.array_equal(got, ref), WAVS[i]
     assert r["panic"] == -9  # THESIA_ERR_PANIC: the folded stereo sum leaves [-1, 1]
+    # a known id with a negative height (wasm-bindgen's u32 wrap): the image would need terabytes;
+    # refused with a RangeError before any host buffer is sized, the process survives
+    assert r["neg_spec"] == ["RangeError", "ERR_ARG"] and r["neg_wav"] == ["RangeError", "ERR_ARG"]
     assert isinstance(r["removed"], bool)
