@@ -754,7 +754,8 @@ def main_viewer(args, rank):
     T1 = engine.Batch.frames_for(plan, [len(x1)])
     dout = engine.DeviceBuffer(T1 * plan.row_bins * 4)
     ent = {"frames": T1, "n_mel": plan.row_bins}
-    for name, k in (("stftx (reference order, bit-exact)", 9), ("fast kernel", 0)):
+    for name, k in (("kernel 7 (reference order, bit-exact; MultiTrack default)", 7),
+                    ("stftx (reference order, bit-exact)", 9), ("fast kernel", 0)):
         b = engine.Batch(plan, din, [0], [len(x1)], dout, kernel=k)
         b.run_timed(3)
         kms = b.run_timed(50) / 50
@@ -816,7 +817,8 @@ def main_viewer(args, rank):
     t_cpu_add = time.perf_counter() - t0
     t_cpu_img = _median_s(lambda: O.grey_to_rgb(greys[0], nwi, 500), 3)
     E["add_tracks"] = {"tracks": 6, "samples_per_track": len(x_full), "gpu_ms": 1e3 * t_add,
-                       "gpu": "MultiTrack.add_tracks: WAV parse + int16 upload + decode + stftx + range + grey, synchronous",
+                       "gpu": "MultiTrack.add_tracks: WAV parse + int16 upload + decode + kernel 7 (bit-exact) + range + "
+                              "grey, synchronous",
                        "cpu_oracle_ms": 1e3 * t_cpu_add, "cpu_threads": 6,
                        "cpu": "oracle track_spec per track on 6 threads (rayon par_iter, lib.rs:161-166) + range + "
                               "spec_to_grey; no WAV parse"}
@@ -827,16 +829,17 @@ def main_viewer(args, rank):
     os.remove(path)
     os.rmdir(tmp)
 
-    # -- the kernels behind add_tracks on the same six tracks (int16 input, as MultiTrack uploads)
+    # -- the kernels behind add_tracks on the same six tracks: the mono f32 pool MultiTrack's
+    # decode fills (its batch input), one launch over the six
     n = len(pcm16)
-    flat = np.concatenate([pcm16] * 6)
+    flat = np.concatenate([x_full] * 6)
     din6 = engine.DeviceBuffer.from_host(flat)
     offs = [i * n for i in range(6)]
     T6 = engine.Batch.frames_for(plan, [n] * 6)
     dout6 = engine.DeviceBuffer(T6 * plan.row_bins * 4)
     kk = {}
-    for name, k in (("stftx", 9), ("fast", 0)):
-        b = engine.Batch(plan, din6, offs, [n] * 6, dout6, input_format=engine.IN_S16, kernel=k)
+    for name, k in (("kernel7", 7), ("stftx", 9), ("fast", 0)):
+        b = engine.Batch(plan, din6, offs, [n] * 6, dout6, kernel=k)
         b.run_timed(2)
         kms = b.run_timed(10) / 10
         abytes = flat.nbytes + T6 * plan.row_bins * 4
@@ -844,7 +847,10 @@ def main_viewer(args, rank):
                     "algorithmic_gbs": abytes / (kms * 1e-3) / 1e9,
                     "hbm_frac": abytes / (kms * 1e-3) / 1e9 / HBM_PEAK_GBS}
         b.close()
-    E["add_tracks_kernels"] = dict(kk, frames=T6, algorithmic_bytes=flat.nbytes + T6 * plan.row_bins * 4)
+    E["add_tracks_kernels"] = dict(kk, frames=T6, algorithmic_bytes=flat.nbytes + T6 * plan.row_bins * 4,
+                                   note="kernel7 is MultiTrack's default (bit-exact, round 6: streaming "
+                                        "reference-order kernels at the viewer geometry); stftx its round-5 "
+                                        "default; fast the opt-in tolerance kernel")
     if rank == 0:
         print(json.dumps(out), flush=True)
 
