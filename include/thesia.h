@@ -58,11 +58,13 @@ int thesia_host_register(void* host, size_t bytes);
 int thesia_host_unregister(void* host);
 int thesia_memset_device(void* dst_device, int value, size_t bytes);
 int thesia_device_synchronize(void);
-/* The library's own stream-ordered memory pool on the current device (not the device's default
- * pool): buffers the library frees stay reserved there for its next allocations, without a device
- * synchronisation. thesia_pool_trim hands the unused reserve back to the device (it also runs in
+/* The library's block cache on the current device (round 5; the runtime's stream-ordered pool is
+ * not used: on ROCm 7.2 it lost kernel writes into reused memory, profiles/r06_pool): device
+ * buffers are hipMalloc blocks that, once released, stay with the library for its next
+ * allocations of their size class, ordered behind their last use by an event (no device
+ * synchronisation). thesia_pool_trim hands the idle blocks back to the device (it also runs in
  * thesia_mt_destroy, after MultiTrack compaction and before an allocation that ran out of memory
- * is retried); thesia_pool_bytes reports the pool's reserved and in-use bytes (either may be NULL).
+ * is retried); thesia_pool_bytes reports cached + in-use and in-use bytes (either may be NULL).
  * Plumbing, not part of the reference surface. */
 int thesia_pool_trim(void);
 int thesia_pool_bytes(uint64_t* reserved, uint64_t* used);
@@ -204,8 +206,10 @@ int thesia_batch_kernel_info(const thesia_batch* batch, int* lds_bytes, int* til
 /* Which fused kernel runs the batch: 1 stft_kernel (general), 2 stft2_kernel (4 waves/SIMD),
  * 3 stft3_kernel (streaming; win = n_fft, hop = n_fft/4), 5 stft5_kernel (streaming, n_fft 2048:
  * untangle pairs co-resident in a lane), 7 the streaming reference-order kernels (stftr_kernel at
- * n_fft 2048, stftq_kernel at 256 / 512 / 1024; win = n_fft, hop = n_fft/4: rows equal the
- * reference's bit for bit), 9 stftx_kernel (the reference's operation order, any geometry). */
+ * n_fft 2048, stftq_kernel at 256 / 512 / 1024; win = n_fft, hop = n_fft/4 with f32 / s16 input,
+ * or any even win <= n_fft and any hop with f32 input -- the viewer's geometries, lib.rs:43-46:
+ * rows equal the reference's bit for bit), 9 stftx_kernel (the reference's operation order, any
+ * geometry). */
 int thesia_batch_kernel(const thesia_batch* batch, int* kernel);
 
 /* Named alternatives of a batch (none changes what is computed, only how; all results stay
