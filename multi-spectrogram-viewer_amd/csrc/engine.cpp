@@ -1219,7 +1219,7 @@ static int g_render_path = 0;  // thesia_set_render_path
 
 int render_path() { return __atomic_load_n(&g_render_path, __ATOMIC_RELAXED); }
 int set_render_path(int path) {
-    if (path < 0 || path > 4) return set_error(THESIA_ERR_INVALID_ARG, "render path must be 0 .. 4");
+    if (path < 0 || path > 5) return set_error(THESIA_ERR_INVALID_ARG, "render path must be 0 .. 5");
     __atomic_store_n(&g_render_path, path, __ATOMIC_RELAXED);
     return THESIA_OK;
 }
@@ -1528,6 +1528,7 @@ struct FusedGroup {
     uint32_t st_strip = THESIA_STRIP;
     int st_kv = 0, st_slots = 0, st_acc = 0, st_fc = 0, st_npf = 0, st_waves = 4, st_tile = 0, st_hdr = 0,
         st_wts = 0;
+    int st_ring = 0, st_hg = 0;  // ring mode (render path 5): ring frames, tap groups of 4
     bool st_dword = false;
 };
 
@@ -1544,6 +1545,55 @@ struct StripeTrack {
     uint32_t T, H, nw, oz;
     uint64_t rgb_off;
 };
+void plan_stripe_ring(const std::vector<StripeTrack>& trk, uint32_t bins, uint32_t nheight, FusedGroup& g) {
+    int kvmax = 0, hcmax = 0;
+    bool dword = true;
+    for (const StripeTrack& t : trk) {
+        if ((uint64_t)t.T * bins >= (1ull << 30)) return;  // the kernel's 32-bit byte offsets
+        kvmax = std::max(kvmax, t.vt->max_taps);
+        hcmax = std::max(hcmax, t.ht->max_taps);
+        dword = dword && t.nw % 4 == 0 && t.rgb_off % 4 == 0;
+    }
+    const int kv = kvmax <= 7 ? 7 : kvmax <= 8 ? 8 : kvmax <= 12 ? 12 : kvmax <= 16 ? 16 : 0;
+    const int hg = hcmax <= 8 ? 2 : hcmax <= 12 ? 3 : hcmax <= 16 ? 4 : hcmax <= 24 ? 6 : 0;
+    if (!kv || !hg) return;
+    int ring = 8;
+    while (ring < hcmax + 7) ring *= 2;
+    constexpr int kWaveRows = 64;
+    const uint32_t strip = g.st_strip;
+    int tile = 1, nbmax = 0;
+    for (const StripeTrack& t : trk) {
+        const int top = (int)t.H - (int)bins;
+        for (uint32_t R0 = 0; R0 < nheight; R0 += kWaveRows) {
+            const uint32_t rlo = std::max(R0, t.oz), rhi = std::min(R0 + kWaveRows, nheight);
+            if (rlo >= rhi) continue;
+            const int ya = t.vt->h_left[rlo], nt = t.vt->h_left[rhi - 1] + kv - ya;
+            tile = std::max(tile, nt);
+            nbmax = std::max(nbmax, std::min(ya + nt, (int)t.H) - std::max(ya, top));
+        }
+    }
+    const int hdr = 2 * (int)strip, wts = (int)strip * 4 * hg, slots = ring + 4 * hg + 1;
+    int fc = 16, npf = 16, waves = nheight > 256 ? 8 : 4;
+    auto lds = [&]() { return render_stripe_lds_bytes(fc, tile, hdr, wts, waves, slots); };
+    if (fc * nbmax > 64 * npf || lds() > (waves == 8 ? 81920 : 54613)) fc = 8;
+    if (waves == 8 && lds() > 81920) waves = 4;
+    if (fc * nbmax > 64 * npf || lds() > 163840) return;
+    if (fc * (int)bins >= 65536 || tile * (fc + 4) >= 65536) return;
+    g.stripe = true;
+    g.st_kv = kv;
+    g.st_slots = 4;
+    g.st_acc = 1;
+    g.st_fc = fc;
+    g.st_npf = npf;
+    g.st_waves = waves;
+    g.st_tile = tile;
+    g.st_hdr = hdr;
+    g.st_wts = wts;
+    g.st_dword = dword;
+    g.st_ring = ring;
+    g.st_hg = hg;
+}
+
 // Automatic choice (render path 0): only groups whose frames outnumber their image columns at
 // least 3 to 1. There the two-kernel path's intermediate ([nheight][T] f32, written and read
 // back) dominates its traffic, and the stripe kernel's fixed 8-frame steps waste few slots
@@ -1552,9 +1602,14 @@ struct StripeTrack {
 // 604 -> 504, 22.05 kHz / 256 (3.4) 478 -> 419; slower at T/nw 1.25 .. 1.9 (8 kHz / 256 265 ->
 // 291, 16 kHz / 512 293 -> 317, 24 kHz / 512 341 -> 349, 44.1 kHz / 1024 359 -> 394) and even
 // below 1. Path 4 takes it wherever an instance covers the geometry.
+// Ring mode (render path 5, round 6; `ring`): the groups below 3 frames per column, where the slot
+// mode is not taken, run the stripe kernel with the horizontal sums over each column's exact taps
+// from a per-lane LDS ring of the recent frames' vertical sums (render_stripe.hip): at most 24 taps
+// per column (6 float4 groups), a ring of the next power of 2 >= taps + 7 frames.
 void plan_stripe(const std::vector<StripeTrack>& trk, uint32_t bins, uint32_t nheight, FusedGroup& g,
-                 bool force) {
+                 bool force, bool ring = false) {
     g.stripe = false;
+    g.st_ring = g.st_hg = 0;
     if (trk.empty()) return;
     if (!force) {
         uint64_t frames = 0, cols = 0;
@@ -1562,7 +1617,10 @@ void plan_stripe(const std::vector<StripeTrack>& trk, uint32_t bins, uint32_t nh
             frames += t.T;
             cols += t.nw;
         }
-        if (frames < 3 * cols) return;
+        if (frames < 3 * cols) {
+            if (ring) plan_stripe_ring(trk, bins, nheight, g);
+            return;
+        }
     }
     int kvmax = 0, amax = 0;
     bool dword = true;
@@ -1676,8 +1734,16 @@ int plan_fused_group(const float* d_spec, const uint64_t* row0, size_t bins, siz
     }
     g.ndesc = desc.size() - g.desc0;
     if (stripe) {
-        plan_stripe(strk, (uint32_t)bins, nheight, g, stripe == 2);
-        if (g.stripe) {  // no intermediate: the group's workspace share and its cost change
+        plan_stripe(strk, (uint32_t)bins, nheight, g, stripe == 2, stripe == 3);
+        if (g.stripe && g.st_hg) {  // ring mode: the plain tap tables (hl / hc / ho / hw), no step tables
+            uint64_t cost = 0;
+            for (size_t i = g.desc0; i < g.desc0 + g.ndesc; ++i) {
+                desc[i].tmp_off = 0;
+                cost += (uint64_t)desc[i].T * bins + (3ull * desc[i].nw * nheight) / 4;
+            }
+            g.tmp_tot = 0;
+            g.cost = cost * 3;  // compute-bound like the slot mode (see below)
+        } else if (g.stripe) {  // no intermediate: the group's workspace share and its cost change
             uint64_t cost = 0;
             for (size_t i = g.desc0; i < g.desc0 + g.ndesc; ++i) {
                 const DevTaps* ht = nullptr;  // the step tables for the group's slot count
@@ -1809,7 +1875,7 @@ int render_rgb_fused(size_t n_groups, const float* const* d_specs, const uint64_
         for (size_t k = 0; k < n_groups; ++k) {
             rc = plan_fused_group(d_specs[k], row0s[k], bins[k], ns[k], up_ratio + t0, nwidth + t0, nheight,
                                   rgb_off + t0, desc, groups[k], true,
-                                  rpath == 0 ? 1 : rpath == 4 ? 2 : 0);
+                                  rpath == 0 ? 1 : rpath == 4 ? 2 : rpath == 5 ? 3 : 0);
             if (rc) return rc;
             t0 += ns[k];
         }
@@ -1884,6 +1950,8 @@ int render_rgb_fused(size_t n_groups, const float* const* d_specs, const uint64_
                 L.hdr_cap = g.st_hdr;
                 L.wts_cap = g.st_wts;
                 L.dword_rgb = g.st_dword;
+                L.ring = g.st_ring;
+                L.hg = g.st_hg;
                 L.cmap = cmap_ptr;
                 L.rgb = d_rgb;
                 if (launch_render_stripe(L, st)) return set_error(THESIA_ERR_DEVICE, "render stripe launch failed");

@@ -252,9 +252,14 @@ struct StripeLaunch {
     const uint8_t* cmap;
     uint8_t* rgb;
     int abl;             // experiment build only (THESIA_STRIPE_ABL, timing ablations): 0
+    // ring mode (hg > 0, render path 5): the lane's vertical sums of the strip's last `ring`
+    // frames (a power of 2) in a per-lane LDS ring, each column summed over exactly its taps (hg
+    // float4 groups, zero-padded) when its support has been formed; 0: the slot mode above
+    int ring, hg;
 };
 int launch_render_stripe(const StripeLaunch& L, hipStream_t s);
-int render_stripe_lds_bytes(int fc, int tile_cap, int hdr_cap, int wts_cap, int waves);
+// ring_slots: the ring mode's LDS frames per wave (ring + 4 hg + 1), 0 in slot mode
+int render_stripe_lds_bytes(int fc, int tile_cap, int hdr_cap, int wts_cap, int waves, int ring_slots = 0);
 
 // LDS bytes of the wide vertical pass (grey_vert_wide_kernel<fpl>) for a band / tile / kv
 int grey_vert_wide_lds_bytes(int fpl, uint32_t band, int tile_cap, int kv);

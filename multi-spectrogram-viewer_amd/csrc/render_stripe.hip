@@ -19,6 +19,12 @@
 //   * a column whose support ends in the step is finished: colormap, its 3 bytes packed with
 //     its neighbours' into the wave's RGB staging in LDS, which leaves as contiguous 48-byte row
 //     pieces every 16 columns; the accumulators shift down one slot.
+// Ring mode (HG > 0, round 6; render path 5, for groups with fewer than 3 frames per column): the
+// horizontal slots are replaced by a per-lane LDS ring of the wave's vertical sums over the strip's
+// last RING frames (each lane reads only its own row's entries: no cross-lane hazard); once a
+// step has formed the last frame of a column's support, the column is summed over exactly its
+// taps (HG float4 groups of weights staged per strip column, zero-padded; the ring mirrors its
+// first 4 HG slots after its end so a column's frames are contiguous) and closed as above.
 // Every sum runs in the reference's order (t = 0; t += x * w, no fused multiply-add: the kernel
 // is built with -ffp-contract=off). The padded terms are (+0 weight) x (finite value) = +-0,
 // which leave a sum's bits unchanged (a sum is never -0: it starts at +0 and x + -x rounds to
@@ -62,9 +68,11 @@ __device__ __forceinline__ void wave_sync() {  // cross-lane LDS ordering within
 
 // A accumulators (columns meeting a step), AW the step table's row stride (A rounded up to 4; its
 // entries past A are zero and never read into a sum)
-template <int KV, int A, int AW, int FC, int NPF, int WV>
+template <int KV, int A, int AW, int FC, int NPF, int WV, int HG = 0>
 __global__ void __launch_bounds__(64 * WV) render_stripe_kernel(StripeLaunch L) {
     constexpr int kRows = 64 * WV;  // output rows per block (lane = row)
+    constexpr bool kRing = HG > 0;
+    constexpr int MIR = 4 * HG;  // ring slots mirrored after its end
     extern __shared__ __attribute__((aligned(16))) float sm[];
     constexpr int TS = FC + 4;   // tile row stride (floats): 16-byte rows for the b128 reads
     constexpr int SPC = FC / 8;  // steps per chunk
@@ -91,9 +99,12 @@ __global__ void __launch_bounds__(64 * WV) render_stripe_kernel(StripeLaunch L) 
     uint2* lut = reinterpret_cast<uint2*>(sm);
     int* hdr = reinterpret_cast<int*>(sm + kLutFloats);
     float* wts = reinterpret_cast<float*>(hdr + ((L.hdr_cap + 3) & ~3));
-    const int wave_floats = L.tile_cap * TS + 64 * kSumStride;
+    const int ring_n = kRing ? L.ring : 0;  // a power of 2
+    const int ring_slots = kRing ? ring_n + MIR + 1 : 0;  // (the last one: a dummy mirror target)
+    const int wave_floats = L.tile_cap * TS + 64 * kSumStride + ring_slots * 64;
     float* tile = wts + L.wts_cap + wave * wave_floats;
     float* fsum = tile + L.tile_cap * TS;
+    float* ring = fsum + 64 * kSumStride;  // ring mode: [slot][64 lanes]
     // the RGB staging reuses the sums' space (every lane has read its sums before it is written)
     uint32_t* rgbst = reinterpret_cast<uint32_t*>(fsum);
 
@@ -104,9 +115,24 @@ __global__ void __launch_bounds__(64 * WV) render_stripe_kernel(StripeLaunch L) 
     const int* gh = r.hst + s_lo;
     const float* gw = r.hsw + (uint64_t)s_lo * 8 * AW;
     if (tid < 10) lut[tid] = colormap_pair(L.cmap, tid);
-    for (int i = tid; i < nst; i += kRows) hdr[i] = gh[i];
-    for (int i = tid; i < nst * 2 * AW; i += kRows)  // nst x 8 x AW floats <= wts_cap (host)
-        reinterpret_cast<float4*>(wts)[i] = reinterpret_cast<const float4*>(gw)[i];
+    if constexpr (kRing) {
+        // the strip's columns: {first frame, last frame} and their taps, HG float4 per column
+        // (zero-padded); hdr_cap >= 2 strip, wts_cap >= strip 4 HG (host)
+        const int ncol = (int)(c1 - c0);
+        for (int k = tid; k < ncol; k += kRows) {
+            const int c = (int)c0 + k;
+            hdr[2 * k] = r.hl[c];
+            hdr[2 * k + 1] = r.hl[c] + r.hc[c] - 1;
+        }
+        for (int i = tid; i < ncol * 4 * HG; i += kRows) {
+            const int k = i / (4 * HG), t = i - k * 4 * HG, c = (int)c0 + k;
+            wts[i] = t < r.hc[c] ? r.hw[r.ho[c] + t] : 0.0f;
+        }
+    } else {
+        for (int i = tid; i < nst; i += kRows) hdr[i] = gh[i];
+        for (int i = tid; i < nst * 2 * AW; i += kRows)  // nst x 8 x AW floats <= wts_cap (host)
+            reinterpret_cast<float4*>(wts)[i] = reinterpret_cast<const float4*>(gw)[i];
+    }
     __syncthreads();  // the only block barrier: the waves run on their own from here
 
     // a finished column c: its sum into the lane's row of the wave's staging; every 16 columns
@@ -303,15 +329,19 @@ __global__ void __launch_bounds__(64 * WV) render_stripe_kernel(StripeLaunch L) 
     }
 
     const int nchunks = (nst + SPC - 1) / SPC;
+    if constexpr (kRing) {  // finite ring entries (padded taps read them with +0 weights)
+        for (int i = 0; i < ring_slots; ++i) ring[i * 64 + lane] = 0.0f;
+    }
     if (nb) {
         issue(0);
         wave_sync();  // tile zeroed
         commit(0);
     }
     wave_sync();
-    float acc[A];
+    float acc[kRing ? 1 : A];
 #pragma unroll
-    for (int k = 0; k < A; ++k) acc[k] = 0.0f;
+    for (int k = 0; k < (kRing ? 1 : A); ++k) acc[k] = 0.0f;
+    uint32_t cc = c0;  // ring mode: the next column to close
     // slot a <-> column ca(s) + a of the step's table (columns before c0, finished by the strip
     // on the left, and from c1 on are summed too and never stored)
     for (int k = 0; k < nchunks; ++k) {
@@ -322,7 +352,7 @@ __global__ void __launch_bounds__(64 * WV) render_stripe_kernel(StripeLaunch L) 
         for (int u8 = 0; u8 < SPC; ++u8) {
             const int si = k * SPC + u8;
             if (si >= nst) break;  // uniform
-            const int ca = rfl(hdr[si]);
+            const int ca = kRing ? 0 : rfl(hdr[si]);
             SMARK(vert);
             // vertical sums of the step's 8 frames (resize_v_px order), 4 frames at a time: one
             // ds_read_b128 per tap, a batch of taps' reads in flight
@@ -354,6 +384,46 @@ __global__ void __launch_bounds__(64 * WV) render_stripe_kernel(StripeLaunch L) 
                 v[4 * hf + 1] = a1;
                 v[4 * hf + 2] = a2;
                 v[4 * hf + 3] = a3;
+            }
+            if constexpr (kRing) {
+                // the step's frames into the lane's ring (slot f mod RING, mirrored after the end
+                // for f mod RING < 4 HG), then every column whose support ends by this step's last
+                // frame: t = 0; t += v[f] * w over its taps, ascending (resize_h's order; the
+                // padded taps add (+0 weight) x (finite entry) = +-0)
+                SMARK(ring);
+                const int fb = F0 + 8 * si;
+#pragma unroll
+                for (int u = 0; u < 8; ++u) {
+                    const int sl = (fb + u) & (ring_n - 1);  // uniform
+                    const int ml = sl < MIR ? sl + ring_n : ring_n + MIR;
+                    ring[sl * 64 + lane] = v[u];
+                    ring[ml * 64 + lane] = v[u];
+                }
+                const int fend = fb + 7;
+                while (cc < c1) {  // uniform
+                    const int last = rfl(hdr[2 * (cc - c0) + 1]);
+                    if (last > fend) break;
+                    const int s0 = rfl(hdr[2 * (cc - c0)]) & (ring_n - 1);
+                    const float* rb = ring + s0 * 64 + lane;
+                    const float4* wb = reinterpret_cast<const float4*>(wts) + (cc - c0) * HG;
+                    float xs[4 * HG];
+#pragma unroll
+                    for (int i = 0; i < 4 * HG; ++i) xs[i] = rb[i * 64];
+                    float4 ws[HG];
+#pragma unroll
+                    for (int g = 0; g < HG; ++g) ws[g] = wb[g];
+                    float t = 0.0f;
+#pragma unroll
+                    for (int g = 0; g < HG; ++g) {
+                        t = t + xs[4 * g] * ws[g].x;
+                        t = t + xs[4 * g + 1] * ws[g].y;
+                        t = t + xs[4 * g + 2] * ws[g].z;
+                        t = t + xs[4 * g + 3] * ws[g].w;
+                    }
+                    close_col(cc, t);
+                    ++cc;
+                }
+                continue;
             }
             // horizontal: every slot's chain takes the step's frames in ascending order (the
             // resize_h order; slots outside a column's support add (+0 weight) x v = +-0); the
@@ -407,29 +477,43 @@ __global__ void __launch_bounds__(64 * WV) render_stripe_kernel(StripeLaunch L) 
     }
 }
 
-template <int KV, int A, int AW, int FC, int NPF>
+template <int KV, int A, int AW, int FC, int NPF, int HG = 0>
 const void* stripe_kernel(int waves) {
-    return waves == 8 ? reinterpret_cast<const void*>(render_stripe_kernel<KV, A, AW, FC, NPF, 8>)
-                      : reinterpret_cast<const void*>(render_stripe_kernel<KV, A, AW, FC, NPF, 4>);
+    return waves == 8 ? reinterpret_cast<const void*>(render_stripe_kernel<KV, A, AW, FC, NPF, 8, HG>)
+                      : reinterpret_cast<const void*>(render_stripe_kernel<KV, A, AW, FC, NPF, 4, HG>);
 }
 
 }  // namespace
 
-int render_stripe_lds_bytes(int fc, int tile_cap, int hdr_cap, int wts_cap, int waves) {
+int render_stripe_lds_bytes(int fc, int tile_cap, int hdr_cap, int wts_cap, int waves, int ring_slots) {
     return (kLutFloats + ((hdr_cap + 3) & ~3) + wts_cap +
-            waves * (tile_cap * (fc + 4) + 64 * kSumStride)) * 4;
+            waves * (tile_cap * (fc + 4) + 64 * kSumStride + 64 * ring_slots)) * 4;
 }
 
 int launch_render_stripe(const StripeLaunch& L, hipStream_t s) {
     if (L.n == 0 || L.nh == 0) return 0;
     if (L.n > 65535 || L.strip == 0 || (L.strip & 15) || (L.waves != 4 && L.waves != 8)) return -2;
+    if (L.hg && (L.ring < 8 || (L.ring & (L.ring - 1)))) return -2;
     const void* kern = nullptr;
+    // ring mode (render path 5): KV 7 / 8 / 12 / 16 x HG 2 / 3 / 4 / 6 tap groups, FC 16 or 8
+#define THESIA_STRIPE_RING(KV_, HG_, FC_)                                                      \
+    if (L.hg == HG_ && L.kv == KV_ && L.fc == FC_ && L.npf == 16)                            \
+        kern = stripe_kernel<KV_, 1, 4, FC_, 16, HG_>(L.waves);
+#define THESIA_STRIPE_RING_KV(KV_)                                                             \
+    THESIA_STRIPE_RING(KV_, 2, 16) THESIA_STRIPE_RING(KV_, 3, 16) THESIA_STRIPE_RING(KV_, 4, 16)   \
+    THESIA_STRIPE_RING(KV_, 6, 16) THESIA_STRIPE_RING(KV_, 2, 8) THESIA_STRIPE_RING(KV_, 3, 8)     \
+    THESIA_STRIPE_RING(KV_, 4, 8) THESIA_STRIPE_RING(KV_, 6, 8)
+    if (L.hg) {
+        THESIA_STRIPE_RING_KV(7) THESIA_STRIPE_RING_KV(8) THESIA_STRIPE_RING_KV(12) THESIA_STRIPE_RING_KV(16)
+    }
+#undef THESIA_STRIPE_RING_KV
+#undef THESIA_STRIPE_RING
     // the instances (host plan_stripe picks among them): KV 7 / 8 (the groups that upsample
     // vertically: Lanczos3's 6-7 taps per row, 7 where no row has 8) with 8 / 9 / 10 / 12 (and for
     // KV 8, 16) accumulators (9 and 10 on the 12-wide step table: the 48 kHz / 512 and 22.05 kHz /
     // 256 C5 groups meet at most 9 columns per step); KV 12 / 16 (downsampling) with 16
 #define THESIA_STRIPE(KV_, A_, AW_, FC_, NPF_)                                                     \
-    if (L.kv == KV_ && L.acc == A_ && L.slots == AW_ && L.fc == FC_ && L.npf == NPF_)             \
+    if (!L.hg && L.kv == KV_ && L.acc == A_ && L.slots == AW_ && L.fc == FC_ && L.npf == NPF_)    \
         kern = stripe_kernel<KV_, A_, AW_, FC_, NPF_>(L.waves);
     THESIA_STRIPE(7, 8, 8, 16, 8) THESIA_STRIPE(7, 8, 8, 16, 16) THESIA_STRIPE(7, 8, 8, 8, 16)
     THESIA_STRIPE(7, 9, 12, 16, 8) THESIA_STRIPE(7, 9, 12, 16, 16) THESIA_STRIPE(7, 9, 12, 8, 16)
@@ -444,7 +528,8 @@ int launch_render_stripe(const StripeLaunch& L, hipStream_t s) {
     THESIA_STRIPE(16, 16, 16, 16, 16) THESIA_STRIPE(16, 16, 16, 8, 16)
 #undef THESIA_STRIPE
     if (!kern) return -2;
-    const int lds = render_stripe_lds_bytes(L.fc, L.tile_cap, L.hdr_cap, L.wts_cap, L.waves);
+    const int lds = render_stripe_lds_bytes(L.fc, L.tile_cap, L.hdr_cap, L.wts_cap, L.waves,
+                                            L.hg ? L.ring + 4 * L.hg + 1 : 0);
     if (lds > 163840) return -2;
     if (hipFuncSetAttribute(kern, hipFuncAttributeMaxDynamicSharedMemorySize, lds) != hipSuccess) return -1;
     const uint32_t rows = 64u * (uint32_t)L.waves;

@@ -254,7 +254,8 @@ def set_batches_policy(policy: int) -> None:
 def set_render_path(path: int) -> None:
     """thesia_set_render_path: 0 the fused display with the single-pass kernel where it pays
     (default); 1 per-track launches; 2 three-stage launches; 3 two kernels for every group; 4 the
-    single-pass kernel wherever its instances cover the geometry (all byte-identical)."""
+    single-pass kernel wherever its instances cover the geometry; 5 as 0, plus the single-pass
+    kernel's ring mode for the groups below 3 frames per column (all byte-identical)."""
     check(lib.thesia_set_render_path(path))
 
 

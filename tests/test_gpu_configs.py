@@ -147,8 +147,9 @@ def test_c5_mixed_rate_render_pipeline():
 
 # 0: single-pass stripes for groups downsampling >= 3:1 along time, else two kernels; 1: per-track;
 # 2: three-stage; 3: two kernels for every group (LDS-DMA horizontal; wide vertical pass for
-# upsampling groups); 4: single-pass stripes wherever an instance covers the geometry
-@pytest.mark.parametrize("path", [0, 1, 2, 3, 4])
+# upsampling groups); 4: single-pass stripes wherever an instance covers the geometry; 5: as 0, plus
+# the stripes' ring mode (exact taps from a per-lane LDS ring) for the groups below 3 frames / column
+@pytest.mark.parametrize("path", [0, 1, 2, 3, 4, 5])
 @pytest.mark.parametrize("px_per_sec", [73.0, 30.0, 9.0, 2.0])  # 30: 17-64 taps; 9, 2: wider spans
 @pytest.mark.parametrize("nheight", [90, 400, 600])  # 400, 600: H -> nheight downsampling ~2.5, taller
 def test_render_batch_ragged_groups(path, px_per_sec, nheight):
@@ -187,7 +188,7 @@ def _oracle_check(tracks, out, nheight):
         assert r.rgb.tobytes() == img.tobytes(), (t.sr, t.n_fft, t.pcm.shape)
 
 
-@pytest.mark.parametrize("path", [0, 3, 4])
+@pytest.mark.parametrize("path", [0, 3, 4, 5])
 @pytest.mark.parametrize("mode", ["some_silent", "all_silent"])
 def test_render_silent_tracks(path, mode):
     """Silent tracks in a display batch: their dB rows sit at the global minimum, so the grey
@@ -209,7 +210,7 @@ def test_render_silent_tracks(path, mode):
     _oracle_check(tracks, out, 400)
 
 
-@pytest.mark.parametrize("path", [0, 3, 4])
+@pytest.mark.parametrize("path", [0, 3, 4, 5])
 def test_c5_geometry_500_rows(path):
     """The C5 display geometry (100 px/s x 500 rows, every (rate, n_fft) pair) at 3 s per track:
     the single-pass stripe kernel runs the 3 groups that downsample >= 3:1 along time (path 0) or
