@@ -112,22 +112,50 @@ void DevBuf::release() {
         DevCache& c = g_cache[dev];
         c.live -= cap;
         hipEvent_t ev = nullptr;
-        hipStream_t last = use ? use : st;
-        if (c.cached + cap <= kCacheCap && hipEventCreateWithFlags(&ev, hipEventDisableTiming) == hipSuccess &&
-            hipEventRecord(ev, last) == hipSuccess) {
-            c.free.push_back(CachedBlock{p, cap, last, ev});
+        bool ok = c.cached + cap <= kCacheCap;
+        if (ok && foreign) {
+            // last used on another stream: the event recorded there at that use orders the reuse;
+            // no stream is kept (it may be gone), so every allocation waits for the event
+            ev = use_ev;
+            use_ev = nullptr;
+        } else if (ok) {
+            ok = hipEventCreateWithFlags(&ev, hipEventDisableTiming) == hipSuccess && hipEventRecord(ev, st) == hipSuccess;
+        }
+        if (ok && ev) {
+            c.free.push_back(CachedBlock{p, cap, foreign ? nullptr : st, ev});
             c.cached += cap;
         } else {
             (void)hipGetLastError();
             if (ev) (void)hipEventDestroy(ev);
-            (void)hipFree(p);
+            (void)hipFree(p);  // (a device synchronisation: behind every use, on any stream)
         }
     } else {
         (void)hipFree(p);
     }
     p = nullptr;
     bytes = 0;
-    use = nullptr;
+    foreign = false;
+}
+
+void DevBuf::used_on(hipStream_t s) {
+    if (!p || !s) return;
+    if (s == st) {
+        // the allocation stream: the release event is recorded there; an earlier use on another
+        // stream is ordered into it first
+        if (foreign && use_ev) (void)hipStreamWaitEvent(st, use_ev, 0);
+        foreign = false;
+        return;
+    }
+    if (!use_ev && hipEventCreateWithFlags(&use_ev, hipEventDisableTiming) != hipSuccess) use_ev = nullptr;
+    // (an earlier use on a third stream is ordered into s, so the one event covers both)
+    if (use_ev && foreign) (void)hipStreamWaitEvent(s, use_ev, 0);
+    if (use_ev && hipEventRecord(use_ev, s) == hipSuccess) {
+        foreign = true;
+        return;
+    }
+    (void)hipGetLastError();
+    (void)hipStreamSynchronize(s);  // no event: the work is done before the block can be released
+    foreign = false;
 }
 
 int trim_pool() {
@@ -185,7 +213,7 @@ int DevBuf::alloc(size_t n) {
         for (size_t i = c.free.size(); i-- > 0;) {  // the most recently released first
             CachedBlock& b = c.free[i];
             if (b.cap != cap) continue;
-            if (b.st != s) {
+            if (b.st != s || !b.st) {  // (a block last used on a caller's stream: the event only)
                 const hipError_t q = hipEventQuery(b.ev);
                 if (q != hipSuccess) {
                     (void)hipGetLastError();
@@ -217,7 +245,7 @@ int DevBuf::alloc(size_t n) {
     pooled = true;
     dev = d;
     st = s;
-    use = nullptr;
+    foreign = false;
     bytes = n;
     return THESIA_OK;
 }
@@ -1020,9 +1048,6 @@ int batch_set_option(Batch* b, int option, int64_t value) {
 
 int batch_run(Batch* b, hipStream_t s) {
     if (!s) s = default_stream();
-#ifndef THESIA_DIAG_NO_LAST_USE  // (diagnostic build: the round-5 cache, for the test's control)
-    b->d_tabs.used_on(s);  // the kernels read the track tables on s: a release is ordered there
-#endif
     // per-track output ranges: folded into stft3's staged-row epilogue (linear kinds), else one
     // reduction pass over the rows after the spectrogram launch
     const uint64_t n_tr = b->frame0.empty() ? 0 : b->frame0.size() - 1;
@@ -1060,6 +1085,9 @@ int batch_run(Batch* b, hipStream_t s) {
         launch_range_rows(static_cast<const float*>(b->desc.d_output), b->launch.trk_frame0, n_tr,
                           (uint32_t)b->plan->row_bins(), b->range, s))
         return set_error(THESIA_ERR_DEVICE, "range launch failed");
+#ifndef THESIA_DIAG_NO_LAST_USE  // (diagnostic build: the round-5 cache, for the test's control)
+    b->d_tabs.used_on(s);  // the kernels just enqueued on s read the track tables
+#endif
     return THESIA_OK;
 }
 

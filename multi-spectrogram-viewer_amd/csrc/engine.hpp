@@ -32,43 +32,53 @@ const char* last_error();
 // costs no device synchronisation (a hipFree costs ~160 us, profiles/r03_viewer).
 //
 // The cache's invariant (round 6): a block may be handed out again only after every use of it
-// has been ordered before the next user's work. A DevBuf therefore records the stream of its
-// last use (`use`, the allocation stream until used_on() names another); its release records an
-// event on that stream, and the cache hands the block out again at once only to an allocation on
-// that same stream (in-order behind the uses), to any other stream only once the event has
-// completed. Work on other streams must be joined into the last-use stream before the release
-// (the library's stream pool joins its forks back into the caller's stream; batch_run /
-// batches_run call used_on(s) for the batch's track tables). tests/test_gpu_multitrack.py
+// has been ordered before the next user's work. A block last used on its allocation stream (the
+// library stream) is released with an event recorded there and goes back out at once to the next
+// allocation on that stream (in order behind the uses), to other streams once the event has
+// completed. A block whose work ran on another stream -- a caller's, for a batch run there --
+// is marked by used_on(s) right after that work is enqueued: an event recorded on s then (the
+// stream may be gone by the release: only the event is kept), and the released block goes back
+// out only once that event has completed, on any stream. Work on the library's pool streams is
+// joined into the caller's stream before used_on (batches_run). tests/test_gpu_multitrack.py
 // test_block_cache_cross_stream_reuse checks a block released while a kernel on a busy caller
 // stream still reads it.
 struct DevBuf {
     void* p = nullptr;
     size_t bytes = 0;
-    hipStream_t st = nullptr;   // the stream it was allocated on
-    hipStream_t use = nullptr;  // the stream of its last use (nullptr: st)
-    bool pooled = false;        // a block of the cache (else a plain hipFree on release)
-    int dev = 0;                // the device it was allocated on
+    hipStream_t st = nullptr;      // the stream it was allocated on
+    hipEvent_t use_ev = nullptr;   // recorded after its last use on another stream (used_on)
+    bool foreign = false;          // last used on another stream: released behind use_ev only
+    bool pooled = false;           // a block of the cache (else a plain hipFree on release)
+    int dev = 0;                   // the device it was allocated on
     DevBuf() = default;
     DevBuf(const DevBuf&) = delete;
     DevBuf& operator=(const DevBuf&) = delete;
-    DevBuf(DevBuf&& o) noexcept : p(o.p), bytes(o.bytes), st(o.st), use(o.use), pooled(o.pooled), dev(o.dev) {
+    DevBuf(DevBuf&& o) noexcept
+        : p(o.p), bytes(o.bytes), st(o.st), use_ev(o.use_ev), foreign(o.foreign), pooled(o.pooled), dev(o.dev) {
         o.p = nullptr;
         o.bytes = 0;
+        o.use_ev = nullptr;
+        o.foreign = false;
     }
     DevBuf& operator=(DevBuf&& o) noexcept {
         if (this != &o) {
             release();
-            p = o.p; bytes = o.bytes; st = o.st; use = o.use; pooled = o.pooled; dev = o.dev;
-            o.p = nullptr; o.bytes = 0;
+            if (use_ev) (void)hipEventDestroy(use_ev);
+            p = o.p; bytes = o.bytes; st = o.st; use_ev = o.use_ev; foreign = o.foreign; pooled = o.pooled; dev = o.dev;
+            o.p = nullptr; o.bytes = 0; o.use_ev = nullptr; o.foreign = false;
         }
         return *this;
     }
-    ~DevBuf() { release(); }
+    ~DevBuf() {
+        release();
+        if (use_ev) (void)hipEventDestroy(use_ev);
+    }
     void release();
     int alloc(size_t n);
     int upload(const void* host, size_t n);  // alloc + copy (synchronous)
-    // the block's work now runs on (or is joined into) stream s: its release is ordered there
-    void used_on(hipStream_t s) { use = s; }
+    // the block's work has just been enqueued on (or joined into) stream s: its release is
+    // ordered behind that work (an event recorded on s now, unless s is the allocation stream)
+    void used_on(hipStream_t s);
     template <class T> T* as() const { return static_cast<T*>(p); }
 };
 

@@ -231,6 +231,23 @@ def test_block_cache_cross_stream_reuse():
     got = out_a.to_host(np.float32, (fa, bins))
     bb.close()
     assert hip.hipStreamDestroy(s2) == 0
+    assert np.array_equal(got, want)
+    # the caller's stream destroyed while the batch's kernel is still queued on it, before the
+    # batch is: the release keeps only the event recorded at that use
+    s3 = C.c_void_p()
+    assert hip.hipStreamCreateWithFlags(C.byref(s3), 1) == 0
+    out_a.zero()
+    for _ in range(10):
+        assert hip.hipMemcpyAsync(dst.ptr, src.ptr, C.c_size_t(big), 3, s3) == 0
+    ba = engine.Batch(plan, din, off_a, lens_a, out_a)
+    ba.run(stream=s3)
+    assert hip.hipStreamDestroy(s3) == 0
+    ba.close()
+    bb = engine.Batch(plan, din, off_b, lens_b, out_b)
+    bb.run()
+    engine.synchronize()
+    got = out_a.to_host(np.float32, (fa, bins))
+    bb.close()
     for b in (src, dst, out_a, out_b, ref, din):
         b.close()
     plan.close()
