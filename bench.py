@@ -67,7 +67,9 @@ def parse():
     p.add_argument("--output", choices=["mel_db", "amp_db", "power_db", "complex"], default="mel_db")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-exact", action="store_true",
-                   help="skip the bit-exact (reference-order kernel 7) line reported beside the default one")
+                   help="c4: skip the bit-exact (reference-order kernel 7) line reported beside the default "
+                        "one; c5: time the tolerance kernels as the line's path (default: kernel 7, the "
+                        "tolerance path beside it)")
     p.add_argument("--no-e2e", action="store_true", help="skip the PCIe-inclusive end-to-end sample")
     p.add_argument("--no-rfft-roofline", action="store_true",
                    help="skip the extra complex-output (window+rFFT kernel) roofline measurement")
@@ -536,16 +538,41 @@ def main_c5(args, ws, rank, pg, device):
         p.run_spectrograms()
         p.render(group=None, want_rgb=want_rgb)
 
-    for _ in range(args.warmup):
-        step()
-    engine.synchronize()
-    barrier(pg)
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        step()
-    engine.synchronize()
-    barrier(pg)
-    dt = max_over_ranks(pg, (time.perf_counter() - t0) / args.steps)
+    def use_kernel(k):
+        for _, _, _, b in p.groups:
+            b.set_option(engine.OPT_KERNEL, k)
+
+    def timed_steps(k, warm, n):
+        use_kernel(k)
+        for _ in range(warm):
+            step()
+        engine.synchronize()
+        barrier(pg)
+        t0 = time.perf_counter()
+        for _ in range(n):
+            step()
+        engine.synchronize()
+        barrier(pg)
+        return max_over_ranks(pg, (time.perf_counter() - t0) / n)
+
+    def spectrogram_phase():
+        # each batch's launch alone (HIP events per launch), and the step's spectrogram phase as
+        # it runs: the batches overlapped on the library streams
+        alone = [(pl.n_fft, b.total_frames, b.run_timed(3) / 3, b.kernel) for pl, _, _, b in p.groups]
+        engine.synchronize()
+        p.run_spectrograms()
+        with engine.EventTimer() as tm:
+            for _ in range(3):
+                p.run_spectrograms()
+        return alone, tm.ms / 3
+
+    # The line's path: north_star asks for the final u8 RGB bytes equal to the reference's, so the
+    # reported step runs every batch on the reference-order streaming kernels (7: stftq at n_fft
+    # 256 / 512 / 1024, stftr at 2048; RGB bytes equal to the oracle pipeline's,
+    # tests/test_gpu_parity.py test_e2e_rgb_c5_generator_exact); the tolerance kernels' step is
+    # reported beside it (tolerance_path). --kernel K / --no-exact measure that path instead.
+    main_k = 7 if (args.kernel == 0 and not args.no_exact) else args.kernel
+    dt = timed_steps(main_k, args.warmup, args.steps)
     step(want_rgb=True)  # untimed: pins the host readback buffers once (hipHostRegister)
     engine.synchronize()
     t0 = time.perf_counter()
@@ -553,16 +580,20 @@ def main_c5(args, ws, rank, pg, device):
         step(want_rgb=True)
     engine.synchronize()
     dt_host = max_over_ranks(pg, (time.perf_counter() - t0) / 3)
-    # spectrogram kernels alone (HIP events per group launch)
-    kms_batches = [(pl.n_fft, b.total_frames, b.run_timed(3) / 3, b.kernel) for pl, _, _, b in p.groups]
+    kms_batches, kms_overlap = spectrogram_phase()
     kms = sum(t for _, _, t, _ in kms_batches)
-    # the step's spectrogram phase as it runs: the batches overlapped on the library streams
-    engine.synchronize()
-    p.run_spectrograms()
-    with engine.EventTimer() as tm:
-        for _ in range(3):
-            p.run_spectrograms()
-    kms_overlap = tm.ms / 3
+    tol = None
+    if main_k == 7:
+        tol_dt = timed_steps(0, 2, args.steps)
+        tol_batches, tol_overlap = spectrogram_phase()
+        tol = {"kernel": 0, "ms_per_step": tol_dt * 1e3, "frames_per_s": p.total_frames / tol_dt,
+               "spectrogram_overlapped_ms": tol_overlap,
+               "spectrogram_kernel_ms": sum(t for _, _, t, _ in tol_batches),
+               "per_batch": [{"n_fft": nf, "kernel_ms": t, "kernel": kernel_name(k, nf)} for nf, _, t, k in tol_batches],
+               "exact_over_tolerance_step": dt / tol_dt,
+               "note": "the automatic (tolerance) kernels: rows within the stated fp32 tolerance of the "
+                       "oracle, RGB within the fast path's end-to-end contract (not bit-exact)"}
+        use_kernel(main_k)
     disp = p.display_timed(3)
     # the display's stored PMC record (this geometry, one GPU, render path 0): HBM traffic beside
     # the algorithmic bytes, and its VALU issue roofline (the passes are issue- and
@@ -631,31 +662,6 @@ def main_c5(args, ws, rank, pg, device):
         if rank == 0:
             print(json.dumps({"render_paths_ms": {str(q): {"median": float(np.median(t)), "min": float(min(t))}
                                                   for q, t in res.items()}}), flush=True)
-    exact = None
-    if args.kernel == 0 and ws == 1 and not args.no_exact:
-        # the same step with every batch on the reference-order streaming kernels (7: stftr at
-        # n_fft 2048, stftq at 256 / 512 / 1024): RGB bytes equal to the oracle pipeline's
-        # (tests/test_gpu_parity.py test_e2e_rgb_c5_generator_exact); reported beside the line
-        for _, _, _, b in p.groups:
-            b.set_option(engine.OPT_KERNEL, 7)
-        step()
-        engine.synchronize()
-        t0 = time.perf_counter()
-        for _ in range(max(3, args.steps // 2)):
-            step()
-        engine.synchronize()
-        ex_dt = (time.perf_counter() - t0) / max(3, args.steps // 2)
-        ex_batches = [(pl.n_fft, b.run_timed(3) / 3, b.kernel) for pl, _, _, b in p.groups]
-        p.run_spectrograms()
-        with engine.EventTimer() as tm:
-            for _ in range(3):
-                p.run_spectrograms()
-        exact = {"kernel": 7, "ms_per_step": ex_dt * 1e3, "frames_per_s": p.total_frames / ex_dt,
-                 "spectrogram_overlapped_ms": tm.ms / 3,
-                 "per_batch": [{"n_fft": nf, "kernel_ms": t, "kernel": kernel_name(k, nf)} for nf, t, k in ex_batches],
-                 "note": "reference operation order end to end: the RGB bytes equal the oracle pipeline's"}
-        for _, _, _, b in p.groups:
-            b.set_option(engine.OPT_KERNEL, 0)
     in_bytes = sum(t.pcm.nbytes for t in tracks)
     out_bytes = sum(b.total_frames * pl.row_bins * 4 for pl, _, _, b in p.groups)
     achieved = (in_bytes + out_bytes) / (kms * 1e-3) / 1e9
@@ -675,6 +681,9 @@ def main_c5(args, ws, rank, pg, device):
                        "tracks_per_gpu": len(tracks), "images_per_s": total / dt,
                        "spectrogram_batches": len(p.groups), "display_groups": p._n_disp,
                        "frames_per_gpu": p.total_frames,
+                       "spectrogram_path": (f"kernel {main_k}: reference-order streaming kernels (stftq at n_fft "
+                                            f"256-1024, stftr at 2048), RGB bytes equal to the oracle pipeline's"
+                                            if main_k == 7 else f"kernel {main_k} (0 = automatic, tolerance)"),
                        "ms_per_step_with_rgb_copied_to_host": dt_host * 1e3,
                        "parallelism": f"file-sharded x{ws} (LPT), one all_reduce of 3 scalars"},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
@@ -690,9 +699,9 @@ def main_c5(args, ws, rank, pg, device):
                          "per_batch_max_blocks_ms": mb_ms,
                          "per_batch": [{"n_fft": nf, "frames": fr, "kernel_ms": t, "kernel": kernel_name(k, nf)}
                                        for nf, fr, t, k in kms_batches],
-                         "bit_exact": exact,
                          "overlapped_note": "the step's spectrogram phase: the batches on the library "
                                             "streams (thesia_batches_run), HIP events on the library stream"},
+            "tolerance_path": tol,
             "roofline_display": disp,
             "roofline_display_valu_issue": disp_ic,
         }), flush=True)
