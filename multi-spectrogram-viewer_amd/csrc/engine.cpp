@@ -1048,8 +1048,8 @@ int batch_set_option(Batch* b, int option, int64_t value) {
 
 int batch_run(Batch* b, hipStream_t s) {
     if (!s) s = default_stream();
-    // per-track output ranges: folded into stft3's staged-row epilogue (linear kinds), else one
-    // reduction pass over the rows after the spectrogram launch
+    // per-track output ranges: folded into stft3's staged-row epilogue (linear kinds) and into
+    // kernel 7's (amp dB), else one reduction pass over the rows after the spectrogram launch
     const uint64_t n_tr = b->frame0.empty() ? 0 : b->frame0.size() - 1;
     const bool lin = b->launch.out_kind != OUT_COMPLEX && b->launch.out_kind != OUT_MEL &&
                      b->launch.out_kind != OUT_MEL_AMP_DB;
@@ -1062,7 +1062,12 @@ int batch_run(Batch* b, hipStream_t s) {
         if (rc) return set_error(rc == -2 ? THESIA_ERR_UNSUPPORTED : THESIA_ERR_DEVICE, "stftx launch failed");
     } else if (b->kernel == 7) {
         const bool r = b->plan->n_fft == 2048;
+        // amp dB rows fold their range into the epilogue (stftq / stftr RG instances)
+        const bool fold = b->range && b->launch.out_kind == OUT_AMP_DB;
+        b->launch.trk_range = fold ? b->range : nullptr;
         rc = r ? launch_stftr(b->launch, s) : launch_stftq(b->launch, s);
+        in_kernel = fold && rc == 0;
+        b->launch.trk_range = nullptr;
         if (rc)
             return set_error(rc == -2 ? THESIA_ERR_UNSUPPORTED : THESIA_ERR_DEVICE,
                              r ? "stftr launch failed" : "stftq launch failed");

@@ -254,11 +254,15 @@ constexpr int reg_pbits(int r, int ps) {
 // DIR (round 6): any other geometry -- the viewer's win < n_fft and hops (lib.rs:43-46: 80 / 160 / 221 /
 // 240 at n_fft 512 / 1024) -- with the same FFT and epilogue: every frame loads its n_fft samples
 // itself (no ring: L2 holds the overlap; an odd start, where the frame's points straddle the
-// sample pairs, reads its samples one by one), and the window step adds a per-position constant
-// after the product: -0 inside the window (x * w + -0 = x * w, bits unchanged), +0 in the
-// centring pads, where the reference's frame holds +0 (lib.rs:377-385 pads the windowed frame:
-// x * 0 alone would be -0 for x < 0).
-template <int NC, int KIND, int C, int INF, int WV, int VAR = 0, bool DIR = false>
+// sample pairs, reads its samples one by one), and the window step masks the product: x * w
+// inside the window (bits unchanged), +0 in the centring pads, where the reference's frame holds
+// +0 (lib.rs:377-385 pads the windowed frame and reads no sample there: x * 0 would be -0 for
+// x < 0 and NaN for a non-finite x).
+// RG (round 6, amp dB): the per-track range of the rows (a.trk_range: {ordered max, ordered min,
+// NaN seen}, Batch::range) folded into the epilogue -- max / min / NaN of each frame's values,
+// committed with one atomic triple per track a stream leaves -- instead of the separate pass over
+// the rows (range_rows_kernel); max and min are exact, so the triple is the pass's.
+template <int NC, int KIND, int C, int INF, int WV, int VAR = 0, bool DIR = false, bool RG = false>
 __global__ void __launch_bounds__(64 * WV)
 stftq_kernel(StftLaunch a, uint64_t fps) {
     constexpr int OKQ = KIND == OUT_COMPLEX ? 0 : (KIND == OUT_MEL || KIND == OUT_MEL_AMP_DB) ? 2 : 1;
@@ -273,7 +277,7 @@ stftq_kernel(StftLaunch a, uint64_t fps) {
     float* wtl = lds;
     float2* twl = reinterpret_cast<float2*>(lds + G::WL_FLOATS);
     float2* scl = reinterpret_cast<float2*>(lds + G::WL_FLOATS + G::TW_FLOATS);
-    float* wcl = lds + G::TAB_FLOATS;  // DIR: the window step's added constants (same layout)
+    float* wcl = lds + G::TAB_FLOATS;  // DIR: the window step's pad mask (same layout)
     float* work = lds + G::TAB_FLOATS + (DIR ? G::WL_FLOATS : 0);
     const exact::LogfEntry* logt = logf_tab_to_lds(lds + G::WL_FLOATS + G::TW_FLOATS + G::SC_FLOATS);
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -283,7 +287,8 @@ stftq_kernel(StftLaunch a, uint64_t fps) {
     for (int i = threadIdx.x; i < 2 * NC; i += kBlock) {  // window: lane row (w[2m], w[2m+1])
         const int m = i >> 1, l = m % L, n = m / L;
         wtl[l * G::WL_STRIDE + 2 * n + (i & 1)] = a.wpad[i];
-        if constexpr (DIR) wcl[l * G::WL_STRIDE + 2 * n + (i & 1)] = i >= a.pad_left && i < a.pad_left + a.win ? -0.0f : 0.0f;
+        if constexpr (DIR)  // the window step's mask: all ones inside the window, 0 in the pads
+            wcl[l * G::WL_STRIDE + 2 * n + (i & 1)] = __uint_as_float(i >= a.pad_left && i < a.pad_left + a.win ? ~0u : 0u);
     }
     for (int i = threadIdx.x; i < NC; i += kBlock) {
         twl[i] = a.tw1[i];
@@ -307,6 +312,26 @@ stftq_kernel(StftLaunch a, uint64_t fps) {
     int hint = -1;
     uint64_t g_beg = 1, g_end = 0, base = 0;
     int64_t n = 0;
+    // RG: the range of the rows this frame slot writes for its current track (r_trk)
+    float r_max = -INFINITY, r_min = INFINITY;
+    int r_nan = 0, r_trk = -1;
+    auto r_flush = [&]() {  // the slot's L lanes (xor stays inside the group), then one atomic triple
+#pragma unroll
+        for (int m = L / 2; m >= 1; m >>= 1) {
+            r_max = fmaxf(r_max, __shfl_xor(r_max, m));
+            r_min = fminf(r_min, __shfl_xor(r_min, m));
+            r_nan |= __shfl_xor(r_nan, m);
+        }
+        if ((lane & (L - 1)) == 0) {
+            int* rp = a.trk_range + 3 * r_trk;
+            atomicMax(rp, range_ord(r_max));
+            atomicMin(rp + 1, range_ord(r_min));
+            if (r_nan) atomicOr(rp + 2, 1);
+        }
+        r_max = -INFINITY;
+        r_min = INFINITY;
+        r_nan = 0;
+    };
     for (uint64_t it = 0; it < fps; ++it) {  // wave-uniform trip count
         const uint64_t g = g0 + it;
         const bool valid = g < g1;
@@ -381,13 +406,14 @@ stftq_kernel(StftLaunch a, uint64_t fps) {
                 v[2 * q] = make_float2(raw[2 * q].x * w.x, raw[2 * q].y * w.y);
                 v[2 * q + 1] = make_float2(raw[2 * q + 1].x * w.z, raw[2 * q + 1].y * w.w);
             }
-            if constexpr (DIR) {  // -0 inside the window (bits unchanged), +0 in the pads
-                const float4* cr = reinterpret_cast<const float4*>(wcl + lj * G::WL_STRIDE);
+            if constexpr (DIR) {  // x * w inside the window (bits unchanged), +0 in the pads, whatever x
+                const uint4* cr = reinterpret_cast<const uint4*>(wcl + lj * G::WL_STRIDE);
+                auto msk = [](float x, unsigned m) { return __uint_as_float(__float_as_uint(x) & m); };
 #pragma unroll
                 for (int q = 0; q < P / 2; ++q) {
-                    const float4 c = cr[q];
-                    v[2 * q] = make_float2(v[2 * q].x + c.x, v[2 * q].y + c.y);
-                    v[2 * q + 1] = make_float2(v[2 * q + 1].x + c.z, v[2 * q + 1].y + c.w);
+                    const uint4 c = cr[q];
+                    v[2 * q] = make_float2(msk(v[2 * q].x, c.x), msk(v[2 * q].y, c.y));
+                    v[2 * q + 1] = make_float2(msk(v[2 * q + 1].x, c.z), msk(v[2 * q + 1].y, c.w));
                 }
             }
         }
@@ -547,6 +573,16 @@ stftq_kernel(StftLaunch a, uint64_t fps) {
             float* frow = static_cast<float*>(a.out) + g * (uint64_t)nfl;
             const int sh = (int)((reinterpret_cast<uintptr_t>(frow) >> 2) & 3);
             float* st = region + sh;
+            // (RG) this frame's values in this lane: every bin is in some lane's fo, bin NC / 2 in all
+            float f_max = -INFINITY, f_min = INFINITY;
+            int f_nan = 0;
+            auto fold = [&](float x) {
+                if constexpr (RG && OKQ == 1) {
+                    f_max = fmaxf(f_max, x);
+                    f_min = fminf(f_min, x);
+                    f_nan |= x != x;
+                }
+            };
 #pragma unroll
             for (int i = 0; i < NP; ++i) {
                 const int k = lj + L * i;
@@ -558,8 +594,11 @@ stftq_kernel(StftLaunch a, uint64_t fps) {
                 } else {
                     st[k] = fo[2 * i];
                     st[NC - k] = fo[2 * i + 1];
+                    fold(fo[2 * i]);
+                    fold(fo[2 * i + 1]);
                 }
             }
+            if constexpr (OKQ == 1) fold(fo[2 * NP]);
             if (lj == 0) {
                 if constexpr (OKQ == 0) {
                     st[NC] = xo[2 * NP].x;
@@ -571,8 +610,22 @@ stftq_kernel(StftLaunch a, uint64_t fps) {
             wave_lds_sync();
             if (valid) store_row_b128<L>(frow, sh, region, nfl, lj);
             wave_lds_sync();
+            if constexpr (RG && OKQ == 1) {  // the slot's track changed: commit the previous one's
+                const int t = valid ? hint : -1;
+                if (t != r_trk) {  // uniform over the slot's lanes
+                    if (r_trk >= 0) r_flush();
+                    r_trk = t;
+                }
+                if (valid) {
+                    r_max = fmaxf(r_max, f_max);
+                    r_min = fminf(r_min, f_min);
+                    r_nan |= f_nan;
+                }
+            }
         }
     }
+    if constexpr (RG && OKQ == 1)
+        if (r_trk >= 0) r_flush();  // the slot's last track
 }
 
 // ------------------------------------------------------------------------------------------
@@ -583,22 +636,22 @@ static int ldsq_bytes(int wv, bool dir = false) {
     return (GeoQ<NC>::TAB_FLOATS + (dir ? GeoQ<NC>::WL_FLOATS : 0) + wv * GeoQ<NC>::FPW * GeoQ<NC>::RS) * 4;
 }
 
-template <int NC, int KIND, int C, int INF, int WV, int VAR = 0, bool DIR = false>
+template <int NC, int KIND, int C, int INF, int WV, int VAR = 0, bool DIR = false, bool RG = false>
 static int launchq_k(const StftLaunch& a, hipStream_t s) {
 #ifdef THESIA_EXPERIMENTS
     if constexpr (VAR == 0 && KIND == OUT_AMP_DB && C == 1 && INF == IN_S16) {
         const char* e = getenv("THESIA_STFT_VARIANT");
         const int v = e ? atoi(e) : 0;
-        if (v == 1) return launchq_k<NC, KIND, C, INF, WV, 1>(a, s);
-        if (v == 3) return launchq_k<NC, KIND, C, INF, WV, 3>(a, s);
-        if (v == 4) return launchq_k<NC, KIND, C, INF, WV, 4>(a, s);
-        if (v == 12 && WV != 12) return launchq_k<NC, KIND, C, INF, 12, 0>(a, s);
-        if (v == 16) return launchq_k<NC, KIND, C, INF, WV, 16>(a, s);
+        if (v == 1) return launchq_k<NC, KIND, C, INF, WV, 1, DIR, RG>(a, s);
+        if (v == 3) return launchq_k<NC, KIND, C, INF, WV, 3, DIR, RG>(a, s);
+        if (v == 4) return launchq_k<NC, KIND, C, INF, WV, 4, DIR, RG>(a, s);
+        if (v == 12 && WV != 12) return launchq_k<NC, KIND, C, INF, 12, 0, DIR, RG>(a, s);
+        if (v == 16) return launchq_k<NC, KIND, C, INF, WV, 16, DIR, RG>(a, s);
     }
 #endif
     const int lds = ldsq_bytes<NC>(WV, DIR);
     if (lds > 163840) return -2;
-    auto kern = stftq_kernel<NC, KIND, C, INF, WV, VAR, DIR>;
+    auto kern = stftq_kernel<NC, KIND, C, INF, WV, VAR, DIR, RG>;
     if (hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize, lds) !=
         hipSuccess)
         return -1;
@@ -624,7 +677,9 @@ static int launchq_c(const StftLaunch& a, hipStream_t s) {
         case OUT_COMPLEX: return launchq_k<NC, OUT_COMPLEX, C, INF, WV, 0, DIR>(a, s);
         case OUT_MAG: return launchq_k<NC, OUT_MAG, C, INF, WV, 0, DIR>(a, s);
         case OUT_POWER: return launchq_k<NC, OUT_POWER, C, INF, WV, 0, DIR>(a, s);
-        case OUT_AMP_DB: return launchq_k<NC, OUT_AMP_DB, C, INF, WV, 0, DIR>(a, s);
+        case OUT_AMP_DB:  // (the range folded in when the batch asks for it: the C5 / viewer kind)
+            return a.trk_range ? launchq_k<NC, OUT_AMP_DB, C, INF, WV, 0, DIR, true>(a, s)
+                               : launchq_k<NC, OUT_AMP_DB, C, INF, WV, 0, DIR>(a, s);
         case OUT_POWER_DB: return launchq_k<NC, OUT_POWER_DB, C, INF, WV, 0, DIR>(a, s);
         case OUT_MEL: return launchq_k<NC, OUT_MEL, C, INF, WV, 0, DIR>(a, s);
         case OUT_MEL_AMP_DB: return launchq_k<NC, OUT_MEL_AMP_DB, C, INF, WV, 0, DIR>(a, s);

@@ -123,9 +123,12 @@ __device__ __forceinline__ void melr_stream(const int4* meta, const float4* wt, 
 // stream, 4 no untangle / |X| / mel (the FFT alone).
 // DIR (round 6): any other geometry with n_fft 2048 -- the viewer's win 1764 / 1920 and hops 441 /
 // 480 (lib.rs:43-46, 44.1 / 48 kHz) -- as stftq_kernel's DIR: every frame loads its samples itself
-// (no ring; an odd start sample by sample) and the window step adds -0 inside the window, +0 in
-// the centring pads (the reference pads the windowed frame with +0, lib.rs:377-385).
-template <int KIND, int C, int INF, int WV, int VAR = 0, bool DIR = false>
+// (no ring; an odd start sample by sample) and the window step keeps x * w inside the window and
+// +0 in the centring pads, whatever the sample there (a mask: the reference pads the windowed
+// frame with +0 and reads no sample there, lib.rs:377-385).
+// RG (round 6, amp dB): the per-track range of the rows folded into the epilogue (Batch::range,
+// as stftq_kernel's RG) instead of the separate pass over the rows.
+template <int KIND, int C, int INF, int WV, int VAR = 0, bool DIR = false, bool RG = false>
 __global__ void __launch_bounds__(64 * WV)
 stftr_kernel(StftLaunch a, uint64_t fps) {
     using G = GeoR;
@@ -140,7 +143,7 @@ stftr_kernel(StftLaunch a, uint64_t fps) {
     float* wtl = lds;
     float2* twl = reinterpret_cast<float2*>(lds + G::WL_FLOATS);
     float2* scl = reinterpret_cast<float2*>(lds + G::WL_FLOATS + G::TW_FLOATS);
-    float* wcl = lds + G::TAB_FLOATS;  // DIR: the window step's added constants (same layout)
+    float* wcl = lds + G::TAB_FLOATS;  // DIR: the window step's pad mask (same layout)
     float* work = lds + G::TAB_FLOATS + (DIR ? G::WL_FLOATS : 0);
     const exact::LogfEntry* logt = logf_tab_to_lds(lds + G::WL_FLOATS + G::TW_FLOATS + G::SC_FLOATS);
     int4* pm_lds = reinterpret_cast<int4*>(work + WV * G::REGION);
@@ -151,7 +154,8 @@ stftr_kernel(StftLaunch a, uint64_t fps) {
     for (int i = threadIdx.x; i < 2 * NC; i += kBlock) {  // window: lane row (w[2m], w[2m+1])
         const int m = i >> 1, l = m % L, n = m / L;
         wtl[l * G::WL_STRIDE + 2 * n + (i & 1)] = a.wpad[i];
-        if constexpr (DIR) wcl[l * G::WL_STRIDE + 2 * n + (i & 1)] = i >= a.pad_left && i < a.pad_left + a.win ? -0.0f : 0.0f;
+        if constexpr (DIR)  // the window step's mask: all ones inside the window, 0 in the pads
+            wcl[l * G::WL_STRIDE + 2 * n + (i & 1)] = __uint_as_float(i >= a.pad_left && i < a.pad_left + a.win ? ~0u : 0u);
     }
     for (int i = threadIdx.x; i < NC; i += kBlock) {
         twl[i] = a.tw1[i];
@@ -179,6 +183,26 @@ stftr_kernel(StftLaunch a, uint64_t fps) {
     int hint = -1;
     uint64_t g_beg = 1, g_end = 0, base = 0;
     int64_t n = 0;
+    // RG: the range of the rows this wave writes for its current track (r_trk)
+    float r_max = -INFINITY, r_min = INFINITY;
+    int r_nan = 0, r_trk = -1;
+    auto r_flush = [&]() {
+#pragma unroll
+        for (int m = 32; m >= 1; m >>= 1) {
+            r_max = fmaxf(r_max, __shfl_xor(r_max, m));
+            r_min = fminf(r_min, __shfl_xor(r_min, m));
+            r_nan |= __shfl_xor(r_nan, m);
+        }
+        if (lane == 0) {
+            int* rp = a.trk_range + 3 * r_trk;
+            atomicMax(rp, range_ord(r_max));
+            atomicMin(rp + 1, range_ord(r_min));
+            if (r_nan) atomicOr(rp + 2, 1);
+        }
+        r_max = -INFINITY;
+        r_min = INFINITY;
+        r_nan = 0;
+    };
     for (uint64_t it = 0; it < fps; ++it) {  // wave-uniform trip count
         const uint64_t g = g0 + it;
         const bool valid = g < g1;
@@ -255,13 +279,14 @@ stftr_kernel(StftLaunch a, uint64_t fps) {
                 v[2 * q] = make_float2(raw[2 * q].x * w.x, raw[2 * q].y * w.y);
                 v[2 * q + 1] = make_float2(raw[2 * q + 1].x * w.z, raw[2 * q + 1].y * w.w);
             }
-            if constexpr (DIR) {  // -0 inside the window (bits unchanged), +0 in the pads
-                const float4* cr = reinterpret_cast<const float4*>(wcl + lj * G::WL_STRIDE);
+            if constexpr (DIR) {  // x * w inside the window (bits unchanged), +0 in the pads, whatever x
+                const uint4* cr = reinterpret_cast<const uint4*>(wcl + lj * G::WL_STRIDE);
+                auto msk = [](float x, unsigned m) { return __uint_as_float(__float_as_uint(x) & m); };
 #pragma unroll
                 for (int q = 0; q < P / 2; ++q) {
-                    const float4 c = cr[q];
-                    v[2 * q] = make_float2(v[2 * q].x + c.x, v[2 * q].y + c.y);
-                    v[2 * q + 1] = make_float2(v[2 * q + 1].x + c.z, v[2 * q + 1].y + c.w);
+                    const uint4 c = cr[q];
+                    v[2 * q] = make_float2(msk(v[2 * q].x, c.x), msk(v[2 * q].y, c.y));
+                    v[2 * q + 1] = make_float2(msk(v[2 * q + 1].x, c.z), msk(v[2 * q + 1].y, c.w));
                 }
             }
         }
@@ -341,6 +366,9 @@ stftr_kernel(StftLaunch a, uint64_t fps) {
             xkp.y = 0.5f * ((pdim - sckp.x * sim) - sckp.y * pdre);
         };
         float* row = region;
+        constexpr bool FOLD = RG && !CPLX && !MEL;
+        float f_max = -INFINITY, f_min = INFINITY;  // (FOLD) this frame's values in this lane
+        int f_nan = 0;
         const int sh = MEL ? 0
                      : (int)((reinterpret_cast<uintptr_t>(static_cast<float*>(a.out) + g * (uint64_t)(CPLX ? 2 * F : F)) >> 2) & 3);
         auto emit = [&](int k, float2 x) {
@@ -357,6 +385,11 @@ stftr_kernel(StftLaunch a, uint64_t fps) {
                     if constexpr (KIND == OUT_AMP_DB) val = rdb(val, a.log_amin, 1e-18f, 20.0f, logt);
                 }
                 row[sh + k] = val;
+                if constexpr (FOLD) {
+                    f_max = fmaxf(f_max, val);
+                    f_min = fminf(f_min, val);
+                    f_nan |= val != val;
+                }
             }
         };
         const float2* scc = scl + col;              // sin_cos of bins col + 64 r
@@ -399,8 +432,22 @@ stftr_kernel(StftLaunch a, uint64_t fps) {
             constexpr int nfl = CPLX ? 2 * F : F;
             float* frow = static_cast<float*>(a.out) + g * (uint64_t)nfl;
             if (valid) store_row_b128<L>(frow, sh, region, nfl, lj);
+            if constexpr (FOLD) {  // the wave's track changed: commit the previous one's
+                const int t = valid ? hint : -1;
+                if (t != r_trk) {  // wave-uniform
+                    if (r_trk >= 0) r_flush();
+                    r_trk = t;
+                }
+                if (valid) {
+                    r_max = fmaxf(r_max, f_max);
+                    r_min = fminf(r_min, f_min);
+                    r_nan |= f_nan;
+                }
+            }
         }
     }
+    if constexpr (RG && !CPLX && !MEL)
+        if (r_trk >= 0) r_flush();  // the wave's last track
 }
 
 // ------------------------------------------------------------------------------------------
@@ -415,7 +462,7 @@ static int ldsr_bytes(const StftLaunch& a, int wv) {
     return (GeoR::TAB_FLOATS + (r_canon(a) ? 0 : GeoR::WL_FLOATS) + wv * GeoR::REGION) * 4 + meltab;
 }
 
-template <int KIND, int C, int INF, int WV, int VAR = 0, bool DIR = false>
+template <int KIND, int C, int INF, int WV, int VAR = 0, bool DIR = false, bool RG = false>
 static int launchr_k(const StftLaunch& a, hipStream_t s) {
 #ifdef THESIA_EXPERIMENTS
     if constexpr (VAR == 0 && KIND == OUT_MEL_AMP_DB && C == 2 && INF == IN_F32 && WV == 12) {
@@ -429,7 +476,7 @@ static int launchr_k(const StftLaunch& a, hipStream_t s) {
 #endif
     const int lds = ldsr_bytes(a, WV);
     if (lds > 163840) return -2;
-    auto kern = stftr_kernel<KIND, C, INF, WV, VAR, DIR>;
+    auto kern = stftr_kernel<KIND, C, INF, WV, VAR, DIR, RG>;
     if (hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize, lds) !=
         hipSuccess)
         return -1;
@@ -460,7 +507,9 @@ static int launchr_c(const StftLaunch& a, hipStream_t s) {
         case OUT_COMPLEX: return launchr_w<OUT_COMPLEX, C, INF, DIR>(a, s);
         case OUT_MAG: return launchr_w<OUT_MAG, C, INF, DIR>(a, s);
         case OUT_POWER: return launchr_w<OUT_POWER, C, INF, DIR>(a, s);
-        case OUT_AMP_DB: return launchr_w<OUT_AMP_DB, C, INF, DIR>(a, s);
+        case OUT_AMP_DB:  // (the range folded in when the batch asks for it: the C5 / viewer kind)
+            return a.trk_range ? launchr_k<OUT_AMP_DB, C, INF, 12, 0, DIR, true>(a, s)
+                               : launchr_w<OUT_AMP_DB, C, INF, DIR>(a, s);
         case OUT_POWER_DB: return launchr_w<OUT_POWER_DB, C, INF, DIR>(a, s);
         case OUT_MEL: return launchr_w<OUT_MEL, C, INF, DIR>(a, s);
         case OUT_MEL_AMP_DB: return launchr_w<OUT_MEL_AMP_DB, C, INF, DIR>(a, s);

@@ -117,3 +117,75 @@ def test_amp_db_fold_instances(n_fft, ch, fmt):
                 ri = r[int(b.frame0[i]):int(b.frame0[i + 1])]
                 assert not nan[i] and mx[i] == ri.max() and mn[i] == ri.min(), i
     assert np.array_equal(rows[0], rows[1])
+
+
+def _k7_rows_and_ranges(plan, din, offs, lens, T, inf, ch, kernel, max_blocks, with_range):
+    dout = engine.DeviceBuffer(T * plan.row_bins * 4)
+    b = engine.Batch(plan, din, offs, lens, dout, input_format=inf, channels=ch, fold_mono=True, kernel=kernel,
+                     max_blocks=max_blocks)
+    assert b.kernel == kernel
+    drange = engine.DeviceBuffer(12 * len(lens))
+    if with_range:
+        b.set_option(engine.OPT_RANGE, drange.ptr.value)
+    for _ in range(2):  # the slots are re-initialised by every run
+        b.run()
+    engine.synchronize()
+    rows = dout.to_host(np.float32, (T, plan.row_bins))
+    rr = engine.ranges_read(drange, len(lens)) if with_range else None
+    f0 = [int(v) for v in b.frame0]
+    b.close()
+    dout.close()
+    drange.close()
+    return rows, rr, f0
+
+
+@pytest.mark.parametrize("geo", [(256, 256, 64), (512, 512, 128), (1024, 1024, 256), (2048, 2048, 512),
+                                 (1024, 884, 221), (2048, 1920, 480), (2048, 1764, 441)])
+@pytest.mark.parametrize("ch,fmt,max_blocks", [(1, "s16", 0), (2, "f32", 3), (1, "f32", 1)])
+def test_kernel7_amp_db_range_fold(geo, ch, fmt, max_blocks):
+    """Round 6: kernel 7's amp dB rows fold the per-track range into the epilogue (stftq / stftr RG
+    instances) instead of the pass over the rows: the rows are the same bits with and without the
+    range option, and the (max, min, NaN) triples equal kernel 9's (the separate pass) and the
+    rows' max / min -- ragged tracks, streams crossing track boundaries (max_blocks), a track with
+    a NaN sample (its |X| is NaN; decibel.rs's amin clamp takes it to the floor: no NaN rows) and a
+    silent one."""
+    n_fft, win, hop = geo
+    if (win, hop) != (n_fft, n_fft // 4) and fmt != "f32":
+        pytest.skip("kernel 7 takes the viewer geometries from f32 (MultiTrack's pool)")
+    rng = np.random.default_rng(n_fft + win + hop + ch)
+    lens = [n_fft * 3 + 17, n_fft * 40 + 5, win - 1, n_fft * 11 + 300, n_fft * 2, n_fft * 6 + 9]
+    tracks = []
+    for i, n in enumerate(lens):
+        t = rng.standard_normal((n, ch)) * np.float32(10.0) ** rng.uniform(-4, -0.5)
+        if i == 4:
+            t[:] = 0.0  # silent: every row at the dB floor
+        tracks.append(t)
+    if fmt == "f32":
+        tracks = [t.astype(np.float32) for t in tracks]
+        tracks[3][n_fft * 5 + 7, 0] = np.nan
+        inf = engine.IN_F32
+    else:
+        tracks = [(t * 32767).clip(-32768, 32767).astype(np.int16) for t in tracks]
+        inf = engine.IN_S16
+    flat = np.concatenate([t.reshape(-1) for t in tracks])
+    offs = np.cumsum([0] + [t.size for t in tracks[:-1]]).astype(np.uint64)
+    plan = engine.Plan(n_fft, win, hop, engine.OUT_AMP_DB, sr=48000)
+    T = engine.Batch.frames_for(plan, lens)
+    din = engine.DeviceBuffer.from_host(flat)
+    rows0, _, _ = _k7_rows_and_ranges(plan, din, offs, lens, T, inf, ch, 7, max_blocks, False)
+    rows7, (mx7, mn7, nan7), f0 = _k7_rows_and_ranges(plan, din, offs, lens, T, inf, ch, 7, max_blocks, True)
+    rows9, (mx9, mn9, nan9), _ = _k7_rows_and_ranges(plan, din, offs, lens, T, inf, ch, 9, 0, True)
+    assert np.array_equal(rows0.view(np.uint32), rows7.view(np.uint32))
+    assert np.array_equal(rows7.view(np.uint32), rows9.view(np.uint32))
+    assert np.array_equal(mx7.view(np.uint32), mx9.view(np.uint32))
+    assert np.array_equal(mn7.view(np.uint32), mn9.view(np.uint32))
+    assert np.array_equal(nan7 != 0, nan9 != 0)
+    for i in range(len(lens)):
+        r = rows7[f0[i]:f0[i + 1]]
+        bad = np.isnan(r)
+        assert bool(nan7[i]) == bool(bad.any()), i
+        ok = r[~bad]
+        if ok.size:
+            assert mx7[i] == ok.max() and mn7[i] == ok.min(), (i, mx7[i], ok.max(), mn7[i], ok.min())
+    din.close()
+    plan.close()
