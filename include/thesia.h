@@ -209,7 +209,10 @@ int thesia_batch_kernel_info(const thesia_batch* batch, int* lds_bytes, int* til
  * n_fft 2048, stftq_kernel at 256 / 512 / 1024; win = n_fft, hop = n_fft/4 with f32 / s16 input,
  * or any even win <= n_fft and any hop with f32 input -- the viewer's geometries, lib.rs:43-46:
  * rows equal the reference's bit for bit), 9 stftx_kernel (the reference's operation order, any
- * geometry). */
+ * geometry). At win < n_fft, 7 and 9 read no sample in a frame's centring pads (lib.rs:377-385),
+ * so a non-finite sample there leaves the frame finite, as in the reference; the tolerance
+ * kernels (1-5) multiply the pads by the zero-padded window, and such a frame comes out
+ * non-finite. */
 int thesia_batch_kernel(const thesia_batch* batch, int* kernel);
 
 /* Named alternatives of a batch (none changes what is computed, only how; all results stay
@@ -232,7 +235,7 @@ typedef enum {
     /* a device buffer of 3 int32 per track (value = its address, 0 = off): every run also
      * leaves each track's max / min over its output rows and a NaN flag there (the per-track
      * reduction of update_spec_greys, lib.rs:194-207), folded into the streaming kernel's row
-     * epilogue for the linear kinds, else one pass over the rows; read with
+     * epilogue (stft3: the linear kinds; kernel 7: amp dB), else one pass over the rows; read with
      * thesia_batch_ranges_read. Real output kinds only. */
     THESIA_BATCH_OPT_RANGE = 4,
     /* mel projection of stft5_kernel (the mel kinds at n_fft 2048): 0 = automatic, 1 = the
