@@ -38,18 +38,22 @@ struct GeoQ {
     static constexpr int B = NC == 128 ? 7 : NC == 256 ? 8 : 9;
     static constexpr int NL = L == 16 ? 4 : 5, NR = P == 8 ? 3 : 4;
     static constexpr int NLEV = (B % 2) ? 1 + (B - 3) / 2 : B / 2;
-    static constexpr int WL_STRIDE = 2 * P + 4, WL_FLOATS = L * WL_STRIDE;
-    static constexpr int TW_FLOATS = 2 * NC, SC_FLOATS = 2 * NC + 4;
+    // (the tables padded to 128-byte multiples: the frame regions after them start 128-byte
+    // aligned, which the swizzled accesses below need)
+    static constexpr int WL_STRIDE = 2 * P + 4, WL_FLOATS = (L * WL_STRIDE + 31) / 32 * 32;
+    static constexpr int TW_FLOATS = 2 * (NC + NC / 32), SC_FLOATS = 2 * NC + 4;  // twiddles: tpad
     static constexpr int LOGT_FLOATS = 64;  // logf's table (exact_math.hpp kLogfT), LDS copy
-    static constexpr int TAB_FLOATS = WL_FLOATS + TW_FLOATS + SC_FLOATS + LOGT_FLOATS;
-    // a frame's region: Z (2 NC floats), later the staged row (complex: 2F floats from sh <= 3)
-    // (or, during the FFT, the relayout of the NC points: 2 NC floats plus one float2 of padding
-    // per 16, relayout_pad)
-    static constexpr int RS_ROW = (2 * F + 3 + 3) / 4 * 4;
-    static constexpr int RS_RELAYOUT = (2 * (NC + NC / 16) + 3) / 4 * 4;
-    static constexpr int RS = RS_ROW > RS_RELAYOUT ? RS_ROW : RS_RELAYOUT;
+    static constexpr int TAB_FLOATS = (WL_FLOATS + TW_FLOATS + SC_FLOATS + LOGT_FLOATS + 31) / 32 * 32;
+    // a frame's region: the relayouts and the Z row (NC float2 at swizzled places; the untangle's
+    // partner read of lane 0 at i = 0, whose value is not used, may reach NC + 15), later the staged
+    // row (complex: 2F floats from sh <= 3, 16 floats further in the odd frame slots of a 16-lane
+    // layout). The stride is 32 mod 64 dwords: a 32-lane LDS read spans two 16-lane frame slots,
+    // which then fall on the two halves of the 64 banks.
+    static constexpr int RS_NEED0 = 2 * F + 3 + (L == 16 ? 16 : 0), RS_NEED1 = 2 * NC + 32;
+    static constexpr int RS_NEED = RS_NEED0 > RS_NEED1 ? RS_NEED0 : RS_NEED1;
+    static constexpr int RS = (RS_NEED + 31) / 64 * 64 + 32;
     static_assert(L * P == NC && (1 << NL) == L && (1 << NR) == P && P % 4 == 0, "geometry");
-    static_assert(RS >= 2 * NC && RS % 4 == 0, "region");
+    static_assert(RS >= RS_NEED && RS % 64 == 32 && TAB_FLOATS % 32 == 0 && WL_FLOATS % 32 == 0, "region");
 };
 
 struct QLev {
@@ -213,6 +217,75 @@ constexpr int reg_mbits(int r) {
 // Separable: pad(ml | mr) = pad(ml) + pad(mr) for disjoint bits.
 __host__ __device__ constexpr int relayout_pad(int m) { return m + (m >> 4); }
 
+// LDS swizzles (round 6). The frame's points sit in its region at index
+// x ^ G(x >> 4) (float2 units): a GF(2)-linear map of the index's bits >= 4 onto its bits 0-3,
+// one 4-bit image per bit (REL: the relayouts' point index m; Z: the Z row's bin p). The images
+// (scratch search over the rule) make every relayout's write (ds_write_b64: 16-lane groups,
+// banks mod 32) and read (ds_read_b64: 32-lane groups, banks mod 64, two 16-lane frame slots RS
+// apart) and the Z row's write conflict-free; relayout_pad's padding left them 2-8-way. Linear:
+// swz(a ^ b) = swz(a) ^ swz(b) for disjoint bits, so an access is a per-lane byte base (128-byte
+// aligned region + 8 swz(lane part)) XOR a compile-time constant (8 x the register part's bits
+// 0-3) plus an immediate offset (its bits >= 4).
+template <int NC> struct SwzQ;
+template <> struct SwzQ<128> {
+    static constexpr int REL[5] = {5, 10, 0, 0, 0}, Z[5] = {4, 0, 0, 0, 0};
+};
+template <> struct SwzQ<256> {
+    static constexpr int REL[5] = {5, 10, 0, 0, 0}, Z[5] = {1, 2, 0, 0, 0};
+};
+template <> struct SwzQ<512> {
+    static constexpr int REL[5] = {4, 9, 6, 0, 0}, Z[5] = {1, 2, 4, 0, 0};
+};
+template <int NC, bool ZR>
+__host__ __device__ constexpr int swzq(int x) {
+    int o = x;
+    for (int h = 0; h < 5; ++h)
+        if ((x >> (4 + h)) & 1) o ^= ZR ? SwzQ<NC>::Z[h] : SwzQ<NC>::REL[h];
+    return o;
+}
+// swzq for a run-time x < 32 (only bit 4 can be high)
+template <int NC, bool ZR>
+__device__ __forceinline__ int swzq_small(int x) {
+    constexpr int g = ZR ? SwzQ<NC>::Z[0] : SwzQ<NC>::REL[0];
+    return x ^ ((x & 16) ? g : 0);
+}
+// twiddle table index: one float2 of padding per 32 (the levels' lanes read tw[j t] at strides
+// that put 4-16 distinct j on one bank)
+__host__ __device__ constexpr int tpad(int x) { return x + (x >> 5); }
+__device__ __forceinline__ void ldsw2(float* base, uint32_t a, float2 v) {
+    *reinterpret_cast<float2*>(reinterpret_cast<char*>(base) + a) = v;
+}
+__device__ __forceinline__ float2 ldsr2(const float* base, uint32_t a) {
+    return *reinterpret_cast<const float2*>(reinterpret_cast<const char*>(base) + a);
+}
+// the lane part of a relayout's swizzled point index (the layout of lane_mbits<NC, T, NEW>): the
+// XOR of the images of the m bits the lane holds
+template <int NC, int T, bool NEW>
+__device__ __forceinline__ int lane_swz_m(int lj) {
+    using G = GeoQ<NC>;
+    int o = 0;
+    static_for<0, G::B>([&](auto bc) {
+        constexpr int b = decltype(bc)::value;
+        constexpr bool init = !NEW && T == 0;
+        constexpr int kind = init ? (b < G::NL ? 0 : 1) : QS<NC>::S.lev[NEW ? T : T - 1].kind[b];
+        constexpr int bit = init ? (b < G::NL ? b : b - G::NL) : QS<NC>::S.lev[NEW ? T : T - 1].bit[b];
+        if constexpr (kind == 0) o ^= ((lj >> bit) & 1) ? swzq<NC, false>(1 << b) : 0;
+    });
+    return o;
+}
+// the lane part of the Z row's swizzled bin index (the last level's layout)
+template <int NC>
+__device__ __forceinline__ int lane_swz_p(int lj) {
+    constexpr int T = GeoQ<NC>::NLEV - 1;
+    constexpr QLev q = QS<NC>::S.lev[T];
+    int o = 0;
+    static_for<0, GeoQ<NC>::B>([&](auto bc) {
+        constexpr int b = decltype(bc)::value;
+        if constexpr (q.kind[b] == 0) o ^= ((lj >> q.bit[b]) & 1) ? swzq<NC, true>(1 << QS<NC>::S.pbit[b]) : 0;
+    });
+    return o;
+}
+
 // the lane part of sum over m bits b with pbit[b] < PS held in lane bits of ((lane bit) << pbit)
 template <int NC, int T, bool BELOW>
 __device__ __forceinline__ int lane_pbits(int lj, int ps) {
@@ -264,6 +337,8 @@ constexpr int reg_pbits(int r, int ps) {
 // the rows (range_rows_kernel); max and min are exact, so the triple is the pass's.
 template <int NC, int KIND, int C, int INF, int WV, int VAR = 0, bool DIR = false, bool RG = false>
 __global__ void __launch_bounds__(64 * WV)
+// two blocks per CU for mono input at n_fft 256 (12-wave blocks: 6 waves per SIMD, <= 80 VGPRs)
+__attribute__((amdgpu_waves_per_eu(NC == 128 && C == 1 ? 6 : 1)))
 stftq_kernel(StftLaunch a, uint64_t fps) {
     constexpr int OKQ = KIND == OUT_COMPLEX ? 0 : (KIND == OUT_MEL || KIND == OUT_MEL_AMP_DB) ? 2 : 1;
     using G = GeoQ<NC>;
@@ -291,7 +366,7 @@ stftq_kernel(StftLaunch a, uint64_t fps) {
             wcl[l * G::WL_STRIDE + 2 * n + (i & 1)] = __uint_as_float(i >= a.pad_left && i < a.pad_left + a.win ? ~0u : 0u);
     }
     for (int i = threadIdx.x; i < NC; i += kBlock) {
-        twl[i] = a.tw1[i];
+        twl[tpad(i)] = a.tw1[i];
         scl[i] = a.sincos[i];
     }
     if (threadIdx.x == 0) scl[NC] = make_float2(0.f, 0.f);
@@ -303,6 +378,10 @@ stftq_kernel(StftLaunch a, uint64_t fps) {
     const uint64_t g1 = g0 + fps < total ? g0 + fps : total;
     const int hop = a.hop;
     float* region = work + (wave * FPW + slot) * G::RS;
+    const uint32_t rbase = (uint32_t)(region - lds) * 4u;  // 128-byte aligned (GeoQ)
+    // the staged row's start in the region: 16 floats further in the odd slots of a 16-lane layout,
+    // so the two slots of a 32-lane ds_write_b32 fall on disjoint banks (RS is 0 mod 32)
+    float* const srow = region + ((L == 16 && (slot & 1)) ? 16 : 0);
     const ET* in = static_cast<const ET*>(a.in);
     const float2 w8a = make_float2(a.xw8[0], a.xw8[1]), w8b = make_float2(a.xw8[2], a.xw8[3]);
 
@@ -433,21 +512,22 @@ stftq_kernel(StftLaunch a, uint64_t fps) {
                     qswap<q.swx[s], q.swy[s], P>(v, lj);
                 });
             } else if constexpr (q.nsw > 0) {
-                float2* zb = reinterpret_cast<float2*>(region);
                 wave_lds_sync();  // the region's previous readers are done
                 {
-                    float2* wb = zb + relayout_pad(lane_mbits<NC, t, false>(lj));
+                    const uint32_t wb = rbase + 8u * (uint32_t)lane_swz_m<NC, t, false>(lj);
                     static_for<0, P>([&](auto rc) {
                         constexpr int r = decltype(rc)::value;
-                        wb[relayout_pad(reg_mbits<NC, t, false>(r))] = v[r];
+                        constexpr int f = swzq<NC, false>(reg_mbits<NC, t, false>(r));
+                        ldsw2(lds, (wb ^ (8u * (f & 15))) + 8u * (f & ~15), v[r]);
                     });
                 }
                 wave_lds_sync();
                 {
-                    const float2* rb = zb + relayout_pad(lane_mbits<NC, t, true>(lj));
+                    const uint32_t rb = rbase + 8u * (uint32_t)lane_swz_m<NC, t, true>(lj);
                     static_for<0, P>([&](auto rc) {
                         constexpr int r = decltype(rc)::value;
-                        v[r] = rb[relayout_pad(reg_mbits<NC, t, true>(r))];
+                        constexpr int f = swzq<NC, false>(reg_mbits<NC, t, true>(r));
+                        v[r] = ldsr2(lds, (rb ^ (8u * (f & 15))) + 8u * (f & ~15));
                     });
                 }
             }
@@ -477,27 +557,33 @@ stftq_kernel(StftLaunch a, uint64_t fps) {
                         } else {
                             constexpr int jr = reg_pbits<NC, t>(base_r, q.pstart);
                             const int j = jl + jr;
-                            rbfly(v[r0], v[r1], v[r2], v[r3], twl[j * tstride], twl[2 * j * tstride],
-                                  twl[3 * j * tstride]);
+                            rbfly(v[r0], v[r1], v[r2], v[r3], twl[tpad(j * tstride)], twl[tpad(2 * j * tstride)],
+                                  twl[tpad(3 * j * tstride)]);
                         }
                     }
                 }
             });
         });
-        // ---- Z[p] to the region in natural order ----
+        // ---- Z[p] to the region (bin p at its swizzled place) ----
         wave_lds_sync();  // (the fallback loads' reads of the region are done)
         {
             constexpr int T = G::NLEV - 1;
-            float2* zr = reinterpret_cast<float2*>(region) + lane_pbits<NC, T, false>(lj, 99);
+            const uint32_t zb = rbase + 8u * (uint32_t)lane_swz_p<NC>(lj);
             static_for<0, P>([&](auto rc) {
                 constexpr int r = decltype(rc)::value;
-                constexpr int pr = reg_pbits<NC, T>(r, 99);
-                zr[pr] = v[r];
+                constexpr int f = swzq<NC, true>(reg_pbits<NC, T>(r, 99));
+                ldsw2(lds, (zb ^ (8u * (f & 15))) + 8u * (f & ~15), v[r]);
             });
         }
         wave_lds_sync();
         // ---- untangle (realfft.rs:142-157, stftx's expression): pairs (k, NC - k), k = lj + L i ----
-        const float2* zc = reinterpret_cast<const float2*>(region);
+        // Z[k] at swz(lj) ^ swz(L i) (disjoint bits); Z[NC - k] = Z[c_i + (L - lj)], c_i = NC -
+        // L (i + 1), at swz(L - lj) ^ swz(c_i) for lanes >= 1; lane 0's partner NC - L i carries
+        // into c_i's bits, so its base is L and its constant swz(c_i + L) (a per-lane select), and
+        // at i = 0 its partner is bin 0 itself, the Z[k] it just read
+        const bool l0 = lj == 0;
+        const uint32_t kb = rbase + 8u * (uint32_t)swzq_small<NC, true>(lj);
+        const uint32_t pb = rbase + 8u * (uint32_t)(l0 ? L : swzq_small<NC, true>(L - lj));
         auto bin = [&](float2 b, float2 r, float2 sc) {
             const float s = sc.x, c = sc.y;
             const float xr = 0.5f * (((b.x + r.x) + c * (b.y + r.y)) - s * (b.x - r.x));
@@ -521,11 +607,15 @@ stftq_kernel(StftLaunch a, uint64_t fps) {
         constexpr int NP = P / 2;
         float2 xo[OKQ == 0 ? 2 * NP + 1 : 1];
         float fo[OKQ == 0 ? 1 : 2 * NP + 1];
-#pragma unroll
-        for (int i = 0; i < ((VAR & 4) ? 0 : NP); ++i) {
+        static_for<0, ((VAR & 4) ? 0 : NP)>([&](auto ic) {
+            constexpr int i = decltype(ic)::value;
+            constexpr int fk = swzq<NC, true>(L * i);
+            constexpr int cp = NC - L * (i + 1);
+            constexpr uint32_t xp = 8u * (swzq<NC, true>(cp) & 15), xp0 = 8u * (swzq<NC, true>(cp + L) & 15);
             const int k = lj + L * i;
-            const int kp = (NC - k) & (NC - 1);
-            const float2 zk = zc[k], zp = zc[kp];
+            const float2 zk = ldsr2(lds, (kb ^ (8u * (fk & 15))) + 8u * (fk & ~15));
+            float2 zp = ldsr2(lds, (pb ^ (l0 ? xp0 : xp)) + 8u * cp);
+            if constexpr (i == 0) zp = l0 ? zk : zp;  // lane 0's bin 0 pairs with itself (NC - 0 = 0 mod NC)
             const float2 xk = bin(zk, zp, scl[k]);
             float2 xkp = bin(zp, zk, scl[NC - k]);
             if (i == 0 && lj == 0) xkp = make_float2(zk.x - zk.y, 0.0f);  // realfft.rs:157 (bin NC)
@@ -539,9 +629,9 @@ stftq_kernel(StftLaunch a, uint64_t fps) {
                 fo[2 * i] = exact::hypotf_cr(xk.x, xk.y);
                 fo[2 * i + 1] = exact::hypotf_cr(xkp.x, xkp.y);
             }
-        }
+        });
         {  // bin NC / 2 pairs with itself (lane 0 keeps it)
-            const float2 zh = zc[NC / 2];
+            const float2 zh = ldsr2(lds, rbase + 8u * swzq<NC, true>(NC / 2));
             const float2 xh = bin(zh, zh, scl[NC / 2]);
             if constexpr (OKQ == 0) xo[2 * NP] = xh;
             else if constexpr (OKQ == 1) fo[2 * NP] = value(xh);
@@ -572,7 +662,7 @@ stftq_kernel(StftLaunch a, uint64_t fps) {
             constexpr int nfl = OKQ == 0 ? 2 * F : F;
             float* frow = static_cast<float*>(a.out) + g * (uint64_t)nfl;
             const int sh = (int)((reinterpret_cast<uintptr_t>(frow) >> 2) & 3);
-            float* st = region + sh;
+            float* st = srow + sh;
             // (RG) this frame's values in this lane: every bin is in some lane's fo, bin NC / 2 in all
             float f_max = -INFINITY, f_min = INFINITY;
             int f_nan = 0;
@@ -608,7 +698,7 @@ stftq_kernel(StftLaunch a, uint64_t fps) {
                 }
             }
             wave_lds_sync();
-            if (valid) store_row_b128<L>(frow, sh, region, nfl, lj);
+            if (valid) store_row_b128<L>(frow, sh, srow, nfl, lj);
             wave_lds_sync();
             if constexpr (RG && OKQ == 1) {  // the slot's track changed: commit the previous one's
                 const int t = valid ? hint : -1;
