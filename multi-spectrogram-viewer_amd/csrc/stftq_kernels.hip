@@ -19,7 +19,9 @@
 //   256   16 x 16   r4(6,7), r4(4,5), r4(2,3), r4(0,1)    2 before each of the last two
 //   512   32 x 16   b8(6-8), r4(4,5), r4(2,3), r4(0,1)    1 (permlane16), 2, 2
 //
-// Then Z[p] goes to the frame's LDS region in natural order, each lane untangles the pairs
+// (The swaps other than permlane16 run as one LDS round trip of the frame's points, at
+// bank-conflict-free swizzled places: SwzQ below.) Then Z[p] goes to the frame's LDS region (bin p
+// at its swizzled place), each lane untangles the pairs
 // (k, NC - k), k = l + L i (realfft.rs:142-157 as stftx), and the row leaves through the region
 // as aligned 16-byte stores (|X| by the correctly rounded hypot, dB by glibc's log10f; mel as the
 // k-ascending fma chain over each filter's band, as stftx).
@@ -212,17 +214,13 @@ constexpr int reg_mbits(int r) {
     }
     return m;
 }
-// LDS slot of point m: one float2 of padding per 16 (the lane bits of a later level's layout
-// are m's higher bits: unpadded, a store or load of 16 lanes would hit one bank group).
-// Separable: pad(ml | mr) = pad(ml) + pad(mr) for disjoint bits.
-__host__ __device__ constexpr int relayout_pad(int m) { return m + (m >> 4); }
-
 // LDS swizzles (round 6). The frame's points sit in its region at index
 // x ^ G(x >> 4) (float2 units): a GF(2)-linear map of the index's bits >= 4 onto its bits 0-3,
 // one 4-bit image per bit (REL: the relayouts' point index m; Z: the Z row's bin p). The images
 // (scratch search over the rule) make every relayout's write (ds_write_b64: 16-lane groups,
 // banks mod 32) and read (ds_read_b64: 32-lane groups, banks mod 64, two 16-lane frame slots RS
-// apart) and the Z row's write conflict-free; relayout_pad's padding left them 2-8-way. Linear:
+// apart) and the Z row's write conflict-free (round 5's one-float2-per-16 padding left them
+// 2-8-way; no integer padding can serve n_fft 256's three layouts at once). Linear:
 // swz(a ^ b) = swz(a) ^ swz(b) for disjoint bits, so an access is a per-lane byte base (128-byte
 // aligned region + 8 swz(lane part)) XOR a compile-time constant (8 x the register part's bits
 // 0-3) plus an immediate offset (its bits >= 4).
