@@ -124,6 +124,15 @@ int MultiTrack::add_tracks(const std::vector<uint64_t>& ids, const std::vector<P
     };
     std::vector<Group> groups;
     std::vector<std::unique_ptr<DevBuf>> big_raws;  // uploads of calls beyond kStageKeep
+    // per-track (max, min, NaN) of the new rows (lib.rs:197-200), left by the spectrogram launches
+    // themselves (Batch::range: folded into kernel 7's amp-dB epilogue, one pass over the rows for
+    // the other kinds), 3 int32 per track in group order
+    DevBuf rng;
+    {
+        const int rc = rng.alloc(std::max<size_t>(nt.size(), 1) * 3 * sizeof(int));
+        if (rc) return rc;
+    }
+    size_t t_rng = 0;
     for (auto& [sr, idx] : by_sr) {
         Plan* plan = nullptr;
         auto pit = plans_.find(sr);
@@ -198,6 +207,8 @@ int MultiTrack::add_tracks(const std::vector<uint64_t>& ids, const std::vector<P
         // contract relative to the reference's own f32 error (tests/test_gpu_parity.py
         // _check_multitrack)
         rc = batch_set_option(b, THESIA_BATCH_OPT_KERNEL, fast_ ? 0 : b->kr_ok ? 7 : 9);
+        if (!rc) rc = batch_set_option(b, THESIA_BATCH_OPT_RANGE, (int64_t)(uintptr_t)(rng.as<int>() + 3 * t_rng));
+        t_rng += idx.size();
         if (!rc) rc = batch_run(b, s);
         if (rc) return rc;
         g.spec = spec->as<float>();
@@ -217,21 +228,11 @@ int MultiTrack::add_tracks(const std::vector<uint64_t>& ids, const std::vector<P
         if (e != hipSuccess) return set_error(THESIA_ERR_DEVICE, hipGetErrorString(e));
     }
     // 3) per-track max / min (lib.rs:197-200; a NaN makes ndarray-stats return Err -> +-inf):
-    //    one launch over every group
+    //    the ranges the launches left, one readback
     {
-        std::vector<const float*> specs;
-        std::vector<const uint64_t*> row0s;
-        std::vector<size_t> bins, ns;
-        for (const Group& g : groups) {
-            specs.push_back(g.spec);
-            row0s.push_back(g.batch->frame0.data());
-            bins.push_back(g.bins);
-            ns.push_back(g.idx.size());
-        }
         std::vector<float> mx(nt.size()), mn(nt.size());
         std::vector<int> nan(nt.size());
-        int rc = minmax_segments_multi(groups.size(), specs.data(), row0s.data(), bins.data(), ns.data(),
-                                       mx.data(), mn.data(), nan.data(), s);
+        int rc = ranges_read(rng.as<int>(), nt.size(), mx.data(), mn.data(), nan.data(), s);
         if (rc) return rc;
         size_t t = 0;
         for (const Group& g : groups)
