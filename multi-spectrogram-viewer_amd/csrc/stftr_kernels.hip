@@ -508,7 +508,9 @@ static int launchr_c(const StftLaunch& a, hipStream_t s) {
         case OUT_MAG: return launchr_w<OUT_MAG, C, INF, DIR>(a, s);
         case OUT_POWER: return launchr_w<OUT_POWER, C, INF, DIR>(a, s);
         case OUT_AMP_DB:  // (the range folded in when the batch asks for it: the C5 / viewer kind)
-            return a.trk_range ? launchr_k<OUT_AMP_DB, C, INF, 12, 0, DIR, true>(a, s)
+            // (16-wave blocks -- 4 waves per SIMD -- where the fold fits 128 VGPRs without spills
+            // and the LDS: mono int16 at the canonical geometry, the C5 rows; 12 elsewhere)
+            return a.trk_range ? launchr_k<OUT_AMP_DB, C, INF, (C == 1 && INF == IN_S16 && !DIR) ? 16 : 12, 0, DIR, true>(a, s)
                                : launchr_w<OUT_AMP_DB, C, INF, DIR>(a, s);
         case OUT_POWER_DB: return launchr_w<OUT_POWER_DB, C, INF, DIR>(a, s);
         case OUT_MEL: return launchr_w<OUT_MEL, C, INF, DIR>(a, s);
