@@ -110,19 +110,22 @@ THESIA_HD inline float log10f_normal_tab(float x, const LogfEntry* tab) {
     const int32_t i0 = (int32_t)(((uint32_t)k0 & 0x80000000u) >> 31);
     const uint32_t ix = (uint32_t)((hx & 0x007fffff) | ((0x7f - i0) << 23));  // x' in [1, 2) or [0.5, 1)
     const float y = (float)(k0 + i0);
-    // logf(x') (optimized-routines logf.c)
+    // logf(x') (optimized-routines logf.c) in the contracted form glibc's x86-64 FMA variant of
+    // logf computes (five fma instead of five products and five sums): the float it rounds to
+    // equals the unfused form's and glibc's on every positive normal float (exhaustive host check,
+    // round 6: 0 mismatches in 2 130 706 432; tests/test_exact_math.py re-checks every 3rd)
     const uint32_t tmp = ix - 0x3f330000u;
     const int i = (int)((tmp >> (23 - 4)) % 16);
     const int k = (int32_t)tmp >> 23;
     const uint32_t iz = ix - (tmp & (0x1ffu << 23));
     const double invc = tab[i].invc, logc = tab[i].logc;
     const double z = (double)bits_f32(iz);
-    const double r = z * invc - 1.0;
-    const double y0 = logc + (double)k * Ln2;
+    const double r = __builtin_fma(z, invc, -1.0);
+    const double y0 = __builtin_fma((double)k, Ln2, logc);
     const double r2 = r * r;
-    double q = A1 * r + A2;
-    q = A0 * r2 + q;
-    q = q * r2 + (y0 + r);
+    double q = __builtin_fma(A1, r, A2);
+    q = __builtin_fma(A0, r2, q);
+    q = __builtin_fma(q, r2, y0 + r);
     const float lx = (float)q;
     const float zz = y * log10_2lo + ivln10 * lx;
     const float res = zz + y * log10_2hi;
