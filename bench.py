@@ -465,10 +465,14 @@ def profile_record(params):
 
 
 def provenance(rec):
-    return {"profile": "profiles/" + rec.get("profile", "?"), "date": rec.get("date"), "box": rec.get("box"),
-            "measured_in_this_run": False,
-            "note": "stored rocprofv3 PMC counts of the same workload from a builder box "
-                    "(profiles/pmc_traffic.json), not measured by this run"}
+    out = {"profile": "profiles/" + rec.get("profile", "?"), "date": rec.get("date"), "box": rec.get("box"),
+           "measured_in_this_run": False,
+           "note": "stored rocprofv3 PMC counts of the same workload from a builder box "
+                   "(profiles/pmc_traffic.json), not measured by this run"}
+    latest = rec.get("reconfirmed_round6")
+    if latest:  # the latest re-measurement of the same counters on the current kernels
+        out["reconfirmed"] = {"profile": "profiles/" + latest.get("profile", "?"), "note": latest.get("note")}
+    return out
 
 
 # VALU issue ceiling (MI355X_MICROARCH.md constants table): a wave64 v_fma_f32 occupies its
